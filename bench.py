@@ -1,0 +1,195 @@
+"""Benchmark of the Lanczos H·v hot path (BASELINE.json metric:
+"Lanczos SpMV GB/s + ground-state iters/s, Ns=16 half-filled sector, 1/2/4/8 GPU").
+
+Workload (configs[1]): Norb=1, Nbath=7 (reference Nlevels=16), half-filled
+sector (nup,ndw)=(4,4), dim 4,900, stored H in real(8), synthetic random bath
+(seeded per rank).  One step = one device-resident plain-Lanczos run of
+`--niter` iterations (lanc_niter=512 by default) from a fixed start vector.
+value = Lanczos iterations/s summed over all ranks (weak scaling: every rank
+runs its own sector replica; sectors are independent, no collective in the
+data path).
+
+Also reported (rank 0):
+  * spmv_gbs: stored SpMV GB/s on the c2 sector (algorithmic bytes, L2-resident);
+  * roofline: stored SpMV on the Nlevels=28 (7,7) sector (dim 11,778,624,
+    nnz 176,679,360, real(8)) — the only size where HBM is the bound
+     — timed with HIP events on the launch stream;
+  * cpu_baseline: the oracle's row-gather CSR SpMV + plain recurrence
+    (restated reference algorithm), 1 host core, bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (ROOT, os.path.join(ROOT, "dmft-ed_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def spmv_bytes_real(nnz, dim):
+    """Algorithmic bytes of one real(8) stored SpMV: 12 nnz + 8 (dim+1) + 16 dim."""
+    return 12 * nnz + 8 * (dim + 1) + 16 * dim
+
+
+def time_kernel(fn, iters, stream):
+    """Average device time (ms) of fn() over iters launches, HIP events on `stream`."""
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(iters):
+        fn()
+    e1.record(stream)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def measure_spmv(Sector, cfg, q, iters, warm=5):
+    with Sector(cfg, q[0], q[1], stored=True, direct=False, real=True) as S:
+        dim, nnz = S.dim, S.nnz
+        x = torch.sin(torch.arange(1, dim + 1, dtype=torch.float64, device="cuda")).contiguous()
+        y = torch.empty_like(x)
+        st = torch.cuda.current_stream()
+        for _ in range(warm):
+            S.hxv_dev(x, y, path=0, stream=st)
+        ms = time_kernel(lambda: S.hxv_dev(x, y, path=0, stream=st), iters, st)
+        return dim, nnz, ms
+
+
+def cpu_baseline(budget_s=10.0):
+    """Oracle (restated reference loops) on 1 host core: plain Lanczos iters/s on c2."""
+    from edgpu.params import make_config
+    from oracle.oracle import Oracle, lanc_tridiag, start_vector
+
+    cfg = make_config(Norb=1, Nbath=7, bath="random", seed=20251015)
+    orc = Oracle(cfg)
+    hmap = orc.build_sector(4, 4)
+    csr = orc.build_csr(hmap)
+    v0 = start_vector(len(hmap))
+    n = 200
+    t0 = time.perf_counter()
+    runs = 0
+    while time.perf_counter() - t0 < budget_s:
+        lanc_tridiag(csr, v0, n, threshold=0.0)
+        runs += 1
+    dt = time.perf_counter() - t0
+    return {"value": runs * n / dt, "unit": "Lanczos iters/s", "cores": 1, "kind": "port",
+            "sample": f"{runs} x {n}-step plain-Lanczos runs (complex(8), row-gather CSR, "
+                      f"c2 (4,4) sector, random bath) in {dt:.1f}s on 1 core"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--niter", type=int, default=512)
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.cuda.current_device()
+
+    from edgpu.hamiltonian import Sector
+    from edgpu.params import make_config
+
+    cfg = make_config(Norb=1, Nbath=7, bath="random", seed=20251015 + rank)
+    S = Sector(cfg, 4, 4, stored=True, direct=False, real=True, device=dev)
+    v0 = torch.sin(torch.arange(1, S.dim + 1, dtype=torch.float64, device="cuda"))
+
+    def step():
+        return S.lanc_run(args.niter, v0_dev=v0)
+
+    for _ in range(args.warmup):
+        step()
+
+    def barrier():
+        if dist:
+            tdist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    dev_ms = 0.0
+    for _ in range(args.steps):
+        _, _, ms = step()
+        dev_ms += ms
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        dt = float(t.item())
+    iters_total = args.steps * args.niter * world
+    value = iters_total / dt
+
+    out = None
+    if rank == 0:
+        # SpMV GB/s on the headline sector (L2-resident; launch-latency bound)
+        dim2, nnz2, ms2 = measure_spmv(Sector, cfg, (4, 4), 2000)
+        gbs2 = spmv_bytes_real(nnz2, dim2) / (ms2 * 1e-3) / 1e9
+        roof = None
+        if not args.no_roofline:
+            cfg28 = make_config(Norb=1, Nbath=13, bath="random", seed=20251015)
+            dim28, nnz28, ms28 = measure_spmv(Sector, cfg28, (7, 7), 50)
+            B = spmv_bytes_real(nnz28, dim28)
+            ach = B / (ms28 * 1e-3) / 1e9
+            roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                    "kernel": "k_spmv<real,real> (stored SELL-64 H·v)",
+                    "workload": f"Nlevels=28 Norb=1 Nbath=13 (7,7) sector, dim {dim28}, nnz {nnz28}, "
+                                f"real(8), {B} algorithmic bytes/launch",
+                    "ms_per_launch": round(ms28, 4)}
+        cpu = None if args.no_cpu else cpu_baseline()
+        out = {
+            "metric": "Lanczos SpMV GB/s + ground-state iters/s, Ns=16 half-filled sector, 1/2/4/8 GPU",
+            "value": round(value, 1),
+            "unit": "Lanczos iters/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded random bath per rank)",
+            "config": {"workload": "c2: Norb=1 Nbath=7 (Nlevels=16) half-filled (4,4) sector, dim 4900, "
+                                   f"stored real(8) H, plain Lanczos {args.niter} iters/step",
+                       "parallelism": f"sector replicas x{world}"},
+            "device_ms_per_step": round(dev_ms / args.steps, 4),
+            "spmv_gbs_c2": round(gbs2, 1),
+            "spmv_ms_c2": round(ms2, 5),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    S.close()
+    if dist:
+        tdist.barrier()
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,559 @@
+// ed_kernels.hpp — HIP kernels of the H·v hot path for gfx950 (CDNA4).
+//
+// Kernels (one thread per basis row, 256-thread blocks = 4 wavefronts,
+// grid-strided over whole 64-row slices so that a wavefront is exactly one
+// SELL slice):
+//   k_build_map    H%map from the (off, rank) tables        build_sector ED_SETUP.f90:886-984
+//   k_count        elements per row + SELL-64 slice width   ed_buildH_c pass 1
+//   k_fill         SELL-64 fill, reference row order        ed_buildH_c + sp_insert_element
+//   k_spmv         stored H·v, SELL-64                      spMatVec_cc STORED_HxV.f90:132-143
+//   k_direct       matrix-free H·v (gather, any ed_mode)     directMatVec_cc DIRECT_HxV.f90:21-92
+//   k_kron         matrix-free H·v, normal mode without Jx/Jp: H = D + Hup(x)1 + 1(x)Hdw
+//   k_lanc_*       device-resident plain Lanczos recurrence .repo/PLAIN_LANCZOS.f90:87-118
+//
+// The three H·v kernels share one epilogue interface, so the Lanczos update
+// (w = Hv - b*v_prev, alpha = <v,w>) is fused into the H·v pass and the
+// partial dot products are combined in-kernel by the last block to finish
+// (deterministic fixed-order sum, agent-scope release/acquire per
+// cdna_hip_programming.md Guideline 16).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "ed_model.hpp"
+
+namespace edg {
+
+constexpr int kBlock = 256;  // 4 wavefronts of 64
+
+// ------------------------------------------------------------------ values
+template <bool C> using val_t = typename std::conditional<C, double2, double>::type;
+
+__device__ __forceinline__ double mkval(double re, double, std::false_type) { return re; }
+__device__ __forceinline__ double2 mkval(double re, double im, std::true_type) { return make_double2(re, im); }
+template <bool C> __device__ __forceinline__ val_t<C> mk(double re, double im) {
+  return mkval(re, im, std::integral_constant<bool, C>());
+}
+
+__device__ __forceinline__ double mul(double h, double x) { return h * x; }
+__device__ __forceinline__ double2 mul(double h, double2 x) { return make_double2(h * x.x, h * x.y); }
+__device__ __forceinline__ double2 mul(double2 h, double2 x) {
+  return make_double2(h.x * x.x - h.y * x.y, h.x * x.y + h.y * x.x);
+}
+__device__ __forceinline__ double add(double a, double b) { return a + b; }
+__device__ __forceinline__ double2 add(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ double sub(double a, double b) { return a - b; }
+__device__ __forceinline__ double2 sub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ double scl(double s, double a) { return s * a; }
+__device__ __forceinline__ double2 scl(double s, double2 a) { return make_double2(s * a.x, s * a.y); }
+// Re(conj(a)*b): dot_product real part
+__device__ __forceinline__ double redot(double a, double b) { return a * b; }
+__device__ __forceinline__ double redot(double2 a, double2 b) { return a.x * b.x + a.y * b.y; }
+template <class V> __device__ __forceinline__ V vzero();
+template <> __device__ __forceinline__ double vzero<double>() { return 0.0; }
+template <> __device__ __forceinline__ double2 vzero<double2>() { return make_double2(0.0, 0.0); }
+
+// -------------------------------------------------------------- reductions
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+  return v;
+}
+// Deterministic block sum; result valid in every thread.
+__device__ __forceinline__ double block_sum(double v) {
+  __shared__ double ws[kBlock / 64];
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double t = 0.0;
+#pragma unroll
+  for (int w = 0; w < kBlock / 64; w++) t = t + ws[w];
+  return t;
+}
+
+struct RedSlot {
+  double* partials;       // [gridDim.x]
+  unsigned int* counter;  // zero on entry; reset by the last block
+};
+
+// Block-partial sum -> partials; the last block to arrive (atomic ticket)
+// returns true with the full sum in *total (fixed order: independent of
+// arrival order).
+__device__ __forceinline__ bool grid_reduce_last(double v, RedSlot slot, double* total) {
+  __shared__ int amlast;
+  double s = block_sum(v);
+  if (threadIdx.x == 0) {
+    slot.partials[blockIdx.x] = s;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned int t = atomicAdd(slot.counter, 1u);
+    amlast = (t == gridDim.x - 1);
+  }
+  __syncthreads();
+  if (!amlast) return false;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  double a = 0.0;
+  for (unsigned int b = threadIdx.x; b < gridDim.x; b += kBlock) a = a + slot.partials[b];
+  *total = block_sum(a);
+  if (threadIdx.x == 0) *slot.counter = 0u;
+  return true;
+}
+
+// ---------------------------------------------------------------- indexing
+struct DevIndex {
+  const int32_t* off;
+  const uint32_t* rank;
+  int ns;
+  uint32_t mask;
+  __device__ __forceinline__ int32_t operator()(uint32_t k) const {
+    return off[k >> ns] + (int32_t)rank[k & mask];
+  }
+};
+
+// ------------------------------------------------------------- basis / map
+__global__ void __launch_bounds__(kBlock) k_build_map(const int64_t* __restrict__ blk_off,
+                                                      const uint32_t* __restrict__ blk_idw, int nblk,
+                                                      const int32_t* __restrict__ need_nup,
+                                                      const uint32_t* __restrict__ by_pc,
+                                                      const int32_t* __restrict__ pc_start, int ns,
+                                                      int64_t dim, uint32_t* __restrict__ map) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < dim;
+       i += (int64_t)gridDim.x * kBlock) {
+    int lo = 0, hi = nblk;  // blk_off[lo] <= i < blk_off[hi]
+    while (hi - lo > 1) {
+      int mid = (lo + hi) >> 1;
+      if (blk_off[mid] <= i) lo = mid;
+      else hi = mid;
+    }
+    uint32_t idw = blk_idw[lo];
+    int nup = need_nup[idw];
+    uint32_t iup = by_pc[pc_start[nup] + (i - blk_off[lo])];
+    map[i] = iup | (idw << ns);
+  }
+}
+
+// ------------------------------------------------------------ stored build
+struct CountAcc {
+  int n = 0;
+  __device__ __forceinline__ void diag(double, double) {}
+  __device__ __forceinline__ void off(uint32_t, double, double) { n++; }
+};
+
+// cnt[i] = off-diagonal elements of row i; width[s] = max over slice s.
+__global__ void __launch_bounds__(kBlock) k_count(const EdModel* __restrict__ Mp,
+                                                  const uint32_t* __restrict__ map, int64_t dim,
+                                                  int64_t nslice, uint16_t* __restrict__ cnt,
+                                                  int32_t* __restrict__ width) {
+  const EdModel& M = *Mp;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nslice * 64;
+       i += (int64_t)gridDim.x * kBlock) {
+    int c = 0;
+    if (i < dim) {
+      CountAcc a;
+      gen_row(M, map[i], a);
+      c = a.n;
+      cnt[i] = (uint16_t)c;
+    }
+    int w = wave_max(c);
+    if ((threadIdx.x & 63) == 0) width[i >> 6] = w;
+  }
+}
+
+// Exclusive scan of 64*width -> sptr (int64), three-pass.
+__global__ void __launch_bounds__(1024) k_scan_blocks(const int32_t* __restrict__ width, int64_t n,
+                                                      int64_t* __restrict__ out,
+                                                      int64_t* __restrict__ bsum) {
+  __shared__ int64_t s[1024];
+  int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x;
+  int64_t x = (i < n) ? 64 * (int64_t)width[i] : 0;
+  s[threadIdx.x] = x;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    int64_t t = (threadIdx.x >= (unsigned)o) ? s[threadIdx.x - o] : 0;
+    __syncthreads();
+    s[threadIdx.x] += t;
+    __syncthreads();
+  }
+  if (i < n) out[i] = s[threadIdx.x] - x;  // exclusive within block
+  if (threadIdx.x == 1023) bsum[blockIdx.x] = s[1023];
+}
+__global__ void k_scan_spine(int64_t* __restrict__ bsum, int64_t nb, int64_t* __restrict__ total) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    int64_t acc = 0;
+    for (int64_t b = 0; b < nb; b++) {
+      int64_t t = bsum[b];
+      bsum[b] = acc;
+      acc += t;
+    }
+    *total = acc;
+  }
+}
+__global__ void __launch_bounds__(1024) k_scan_add(int64_t* __restrict__ out, int64_t n,
+                                                   const int64_t* __restrict__ bsum,
+                                                   const int64_t* __restrict__ total) {
+  int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x;
+  if (i < n) out[i] += bsum[blockIdx.x];
+  if (i == 0) out[n] = *total;
+}
+
+template <bool HC>
+struct FillAcc {
+  using H = val_t<HC>;
+  int64_t base;
+  int k = 0;
+  DevIndex idx;
+  int32_t* cols;
+  H* vals;
+  H dv;
+  __device__ __forceinline__ void diag(double re, double im) { dv = mk<HC>(re, im); }
+  __device__ __forceinline__ void off(uint32_t kst, double re, double im) {
+    int64_t q = base + 64 * (int64_t)k;
+    cols[q] = idx(kst);
+    vals[q] = mk<HC>(re, im);
+    k++;
+  }
+};
+
+template <bool HC>
+__global__ void __launch_bounds__(kBlock) k_fill(const EdModel* __restrict__ Mp,
+                                                 const uint32_t* __restrict__ map, int64_t dim,
+                                                 DevIndex idx, const int64_t* __restrict__ sptr,
+                                                 val_t<HC>* __restrict__ diag,
+                                                 int32_t* __restrict__ cols,
+                                                 val_t<HC>* __restrict__ vals) {
+  const EdModel& M = *Mp;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < dim;
+       i += (int64_t)gridDim.x * kBlock) {
+    int64_t s = i >> 6;
+    FillAcc<HC> a;
+    a.base = sptr[s] + (i & 63);
+    a.idx = idx;
+    a.cols = cols;
+    a.vals = vals;
+    gen_row(M, map[i], a);
+    diag[i] = a.dv;
+    int w = (int)((sptr[s + 1] - sptr[s]) >> 6);
+    for (int k = a.k; k < w; k++) {  // padding: own column, zero value
+      int64_t q = a.base + 64 * (int64_t)k;
+      cols[q] = (int32_t)i;
+      vals[q] = mk<HC>(0.0, 0.0);
+    }
+  }
+}
+
+// --------------------------------------------------------------- epilogues
+// row(i, acc, xi) receives (H x)_i and x_i; returns the row's contribution to
+// the fused reduction.  finish(part) runs once per thread after the loop.
+template <bool VC>
+struct EpiStore {
+  using V = val_t<VC>;
+  V* hv;
+  __device__ __forceinline__ bool skip() const { return false; }
+  __device__ __forceinline__ void prepare() {}
+  __device__ __forceinline__ double row(int64_t i, V acc, V) {
+    hv[i] = acc;
+    return 0.0;
+  }
+  __device__ __forceinline__ void finish(double) {}
+};
+
+// Device scalars of one Lanczos run.
+struct LancState {
+  double beta;    // b of the previous iteration (normalisation of R)
+  double invb;    // 1/b
+  double alpha;   // a of the current iteration
+  double thresh;  // breakdown threshold
+  double tmp;
+  int iter;       // iterations completed
+  int done;       // breakdown reached
+  int pad[2];
+};
+
+// Lanczos step, part A (fused into the H·v kernel).  Input R = unnormalised
+// r_k (b_k = st->beta), P = v_{k-1}.  Per row: v = R*invb, w = (H R)*invb - b*P,
+// P <- v, W <- w; alpha_k = sum Re(conj(v) w).  .repo/PLAIN_LANCZOS.f90:105-114
+template <bool VC>
+struct EpiLancA {
+  using V = val_t<VC>;
+  LancState* st;
+  V* P;
+  V* W;
+  V* basis;      // optional: Krylov basis, column k at basis + k*dim
+  int64_t dim;
+  double* alpha_out;
+  RedSlot slot;
+  double invb, b;
+  V* bcol;
+  __device__ __forceinline__ bool skip() const { return st->done != 0; }
+  __device__ __forceinline__ void prepare() {
+    invb = st->invb;
+    b = st->beta;
+    bcol = basis ? basis + (int64_t)st->iter * dim : nullptr;
+  }
+  __device__ __forceinline__ double row(int64_t i, V acc, V xi) {
+    V v = scl(invb, xi);
+    V h = scl(invb, acc);
+    V w = sub(h, scl(b, P[i]));
+    P[i] = v;
+    W[i] = w;
+    if (bcol) bcol[i] = v;
+    return redot(v, w);
+  }
+  __device__ __forceinline__ void finish(double part) {
+    double tot;
+    if (grid_reduce_last(part, slot, &tot) && threadIdx.x == 0) {
+      st->alpha = tot;
+      alpha_out[st->iter] = tot;
+    }
+  }
+};
+
+// ------------------------------------------------------------- stored H·v
+template <bool HC, bool VC, class Epi>
+__global__ void __launch_bounds__(kBlock) k_spmv(const val_t<HC>* __restrict__ diag,
+                                                 const int64_t* __restrict__ sptr,
+                                                 const int32_t* __restrict__ cols,
+                                                 const val_t<HC>* __restrict__ vals,
+                                                 const val_t<VC>* __restrict__ x, int64_t dim,
+                                                 int64_t nslice, Epi epi) {
+  using V = val_t<VC>;
+  if (epi.skip()) return;
+  epi.prepare();
+  double part = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nslice * 64;
+       i += (int64_t)gridDim.x * kBlock) {
+    if (i < dim) {
+      const int64_t s = i >> 6;
+      const int64_t s0 = sptr[s];
+      const int w = (int)((sptr[s + 1] - s0) >> 6);
+      const int64_t base = s0 + (i & 63);
+      const V xi = x[i];
+      // spMatVec_cc: Hv=0; Hv(i)=Hv(i)+vals(j)*v(cols(j)), diagonal first
+      V acc = add(vzero<V>(), mul(diag[i], xi));
+#pragma unroll 4
+      for (int k = 0; k < w; k++) {
+        const int64_t q = base + 64 * (int64_t)k;
+        acc = add(acc, mul(vals[q], x[cols[q]]));
+      }
+      part += epi.row(i, acc, xi);
+    }
+  }
+  epi.finish(part);
+}
+
+// ---------------------------------------------------- matrix-free (generic)
+template <bool HC, bool VC>
+struct GatherAcc {
+  using V = val_t<VC>;
+  const V* x;
+  DevIndex idx;
+  int64_t i;
+  V acc, xi;
+  __device__ __forceinline__ void diag(double re, double im) {
+    xi = x[i];
+    acc = add(vzero<V>(), mul(mk<HC>(re, im), xi));
+  }
+  __device__ __forceinline__ void off(uint32_t kst, double re, double im) {
+    acc = add(acc, mul(mk<HC>(re, im), x[idx(kst)]));
+  }
+};
+
+template <bool HC, bool VC, class Epi>
+__global__ void __launch_bounds__(kBlock) k_direct(const EdModel* __restrict__ Mp,
+                                                   const uint32_t* __restrict__ map, DevIndex idx,
+                                                   const val_t<VC>* __restrict__ x, int64_t dim,
+                                                   int64_t nslice, Epi epi) {
+  if (epi.skip()) return;
+  epi.prepare();
+  const EdModel& M = *Mp;
+  double part = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nslice * 64;
+       i += (int64_t)gridDim.x * kBlock) {
+    if (i < dim) {
+      GatherAcc<HC, VC> g;
+      g.x = x;
+      g.idx = idx;
+      g.i = i;
+      gen_row(M, map[i], g);
+      part += epi.row(i, g.acc, g.xi);
+    }
+  }
+  epi.finish(part);
+}
+
+// ------------------------------------------- matrix-free (Kronecker form)
+// Normal mode without spin-exchange/pair-hopping: every off-diagonal term
+// moves one spin species only, and the Jordan-Wigner string of a down-spin
+// hop crosses all up bits twice (sign cancels).  With v viewed as the
+// DimDw x DimUp matrix V (row = rank(idw), column = rank(iup), exactly the
+// reference order), H v = D.V + V Hup^T + Hdw V.  Hup/Hdw are tiny ELL
+// tables (column-major [k][row]), D = Aup[iu] + Adw[iw] + U[imp(iu)][imp(iw)].
+template <bool HC>
+struct KronArgs {
+  using H = val_t<HC>;
+  int64_t dimup, dimdw;
+  int degup, degdw, nimp;
+  const int32_t* upc;
+  const H* upv;
+  const int32_t* dwc;
+  const H* dwv;
+  const H* aup;
+  const H* adw;
+  const double* uimp;    // [nimp*nimp]
+  const uint8_t* impu;   // [dimup]
+  const uint8_t* impd;   // [dimdw]
+};
+
+template <bool HC, bool VC, class Epi>
+__global__ void __launch_bounds__(kBlock) k_kron(KronArgs<HC> K, const val_t<VC>* __restrict__ x,
+                                                 int64_t dim, int64_t nslice, Epi epi) {
+  using V = val_t<VC>;
+  if (epi.skip()) return;
+  epi.prepare();
+  double part = 0.0;
+  const int64_t du = K.dimup;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nslice * 64;
+       i += (int64_t)gridDim.x * kBlock) {
+    if (i < dim) {
+      const int64_t iw = i / du;
+      const int64_t iu = i - iw * du;
+      const V xi = x[i];
+      auto d = add(add(K.aup[iu], K.adw[iw]), mk<HC>(K.uimp[K.impu[iu] * K.nimp + K.impd[iw]], 0.0));
+      V acc = mul(d, xi);
+      const V* xrow = x + iw * du;
+      for (int k = 0; k < K.degup; k++) {
+        const int64_t q = (int64_t)k * du + iu;
+        acc = add(acc, mul(K.upv[q], xrow[K.upc[q]]));
+      }
+      for (int k = 0; k < K.degdw; k++) {
+        const int64_t q = (int64_t)k * K.dimdw + iw;
+        acc = add(acc, mul(K.dwv[q], x[(int64_t)K.dwc[q] * du + iu]));
+      }
+      part += epi.row(i, acc, xi);
+    }
+  }
+  epi.finish(part);
+}
+
+// ------------------------------------------------------------ Lanczos misc
+// Start: R holds v0.  P <- 0; b_1 = ||R|| -> st.  (iteration 1 normalises, :96-101)
+template <bool VC>
+__global__ void __launch_bounds__(kBlock) k_lanc_init(const val_t<VC>* __restrict__ R,
+                                                      val_t<VC>* __restrict__ P, int64_t dim,
+                                                      LancState* st, double thresh,
+                                                      RedSlot slot) {
+  using V = val_t<VC>;
+  double part = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < dim;
+       i += (int64_t)gridDim.x * kBlock) {
+    V r = R[i];
+    part += redot(r, r);
+    P[i] = vzero<V>();
+  }
+  double tot;
+  if (grid_reduce_last(part, slot, &tot) && threadIdx.x == 0) {
+    double b = sqrt(tot);
+    st->beta = b;
+    st->invb = 1.0 / b;
+    st->alpha = 0.0;
+    st->thresh = thresh;
+    st->iter = 0;
+    st->done = (b == 0.0) ? 1 : 0;
+  }
+}
+
+// Lanczos step, part B: w = W - alpha*v (v = P), R <- w, b = ||w||.  (:111-113)
+template <bool VC>
+__global__ void __launch_bounds__(kBlock) k_lanc_b(const val_t<VC>* __restrict__ W,
+                                                   const val_t<VC>* __restrict__ P,
+                                                   val_t<VC>* __restrict__ R, int64_t dim,
+                                                   LancState* st, double* beta_out,
+                                                   RedSlot slot) {
+  using V = val_t<VC>;
+  if (st->done) return;
+  const double a = st->alpha;
+  double part = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < dim;
+       i += (int64_t)gridDim.x * kBlock) {
+    V w = sub(W[i], scl(a, P[i]));
+    R[i] = w;
+    part += redot(w, w);
+  }
+  double tot;
+  if (grid_reduce_last(part, slot, &tot) && threadIdx.x == 0) {
+    double b = sqrt(tot);
+    int it = st->iter;
+    beta_out[it + 1] = b;
+    st->beta = b;
+    st->invb = 1.0 / b;
+    st->iter = it + 1;
+    if (b < st->thresh) st->done = 1;
+  }
+}
+
+// Ritz vector from the stored Krylov basis: y = sum_k z_k v_k; st->tmp = ||y||.
+template <bool VC>
+__global__ void __launch_bounds__(kBlock) k_ritz(const val_t<VC>* __restrict__ basis,
+                                                 const double* __restrict__ z, int n,
+                                                 int64_t dim, val_t<VC>* __restrict__ y,
+                                                 LancState* st, RedSlot slot) {
+  using V = val_t<VC>;
+  double part = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < dim;
+       i += (int64_t)gridDim.x * kBlock) {
+    V acc = vzero<V>();
+    for (int k = 0; k < n; k++) acc = add(acc, scl(z[k], basis[(int64_t)k * dim + i]));
+    y[i] = acc;
+    part += redot(acc, acc);
+  }
+  double tot;
+  if (grid_reduce_last(part, slot, &tot) && threadIdx.x == 0) st->tmp = sqrt(tot);
+}
+
+// y += z * P (second-pass Ritz accumulation when the basis is not kept)
+template <bool VC>
+__global__ void __launch_bounds__(kBlock) k_axpy_p(const val_t<VC>* __restrict__ P,
+                                                   const double* __restrict__ z, int k,
+                                                   int64_t dim, val_t<VC>* __restrict__ y) {
+  const double c = z[k];
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < dim;
+       i += (int64_t)gridDim.x * kBlock)
+    y[i] = add(y[i], scl(c, P[i]));
+}
+
+template <bool VC>
+__global__ void __launch_bounds__(kBlock) k_norm(const val_t<VC>* __restrict__ y, int64_t dim,
+                                                 LancState* st, RedSlot slot) {
+  double part = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < dim;
+       i += (int64_t)gridDim.x * kBlock)
+    part += redot(y[i], y[i]);
+  double tot;
+  if (grid_reduce_last(part, slot, &tot) && threadIdx.x == 0) st->tmp = sqrt(tot);
+}
+
+template <bool VC>
+__global__ void __launch_bounds__(kBlock) k_scale_tmp(val_t<VC>* __restrict__ y, int64_t dim,
+                                                      const LancState* st) {
+  const double n = st->tmp;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < dim;
+       i += (int64_t)gridDim.x * kBlock) {
+    auto v = y[i];
+    if constexpr (VC) y[i] = make_double2(v.x / n, v.y / n);
+    else y[i] = v / n;
+  }
+}
+
+}  // namespace edg

@@ -1,0 +1,1022 @@
+// ed_lib.hip — the C-ABI of include/ed_gpu.h on top of ed_kernels.hpp.
+//
+// Sector object = what the reference keeps in module state between
+// build_Hv_sector and delete_Hv_sector (ED_HAMILTONIAN_SHARED.f90:32-34,
+// ED_VARS_GLOBAL.f90:104-105): the basis H%map, the stored H spH0 (here a
+// device SELL-64 matrix) or the matrix-free kernel's tables, plus the
+// device-resident Lanczos workspace.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "ed_kernels.hpp"
+#include "ed_tables.hpp"
+
+using namespace edg;
+
+// ------------------------------------------------------------------ errors
+static thread_local std::string g_err;
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define HIPCK(x)                                                                       \
+  do {                                                                                 \
+    hipError_t e_ = (x);                                                               \
+    if (e_ != hipSuccess)                                                              \
+      return fail(ED_ERR_HIP, std::string(#x) + " -> " + hipGetErrorString(e_));       \
+  } while (0)
+#define CK(x)                  \
+  do {                         \
+    int r_ = (x);              \
+    if (r_ != ED_OK) return r_; \
+  } while (0)
+
+static constexpr int kMaxGrid = 8192;
+static inline int grid_for(int64_t nthreads) {
+  int64_t b = (nthreads + kBlock - 1) / kBlock;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(b, kMaxGrid));
+}
+
+// -------------------------------------------------------------- sector obj
+struct KronHost {
+  int64_t dimup = 0, dimdw = 0;
+  int degup = 0, degdw = 0, nimp = 0;
+  int32_t *upc = nullptr, *dwc = nullptr;
+  void *upv = nullptr, *dwv = nullptr, *aup = nullptr, *adw = nullptr;
+  double* uimp = nullptr;
+  uint8_t *impu = nullptr, *impd = nullptr;
+};
+
+struct LancWS {
+  int vc = -1;
+  int cap = 0;                  // alpha/beta capacity
+  void *R = nullptr, *P = nullptr, *W = nullptr, *Y = nullptr;
+  LancState* st = nullptr;
+  double* partials = nullptr;   // [kMaxGrid]
+  unsigned int* counter = nullptr;
+  double *alpha = nullptr, *beta = nullptr, *z = nullptr;
+  void* basis = nullptr;
+  int basis_cols = 0;
+};
+
+struct ed_sector {
+  int device = 0;
+  hipStream_t stream = nullptr;  // private stream for synchronous entry points
+  EdModel Mh;
+  EdModel* Md = nullptr;
+  SectorTables T;
+  int flags = 0;
+  bool hc = true;      // complex H values
+  int64_t dim = 0, nslice = 0;
+  int32_t* d_off = nullptr;
+  uint32_t* d_rank = nullptr;
+  uint32_t* d_map = nullptr;
+  // stored (SELL-64)
+  void* d_diag = nullptr;
+  int64_t* d_sptr = nullptr;
+  int32_t* d_cols = nullptr;
+  void* d_vals = nullptr;
+  uint16_t* d_cnt = nullptr;
+  int64_t nnz = 0, padded = 0;
+  // matrix-free
+  bool kron = false;
+  KronHost K;
+  // host-pointer H·v staging
+  void *d_x = nullptr, *d_y = nullptr;
+  LancWS ws;
+  int64_t bytes = 0;
+  std::vector<void*> allocs;
+  // graph cache for Lanczos iterations
+  hipGraphExec_t gexec = nullptr;
+  int g_path = -2, g_vc = -1, g_chunk = 0;
+  bool g_basis = false;
+};
+
+static int dalloc(ed_sector* s, void** p, size_t n) {
+  if (n == 0) n = 16;
+  hipError_t e = hipMalloc(p, n);
+  if (e != hipSuccess) {
+    *p = nullptr;
+    return fail(e == hipErrorOutOfMemory ? ED_ERR_OOM : ED_ERR_HIP,
+                std::string("hipMalloc(") + std::to_string(n) + ") -> " + hipGetErrorString(e));
+  }
+  s->allocs.push_back(*p);
+  s->bytes += (int64_t)n;
+  return ED_OK;
+}
+template <class T>
+static int dalloc_t(ed_sector* s, T** p, size_t count) {
+  return dalloc(s, (void**)p, count * sizeof(T));
+}
+template <class T>
+static int upload(ed_sector* s, T** p, const std::vector<T>& h) {
+  CK(dalloc_t(s, p, h.size()));
+  HIPCK(hipMemcpy(*p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+  return ED_OK;
+}
+
+static void sector_free(ed_sector* s) {
+  if (!s) return;
+  hipSetDevice(s->device);
+  if (s->gexec) hipGraphExecDestroy(s->gexec);
+  for (void* p : s->allocs) hipFree(p);
+  if (s->stream) hipStreamDestroy(s->stream);
+  delete s;
+}
+
+// ---------------------------------------------------------- stored build
+static int build_stored(ed_sector* s) {
+  const int64_t dim = s->dim, ns = s->nslice;
+  uint16_t* cnt;
+  int32_t* width;
+  int64_t* bsum;
+  int64_t* total;
+  CK(dalloc_t(s, &cnt, dim));
+  s->d_cnt = cnt;
+  // width/bsum/total are scratch, freed right after the build
+  HIPCK(hipMalloc((void**)&width, ns * sizeof(int32_t)));
+  int64_t nb = (ns + 1023) / 1024;
+  HIPCK(hipMalloc((void**)&bsum, std::max<int64_t>(nb, 1) * sizeof(int64_t)));
+  HIPCK(hipMalloc((void**)&total, sizeof(int64_t)));
+  CK(dalloc_t(s, &s->d_sptr, ns + 1));
+  hipLaunchKernelGGL(k_count, dim3(grid_for(ns * 64)), dim3(kBlock), 0, s->stream, s->Md, s->d_map,
+                     dim, ns, cnt, width);
+  HIPCK(hipGetLastError());
+  hipLaunchKernelGGL(k_scan_blocks, dim3((unsigned)nb), dim3(1024), 0, s->stream, width, ns,
+                     s->d_sptr, bsum);
+  hipLaunchKernelGGL(k_scan_spine, dim3(1), dim3(64), 0, s->stream, bsum, nb, total);
+  hipLaunchKernelGGL(k_scan_add, dim3((unsigned)nb), dim3(1024), 0, s->stream, s->d_sptr, ns,
+                     bsum, total);
+  HIPCK(hipGetLastError());
+  int64_t slots = 0;
+  HIPCK(hipMemcpyAsync(&slots, total, sizeof(int64_t), hipMemcpyDeviceToHost, s->stream));
+  HIPCK(hipStreamSynchronize(s->stream));
+  hipFree(width);
+  hipFree(bsum);
+  hipFree(total);
+  s->padded = slots;
+  const size_t hv = s->hc ? 16 : 8;
+  CK(dalloc(s, &s->d_diag, dim * hv));
+  CK(dalloc_t(s, &s->d_cols, slots));
+  CK(dalloc(s, &s->d_vals, slots * hv));
+  DevIndex idx{s->d_off, s->d_rank, s->T.ns, s->T.nst - 1};
+  if (s->hc)
+    hipLaunchKernelGGL(k_fill<true>, dim3(grid_for(dim)), dim3(kBlock), 0, s->stream, s->Md,
+                       s->d_map, dim, idx, s->d_sptr, (double2*)s->d_diag, s->d_cols,
+                       (double2*)s->d_vals);
+  else
+    hipLaunchKernelGGL(k_fill<false>, dim3(grid_for(dim)), dim3(kBlock), 0, s->stream, s->Md,
+                       s->d_map, dim, idx, s->d_sptr, (double*)s->d_diag, s->d_cols,
+                       (double*)s->d_vals);
+  HIPCK(hipGetLastError());
+  // nnz = dim (diagonal) + sum(cnt)
+  std::vector<uint16_t> hc(dim);
+  HIPCK(hipMemcpyAsync(hc.data(), cnt, dim * sizeof(uint16_t), hipMemcpyDeviceToHost, s->stream));
+  HIPCK(hipStreamSynchronize(s->stream));
+  int64_t nnz = dim;
+  for (int64_t i = 0; i < dim; i++) nnz += hc[i];
+  s->nnz = nnz;
+  return ED_OK;
+}
+
+// ---------------------------------------------------- Kronecker (normal)
+struct HopAcc {
+  std::vector<uint32_t> tgt;
+  std::vector<double> re, im;
+  void diag(double, double) {}
+  void off(uint32_t k, double r, double i) {
+    tgt.push_back(k);
+    re.push_back(r);
+    im.push_back(i);
+  }
+};
+
+// Separable one-body diagonal of one spin species (Himp diag + Hbath diag).
+static void spin_diag(const EdModel& M, int sp, uint32_t x, double* re, double* im) {
+  const int ss = sp == 0 ? 0 : M.S;
+  double r = 0.0, i = 0.0;
+  for (int o = 0; o < M.norb; o++) {
+    double n = (double)bit(x, o);
+    r = r + M.hloc_re[ss][ss][o][o] * n;
+    i = i + M.hloc_im[ss][ss][o][o] * n;
+    r = r - M.xmu * n;
+  }
+  if (M.bath != ED_BATH_REPLICA) {
+    for (int o = 0; o < M.ne; o++)
+      for (int k = 0; k < M.nbath; k++) r = r + M.e[ss][o][k] * (double)bit(x, M.stride[o][k]);
+  } else {
+    for (int k = 0; k < M.nbath; k++)
+      for (int o = 0; o < M.norb; o++) {
+        double n = (double)bit(x, M.stride[o][k]);
+        r = r + M.hb_re[ss][ss][o][o][k] * n;
+        i = i + M.hb_im[ss][ss][o][o][k] * n;
+      }
+  }
+  *re = r;
+  *im = i;
+}
+
+static int build_kron(ed_sector* s) {
+  const SectorTables& T = s->T;
+  const EdModel& M = s->Mh;
+  KronHost& K = s->K;
+  const int nup = T.q1, ndw = T.q2;
+  K.dimup = T.dimup;
+  K.dimdw = T.dimdw;
+  K.nimp = 1 << M.norb;
+  const uint32_t mask = T.nst - 1;
+  const uint32_t* ups = &T.by_pc[T.pc_start[nup]];
+  const uint32_t* dws = &T.by_pc[T.pc_start[ndw]];
+  const size_t hv = s->hc ? 16 : 8;
+  for (int sp = 0; sp < 2; sp++) {
+    const int64_t nr = sp == 0 ? K.dimup : K.dimdw;
+    const uint32_t* st = sp == 0 ? ups : dws;
+    std::vector<HopAcc> rows(nr);
+    int deg = 0;
+    for (int64_t r = 0; r < nr; r++) {
+      uint32_t m = sp == 0 ? st[r] : (st[r] << M.ns);
+      gen_row(M, m, rows[r]);
+      deg = std::max<int>(deg, (int)rows[r].tgt.size());
+    }
+    std::vector<int32_t> cols((size_t)deg * nr);
+    std::vector<double> vals((size_t)deg * nr * (s->hc ? 2 : 1), 0.0);
+    for (int64_t r = 0; r < nr; r++)
+      for (int k = 0; k < deg; k++) {
+        size_t q = (size_t)k * nr + r;
+        if (k < (int)rows[r].tgt.size()) {
+          uint32_t t = rows[r].tgt[k];
+          uint32_t loc = sp == 0 ? t : (t >> M.ns);
+          if ((sp == 0 && (t >> M.ns) != 0) || (sp == 1 && (t & mask) != 0))
+            return fail(ED_ERR_STATE, "kron: hop mixes spin species");
+          cols[q] = (int32_t)T.rank[loc];
+          if (s->hc) {
+            vals[2 * q] = rows[r].re[k];
+            vals[2 * q + 1] = rows[r].im[k];
+          } else {
+            vals[q] = rows[r].re[k];
+          }
+        } else {
+          cols[q] = (int32_t)r;  // padding: own column, zero value
+        }
+      }
+    std::vector<double> a(nr * (s->hc ? 2 : 1));
+    std::vector<uint8_t> imp(nr);
+    for (int64_t r = 0; r < nr; r++) {
+      double re, im;
+      spin_diag(M, sp, st[r], &re, &im);
+      if (s->hc) {
+        a[2 * r] = re;
+        a[2 * r + 1] = im;
+      } else {
+        a[r] = re;
+      }
+      imp[r] = (uint8_t)(st[r] & (uint32_t)(K.nimp - 1));
+    }
+    int32_t* dc;
+    void *dv, *da;
+    uint8_t* di;
+    CK(upload(s, &dc, cols));
+    CK(dalloc(s, &dv, vals.size() * 8));
+    HIPCK(hipMemcpy(dv, vals.data(), vals.size() * 8, hipMemcpyHostToDevice));
+    CK(dalloc(s, &da, a.size() * 8));
+    HIPCK(hipMemcpy(da, a.data(), a.size() * 8, hipMemcpyHostToDevice));
+    CK(upload(s, &di, imp));
+    if (sp == 0) {
+      K.degup = deg; K.upc = dc; K.upv = dv; K.aup = da; K.impu = di;
+    } else {
+      K.degdw = deg; K.dwc = dc; K.dwv = dv; K.adw = da; K.impd = di;
+    }
+    (void)hv;
+  }
+  std::vector<double> u((size_t)K.nimp * K.nimp);
+  for (int x = 0; x < K.nimp; x++)
+    for (int y = 0; y < K.nimp; y++) u[(size_t)x * K.nimp + y] = hint_value(M, (uint32_t)x, (uint32_t)y);
+  CK(upload(s, &K.uimp, u));
+  return ED_OK;
+}
+
+template <bool HC>
+static KronArgs<HC> kron_args(const ed_sector* s) {
+  using H = val_t<HC>;
+  KronArgs<HC> a;
+  a.dimup = s->K.dimup; a.dimdw = s->K.dimdw; a.degup = s->K.degup; a.degdw = s->K.degdw;
+  a.nimp = s->K.nimp;
+  a.upc = s->K.upc; a.upv = (const H*)s->K.upv; a.dwc = s->K.dwc; a.dwv = (const H*)s->K.dwv;
+  a.aup = (const H*)s->K.aup; a.adw = (const H*)s->K.adw; a.uimp = s->K.uimp;
+  a.impu = s->K.impu; a.impd = s->K.impd;
+  return a;
+}
+
+// ------------------------------------------------------------ H·v launch
+// path: 0 = stored SELL, 1 = direct generic, 2 = direct Kronecker, -1 = default
+static int resolve_path(const ed_sector* s, int path) {
+  if (path == -1) {
+    if (s->flags & ED_STORED) return 0;
+    return s->kron ? 2 : 1;
+  }
+  if (path == 0 && !(s->flags & ED_STORED)) return -1;
+  if (path == 2 && !s->kron) return -1;
+  if (path < 0 || path > 2) return -1;
+  return path;
+}
+
+template <bool HC, bool VC, class Epi>
+static int launch_hxv_t(ed_sector* s, int path, const void* x, Epi epi, hipStream_t st) {
+  using V = val_t<VC>;
+  const int64_t dim = s->dim, ns = s->nslice;
+  const int g = grid_for(ns * 64);
+  if (path == 0) {
+    hipLaunchKernelGGL((k_spmv<HC, VC, Epi>), dim3(g), dim3(kBlock), 0, st,
+                       (const val_t<HC>*)s->d_diag, s->d_sptr, s->d_cols,
+                       (const val_t<HC>*)s->d_vals, (const V*)x, dim, ns, epi);
+  } else if (path == 1) {
+    DevIndex idx{s->d_off, s->d_rank, s->T.ns, s->T.nst - 1};
+    hipLaunchKernelGGL((k_direct<HC, VC, Epi>), dim3(g), dim3(kBlock), 0, st, s->Md, s->d_map, idx,
+                       (const V*)x, dim, ns, epi);
+  } else {
+    hipLaunchKernelGGL((k_kron<HC, VC, Epi>), dim3(g), dim3(kBlock), 0, st, kron_args<HC>(s),
+                       (const V*)x, dim, ns, epi);
+  }
+  HIPCK(hipGetLastError());
+  return ED_OK;
+}
+
+template <bool VC, class Epi>
+static int launch_hxv(ed_sector* s, int path, const void* x, Epi epi, hipStream_t st) {
+  if (s->hc) {
+    if constexpr (VC) return launch_hxv_t<true, true>(s, path, x, epi, st);
+    return fail(ED_ERR_ARG, "complex Hamiltonian needs complex vectors (vtype=1)");
+  }
+  return launch_hxv_t<false, VC>(s, path, x, epi, st);
+}
+
+// ------------------------------------------------------------ Lanczos
+static int lanc_prepare(ed_sector* s, int vc, int cap, bool want_basis, int basis_cols) {
+  LancWS& w = s->ws;
+  const size_t vs = vc ? 16 : 8;
+  if (w.vc != vc) {
+    if (w.vc != -1) return fail(ED_ERR_STATE, "Lanczos workspace already bound to another vtype");
+    CK(dalloc(s, &w.R, s->dim * vs));
+    CK(dalloc(s, &w.P, s->dim * vs));
+    CK(dalloc(s, &w.W, s->dim * vs));
+    CK(dalloc(s, &w.Y, s->dim * vs));
+    CK(dalloc_t(s, &w.st, 1));
+    CK(dalloc_t(s, &w.partials, kMaxGrid));
+    CK(dalloc_t(s, &w.counter, 4));
+    HIPCK(hipMemset(w.counter, 0, 4 * sizeof(unsigned int)));
+    w.vc = vc;
+  }
+  if (cap > w.cap) {
+    CK(dalloc_t(s, &w.alpha, cap + 2));
+    CK(dalloc_t(s, &w.beta, cap + 2));
+    CK(dalloc_t(s, &w.z, cap + 2));
+    w.cap = cap;
+  }
+  if (want_basis && basis_cols > w.basis_cols) {
+    CK(dalloc(s, &w.basis, (size_t)basis_cols * s->dim * vs));
+    w.basis_cols = basis_cols;
+  }
+  return ED_OK;
+}
+
+// splitmix64 hash start vector in [-1,1) (documented in DESIGN.md; tests reproduce it)
+__global__ void k_default_start(double* v, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kBlock) {
+    uint64_t z = (uint64_t)(i + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z = z ^ (z >> 31);
+    v[i] = (double)(z >> 11) * (1.0 / 9007199254740992.0) * 2.0 - 1.0;
+  }
+}
+
+template <bool VC>
+static int lanc_start(ed_sector* s, double thresh, hipStream_t st) {
+  LancWS& w = s->ws;
+  RedSlot slot{w.partials, w.counter};
+  HIPCK(hipMemsetAsync(w.beta, 0, (w.cap + 2) * sizeof(double), st));
+  HIPCK(hipMemsetAsync(w.alpha, 0, (w.cap + 2) * sizeof(double), st));
+  hipLaunchKernelGGL(k_lanc_init<VC>, dim3(grid_for(s->dim)), dim3(kBlock), 0, st,
+                     (const val_t<VC>*)w.R, (val_t<VC>*)w.P, s->dim, w.st, thresh, slot);
+  HIPCK(hipGetLastError());
+  return ED_OK;
+}
+
+template <bool VC>
+static int lanc_iter(ed_sector* s, int path, bool basis, hipStream_t st) {
+  LancWS& w = s->ws;
+  EpiLancA<VC> e;
+  e.st = w.st;
+  e.P = (val_t<VC>*)w.P;
+  e.W = (val_t<VC>*)w.W;
+  e.basis = basis ? (val_t<VC>*)w.basis : nullptr;
+  e.dim = s->dim;
+  e.alpha_out = w.alpha;
+  e.slot = RedSlot{w.partials, w.counter};
+  CK(launch_hxv<VC>(s, path, w.R, e, st));
+  RedSlot slot2{w.partials, w.counter + 1};
+  hipLaunchKernelGGL(k_lanc_b<VC>, dim3(grid_for(s->dim)), dim3(kBlock), 0, st,
+                     (const val_t<VC>*)w.W, (const val_t<VC>*)w.P, (val_t<VC>*)w.R, s->dim, w.st,
+                     w.beta, slot2);
+  HIPCK(hipGetLastError());
+  return ED_OK;
+}
+
+// Run n iterations on stream st; graph-captured in chunks when st is the
+// sector's private stream (launch-bound small sectors).
+template <bool VC>
+static int lanc_iters(ed_sector* s, int path, bool basis, int n, hipStream_t st) {
+  const int chunk = 32;
+  if (st != s->stream || n < chunk) {
+    for (int k = 0; k < n; k++) CK((lanc_iter<VC>(s, path, basis, st)));
+    return ED_OK;
+  }
+  if (!s->gexec || s->g_path != path || s->g_vc != (int)VC || s->g_basis != basis ||
+      s->g_chunk != chunk) {
+    if (s->gexec) {
+      hipGraphExecDestroy(s->gexec);
+      s->gexec = nullptr;
+    }
+    hipGraph_t g;
+    HIPCK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+    int rc = ED_OK;
+    for (int k = 0; k < chunk && rc == ED_OK; k++) rc = lanc_iter<VC>(s, path, basis, st);
+    hipError_t e2 = hipStreamEndCapture(st, &g);
+    if (rc != ED_OK) return rc;
+    HIPCK(e2);
+    HIPCK(hipGraphInstantiate(&s->gexec, g, nullptr, nullptr, 0));
+    hipGraphDestroy(g);
+    s->g_path = path;
+    s->g_vc = VC;
+    s->g_basis = basis;
+    s->g_chunk = chunk;
+  }
+  int k = 0;
+  for (; k + chunk <= n; k += chunk) HIPCK(hipGraphLaunch(s->gexec, st));
+  for (; k < n; k++) CK((lanc_iter<VC>(s, path, basis, st)));
+  return ED_OK;
+}
+
+// Host tridiagonal eigen-solver (tql2, EISPACK; the same algorithm the
+// reference uses for Ritz values, .repo/PLAIN_LANCZOS.f90:427-565).
+static double pythag(double a, double b) {
+  double p = std::max(fabs(a), fabs(b));
+  if (p != 0.0) {
+    double r = std::min(fabs(a), fabs(b)) / p;
+    r = r * r;
+    for (;;) {
+      double t = 4.0 + r;
+      if (t == 4.0) break;
+      double s = r / t, u = 1.0 + 2.0 * s;
+      p = u * p;
+      double su = s / u;
+      r = (su * su) * r;
+    }
+  }
+  return p;
+}
+// d[n] diag, e[n] with e[0] ignored (e[i] couples i-1,i); z column-major n x n or null.
+static int tql2(int n, double* d, double* e, double* z) {
+  if (n == 1) return 0;
+  for (int i = 1; i < n; i++) e[i - 1] = e[i];
+  e[n - 1] = 0.0;
+  double f = 0.0, tst1 = 0.0;
+  for (int l = 0; l < n; l++) {
+    int j = 0;
+    tst1 = std::max(tst1, fabs(d[l]) + fabs(e[l]));
+    int m = l;
+    for (; m < n; m++)
+      if (tst1 + fabs(e[m]) == tst1) break;
+    if (m != l) {
+      for (;;) {
+        if (j >= 30) return l + 1;
+        j++;
+        int l1 = l + 1, l2 = l1 + 1;
+        double g = d[l];
+        double p = (d[l1] - g) / (2.0 * e[l]);
+        double r = pythag(p, 1.0);
+        double sr = p >= 0.0 ? fabs(r) : -fabs(r);
+        d[l] = e[l] / (p + sr);
+        d[l1] = e[l] * (p + sr);
+        double dl1 = d[l1];
+        double h = g - d[l];
+        for (int i = l2; i < n; i++) d[i] -= h;
+        f += h;
+        p = d[m];
+        double c = 1.0, c2 = c, c3 = c, el1 = e[l1], s = 0.0, s2 = 0.0;
+        for (int i = m - 1; i >= l; i--) {
+          c3 = c2;
+          c2 = c;
+          s2 = s;
+          g = c * e[i];
+          h = c * p;
+          r = pythag(p, e[i]);
+          e[i + 1] = s * r;
+          s = e[i] / r;
+          c = p / r;
+          p = c * d[i] - s * g;
+          d[i + 1] = h + s * (c * g + s * d[i]);
+          if (z)
+            for (int k = 0; k < n; k++) {
+              h = z[k + (size_t)n * (i + 1)];
+              z[k + (size_t)n * (i + 1)] = s * z[k + (size_t)n * i] + c * h;
+              z[k + (size_t)n * i] = c * z[k + (size_t)n * i] - s * h;
+            }
+        }
+        p = -s * s2 * c3 * el1 * e[l] / dl1;
+        e[l] = s * p;
+        d[l] = c * p;
+        if (!(tst1 + fabs(e[l]) > tst1)) break;
+      }
+    }
+    d[l] += f;
+  }
+  for (int ii = 1; ii < n; ii++) {
+    int i = ii - 1, k = i;
+    double p = d[i];
+    for (int jj = ii; jj < n; jj++)
+      if (d[jj] < p) { k = jj; p = d[jj]; }
+    if (k != i) {
+      d[k] = d[i];
+      d[i] = p;
+      if (z)
+        for (int jj = 0; jj < n; jj++) std::swap(z[jj + (size_t)n * i], z[jj + (size_t)n * k]);
+    }
+  }
+  return 0;
+}
+
+static double lowest_ritz(const std::vector<double>& a, const std::vector<double>& b, int n) {
+  std::vector<double> d(a.begin(), a.begin() + n), e(n, 0.0);
+  for (int q = 1; q < n; q++) e[q] = b[q];
+  tql2(n, d.data(), e.data(), nullptr);
+  return d[0];
+}
+
+// ---------------------------------------------------------------- C-ABI
+extern "C" {
+
+const char* ed_gpu_last_error(void) { return g_err.c_str(); }
+
+int ed_sector_create(const ed_params* p, int32_t q1, int32_t q2, int32_t flags, int32_t device,
+                     void* stream, ed_sector** out) {
+  (void)stream;
+  if (!out) return fail(ED_ERR_ARG, "out == NULL");
+  *out = nullptr;
+  if (!(flags & (ED_STORED | ED_DIRECT))) return fail(ED_ERR_ARG, "flags need ED_STORED or ED_DIRECT");
+  int ndev = 0;
+  HIPCK(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(ED_ERR_ARG, "bad device ordinal");
+  HIPCK(hipSetDevice(device));
+  ed_sector* s = new ed_sector();
+  s->device = device;
+  int rc = model_from_params(p, &s->Mh);
+  if (rc != ED_OK) {
+    delete s;
+    return fail(rc, "invalid ed_params (Norb/Nspin/Nbath/ed_mode/bath_type)");
+  }
+  const bool real_ok = model_is_real(s->Mh);
+  if ((flags & ED_REAL) && !real_ok) {
+    delete s;
+    return fail(ED_ERR_ARG, "ED_REAL requested but impHloc/bath carry imaginary parts");
+  }
+  s->hc = !(flags & ED_REAL);
+  s->flags = flags;
+  rc = build_tables(s->Mh.ns, s->Mh.mode, q1, s->Mh.mode == ED_MODE_NORMAL ? q2 : 0, &s->T);
+  if (rc != ED_OK) {
+    delete s;
+    return fail(rc, "sector tables: bad quantum numbers or dimension beyond int32");
+  }
+  if (s->T.dim == 0) {
+    delete s;
+    return fail(ED_ERR_ARG, "empty sector");
+  }
+  s->dim = s->T.dim;
+  s->nslice = (s->dim + 63) / 64;
+#define TRY(x)            \
+  do {                    \
+    int r2_ = (x);        \
+    if (r2_ != ED_OK) {   \
+      sector_free(s);     \
+      return r2_;         \
+    }                     \
+  } while (0)
+  hipError_t he = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+  if (he != hipSuccess) {
+    delete s;
+    return fail(ED_ERR_HIP, "hipStreamCreate");
+  }
+  TRY(dalloc_t(s, &s->Md, 1));
+  if (hipMemcpy(s->Md, &s->Mh, sizeof(EdModel), hipMemcpyHostToDevice) != hipSuccess) {
+    sector_free(s);
+    return fail(ED_ERR_HIP, "model upload");
+  }
+  TRY(upload(s, &s->d_off, s->T.off));
+  TRY(upload(s, &s->d_rank, s->T.rank));
+  {
+    int64_t* bo;
+    uint32_t *bi, *bp;
+    int32_t *nn, *ps;
+    TRY(upload(s, &bo, s->T.blk_off));
+    TRY(upload(s, &bi, s->T.blk_idw));
+    TRY(upload(s, &nn, s->T.need_nup));
+    TRY(upload(s, &bp, s->T.by_pc));
+    TRY(upload(s, &ps, s->T.pc_start));
+    TRY(dalloc_t(s, &s->d_map, s->dim));
+    hipLaunchKernelGGL(k_build_map, dim3(grid_for(s->dim)), dim3(kBlock), 0, s->stream, bo, bi,
+                       (int)s->T.blk_idw.size(), nn, bp, ps, s->T.ns, s->dim, s->d_map);
+    if (hipGetLastError() != hipSuccess) {
+      sector_free(s);
+      return fail(ED_ERR_HIP, "k_build_map launch");
+    }
+  }
+  // Kronecker form: normal mode without Jx/Jp terms (no term moves both spins)
+  s->kron = (flags & ED_DIRECT) && s->Mh.mode == ED_MODE_NORMAL && !s->Mh.jhflag;
+  if (flags & ED_STORED) TRY(build_stored(s));
+  if (s->kron) TRY(build_kron(s));
+  if (hipStreamSynchronize(s->stream) != hipSuccess) {
+    sector_free(s);
+    return fail(ED_ERR_HIP, "sector build");
+  }
+#undef TRY
+  *out = s;
+  return ED_OK;
+}
+
+int ed_sector_destroy(ed_sector* s) {
+  sector_free(s);
+  return ED_OK;
+}
+
+int ed_sector_get_info(const ed_sector* s, ed_sector_info* info) {
+  if (!s || !info) return fail(ED_ERR_ARG, "null");
+  memset(info, 0, sizeof(*info));
+  info->dim = s->dim;
+  info->nnz = (s->flags & ED_STORED) ? s->nnz : 0;
+  info->padded = s->padded;
+  info->ns = s->Mh.ns;
+  info->mode = s->Mh.mode;
+  info->q1 = s->T.q1;
+  info->q2 = s->T.q2;
+  info->flags = s->flags;
+  info->kron = s->kron ? 1 : 0;
+  info->dimup = s->T.dimup;
+  info->dimdw = s->T.dimdw;
+  info->device_bytes = s->bytes;
+  return ED_OK;
+}
+
+int ed_sector_hxv_dev_path(ed_sector* s, int32_t path, int32_t vtype, const void* v, void* hv,
+                           void* stream) {
+  if (!s || !v || !hv) return fail(ED_ERR_ARG, "null");
+  int pth = resolve_path(s, path);
+  if (pth < 0) return fail(ED_ERR_ARG, "H·v path not available for this sector");
+  HIPCK(hipSetDevice(s->device));
+  hipStream_t st = (hipStream_t)stream;
+  if (vtype == 1) {
+    EpiStore<true> e{(double2*)hv};
+    return launch_hxv<true>(s, pth, v, e, st);
+  }
+  if (vtype == 0) {
+    EpiStore<false> e{(double*)hv};
+    return launch_hxv<false>(s, pth, v, e, st);
+  }
+  return fail(ED_ERR_ARG, "vtype must be 0 (real) or 1 (complex)");
+}
+
+int ed_sector_hxv_dev(ed_sector* s, int32_t vtype, const void* v, void* hv, void* stream) {
+  return ed_sector_hxv_dev_path(s, -1, vtype, v, hv, stream);
+}
+
+int ed_sector_hxv(ed_sector* s, int32_t nloc, const double* v, double* hv) {
+  if (!s || !v || !hv) return fail(ED_ERR_ARG, "null");
+  // directMatVec_cc: "Nloc != dim(isector)" (DIRECT_HxV.f90:50)
+  if ((int64_t)nloc != s->dim) return fail(ED_ERR_ARG, "ed_gpu_hxv ERROR: Nloc != dim(isector)");
+  HIPCK(hipSetDevice(s->device));
+  if (!s->d_x) {
+    CK(dalloc(s, &s->d_x, s->dim * 16));
+    CK(dalloc(s, &s->d_y, s->dim * 16));
+  }
+  HIPCK(hipMemcpyAsync(s->d_x, v, s->dim * 16, hipMemcpyHostToDevice, s->stream));
+  CK(ed_sector_hxv_dev(s, 1, s->d_x, s->d_y, s->stream));
+  HIPCK(hipMemcpyAsync(hv, s->d_y, s->dim * 16, hipMemcpyDeviceToHost, s->stream));
+  HIPCK(hipStreamSynchronize(s->stream));
+  return ED_OK;
+}
+
+int ed_sector_map(const ed_sector* s, uint32_t* map_host) {
+  if (!s || !map_host) return fail(ED_ERR_ARG, "null");
+  HIPCK(hipSetDevice(s->device));
+  HIPCK(hipMemcpy(map_host, s->d_map, s->dim * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  return ED_OK;
+}
+
+int ed_sector_dump_csr(const ed_sector* s, int64_t* rowptr, int32_t* cols, double* vals) {
+  if (!s || !rowptr || !cols || !vals) return fail(ED_ERR_ARG, "null");
+  if (!(s->flags & ED_STORED)) return fail(ED_ERR_STATE, "sector was built without ED_STORED");
+  HIPCK(hipSetDevice(s->device));
+  const int64_t dim = s->dim, ns = s->nslice, slots = s->padded;
+  const int hw = s->hc ? 2 : 1;
+  std::vector<uint16_t> cnt(dim);
+  std::vector<int64_t> sptr(ns + 1);
+  std::vector<int32_t> sc(slots);
+  std::vector<double> sv(slots * hw), dg(dim * hw);
+  HIPCK(hipMemcpy(cnt.data(), s->d_cnt, dim * 2, hipMemcpyDeviceToHost));
+  HIPCK(hipMemcpy(sptr.data(), s->d_sptr, (ns + 1) * 8, hipMemcpyDeviceToHost));
+  HIPCK(hipMemcpy(sc.data(), s->d_cols, slots * 4, hipMemcpyDeviceToHost));
+  HIPCK(hipMemcpy(sv.data(), s->d_vals, slots * 8 * hw, hipMemcpyDeviceToHost));
+  HIPCK(hipMemcpy(dg.data(), s->d_diag, dim * 8 * hw, hipMemcpyDeviceToHost));
+  int64_t q = 0;
+  rowptr[0] = 0;
+  for (int64_t i = 0; i < dim; i++) {
+    cols[q] = (int32_t)i;
+    vals[2 * q] = dg[hw * i];
+    vals[2 * q + 1] = hw == 2 ? dg[2 * i + 1] : 0.0;
+    q++;
+    int64_t base = sptr[i >> 6] + (i & 63);
+    for (int k = 0; k < cnt[i]; k++) {
+      int64_t t = base + 64 * (int64_t)k;
+      cols[q] = sc[t];
+      vals[2 * q] = sv[hw * t];
+      vals[2 * q + 1] = hw == 2 ? sv[2 * t + 1] : 0.0;
+      q++;
+    }
+    rowptr[i + 1] = q;
+  }
+  return ED_OK;
+}
+
+// Fixed-length run from a device start vector (benchmark entry point).
+int ed_sector_lanc_run(ed_sector* s, int32_t vtype, const void* v0_dev, int32_t niter,
+                       double* alfa, double* beta, float* ms, void* stream) {
+  if (!s || niter < 1) return fail(ED_ERR_ARG, "bad args");
+  HIPCK(hipSetDevice(s->device));
+  const int vc = vtype ? 1 : 0;
+  if (vc == 0 && s->hc) return fail(ED_ERR_ARG, "complex H needs vtype=1");
+  CK(lanc_prepare(s, vc, niter, false, 0));
+  hipStream_t st = s->stream;
+  const size_t vs = vc ? 16 : 8;
+  if (v0_dev) HIPCK(hipMemcpyAsync(s->ws.R, v0_dev, s->dim * vs, hipMemcpyDeviceToDevice, st));
+  else hipLaunchKernelGGL(k_default_start, dim3(grid_for(s->dim * (vc ? 2 : 1))), dim3(kBlock), 0,
+                          st, (double*)s->ws.R, s->dim * (vc ? 2 : 1));
+  const int path = resolve_path(s, -1);
+  hipEvent_t e0, e1;
+  HIPCK(hipEventCreate(&e0));
+  HIPCK(hipEventCreate(&e1));
+  int rc;
+  if (vc) rc = lanc_start<true>(s, 1e-300, st);
+  else rc = lanc_start<false>(s, 1e-300, st);
+  if (rc == ED_OK) {
+    HIPCK(hipEventRecord(e0, st));
+    rc = vc ? lanc_iters<true>(s, path, false, niter, st) : lanc_iters<false>(s, path, false, niter, st);
+    HIPCK(hipEventRecord(e1, st));
+  }
+  HIPCK(hipStreamSynchronize(st));
+  if (ms) HIPCK(hipEventElapsedTime(ms, e0, e1));
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  CK(rc);
+  if (alfa) HIPCK(hipMemcpy(alfa, s->ws.alpha, niter * sizeof(double), hipMemcpyDeviceToHost));
+  if (beta) HIPCK(hipMemcpy(beta, s->ws.beta, niter * sizeof(double), hipMemcpyDeviceToHost));
+  (void)stream;
+  return ED_OK;
+}
+
+static int lanc_load_start(ed_sector* s, int vc, const void* v0) {
+  const size_t vs = vc ? 16 : 8;
+  if (v0) {
+    HIPCK(hipMemcpyAsync(s->ws.R, v0, s->dim * vs, hipMemcpyHostToDevice, s->stream));
+  } else {
+    hipLaunchKernelGGL(k_default_start, dim3(grid_for(s->dim * (vc ? 2 : 1))), dim3(kBlock), 0,
+                       s->stream, (double*)s->ws.R, s->dim * (vc ? 2 : 1));
+    HIPCK(hipGetLastError());
+  }
+  return ED_OK;
+}
+
+int ed_sector_lanc_tridiag(ed_sector* s, int32_t vtype, const void* v0, int32_t nitermax,
+                           double threshold, double* alfa, double* beta, int32_t* nlanc) {
+  if (!s || !alfa || !beta || nitermax < 1) return fail(ED_ERR_ARG, "bad args");
+  HIPCK(hipSetDevice(s->device));
+  const int vc = vtype ? 1 : 0;
+  if (vc == 0 && s->hc) return fail(ED_ERR_ARG, "complex H needs vtype=1");
+  CK(lanc_prepare(s, vc, nitermax, false, 0));
+  CK(lanc_load_start(s, vc, v0));
+  const int path = resolve_path(s, -1);
+  CK(vc ? lanc_start<true>(s, threshold, s->stream) : lanc_start<false>(s, threshold, s->stream));
+  CK(vc ? lanc_iters<true>(s, path, false, nitermax, s->stream)
+        : lanc_iters<false>(s, path, false, nitermax, s->stream));
+  std::vector<double> a(nitermax + 1), b(nitermax + 2);
+  HIPCK(hipMemcpyAsync(a.data(), s->ws.alpha, nitermax * 8, hipMemcpyDeviceToHost, s->stream));
+  HIPCK(hipMemcpyAsync(b.data(), s->ws.beta, (nitermax + 1) * 8, hipMemcpyDeviceToHost, s->stream));
+  LancState hs;
+  HIPCK(hipMemcpyAsync(&hs, s->ws.st, sizeof(hs), hipMemcpyDeviceToHost, s->stream));
+  HIPCK(hipStreamSynchronize(s->stream));
+  // lanczos_plain_tridiag_c: alanc(iter)=a; if(iter<nitermax)blanc(iter+1)=b; exit if |b|<thr
+  int n = hs.iter;
+  for (int q = 0; q < nitermax; q++) {
+    alfa[q] = q < n ? a[q] : 0.0;
+    beta[q] = (q >= 1 && q <= n) ? b[q] : 0.0;
+  }
+  beta[0] = 0.0;
+  if (nlanc) *nlanc = n;
+  return ED_OK;
+}
+
+int ed_sector_lanc_eigh(ed_sector* s, int32_t vtype, const void* v0, int32_t nitermax,
+                        double threshold, int32_t ncheck, double* egs, void* vect,
+                        int32_t* nlanc) {
+  if (!s || !egs || nitermax < 1) return fail(ED_ERR_ARG, "bad args");
+  if (ncheck < 1) ncheck = 10;
+  HIPCK(hipSetDevice(s->device));
+  const int vc = vtype ? 1 : 0;
+  if (vc == 0 && s->hc) return fail(ED_ERR_ARG, "complex H needs vtype=1");
+  const size_t vs = vc ? 16 : 8;
+  // keep the Krylov basis when it fits in 1/4 of free memory (no second pass)
+  size_t fr = 0, tot = 0;
+  HIPCK(hipMemGetInfo(&fr, &tot));
+  const bool keep = vect && ((double)nitermax * s->dim * vs < 0.25 * (double)fr);
+  CK(lanc_prepare(s, vc, nitermax, keep, keep ? nitermax : 0));
+  CK(lanc_load_start(s, vc, v0));
+  const int path = resolve_path(s, -1);
+  CK(vc ? lanc_start<true>(s, threshold, s->stream) : lanc_start<false>(s, threshold, s->stream));
+  // lanczos_plain_c convergence test, evaluated on the host between chunks
+  std::vector<double> a(nitermax + 2, 0.0), b(nitermax + 2, 0.0), esave;
+  int done_iters = 0, nl = 0;
+  bool stop = false;
+  const int chunk = 32;
+  while (!stop && done_iters < nitermax) {
+    int n = std::min(chunk, nitermax - done_iters);
+    const int expected = done_iters + n;
+    CK(vc ? lanc_iters<true>(s, path, keep, n, s->stream)
+          : lanc_iters<false>(s, path, keep, n, s->stream));
+    HIPCK(hipMemcpyAsync(a.data(), s->ws.alpha, nitermax * 8, hipMemcpyDeviceToHost, s->stream));
+    HIPCK(hipMemcpyAsync(b.data(), s->ws.beta, (nitermax + 1) * 8, hipMemcpyDeviceToHost, s->stream));
+    LancState hs;
+    HIPCK(hipMemcpyAsync(&hs, s->ws.st, sizeof(hs), hipMemcpyDeviceToHost, s->stream));
+    HIPCK(hipStreamSynchronize(s->stream));
+    int have = hs.iter;
+    for (int it = done_iters + 1; it <= have && !stop; it++) {
+      // iteration `it`: a = a[it-1], b = b[it]
+      if (fabs(b[it]) < threshold) { stop = true; break; }
+      nl = it;
+      if (nl >= ncheck) {
+        double e0 = lowest_ritz(a, b, nl);
+        esave.push_back(e0);
+        if (esave.size() >= 2 && fabs(esave.back() - esave[esave.size() - 2]) <= threshold) stop = true;
+      }
+    }
+    if (hs.done) stop = true;
+    if (have < expected && !hs.done) return fail(ED_ERR_STATE, "Lanczos iteration count mismatch");
+    done_iters = have;
+  }
+  // Ritz value and vector of the truncated tridiagonal (nl iterations)
+  std::vector<double> d(a.begin(), a.begin() + nl), e(nl, 0.0), z((size_t)nl * nl, 0.0);
+  for (int q = 1; q < nl; q++) e[q] = b[q];
+  for (int q = 0; q < nl; q++) z[q + (size_t)nl * q] = 1.0;
+  if (nl > 0) tql2(nl, d.data(), e.data(), z.data());
+  *egs = nl > 0 ? d[0] : 0.0;
+  if (nlanc) *nlanc = nl;
+  if (vect && nl > 0) {
+    LancWS& w = s->ws;
+    HIPCK(hipMemcpyAsync(w.z, z.data(), nl * 8, hipMemcpyHostToDevice, s->stream));  // Z(:,1)
+    RedSlot slot{w.partials, w.counter + 2};
+    if (keep) {
+      if (vc)
+        hipLaunchKernelGGL(k_ritz<true>, dim3(grid_for(s->dim)), dim3(kBlock), 0, s->stream,
+                           (const double2*)w.basis, w.z, nl, s->dim, (double2*)w.Y, w.st, slot);
+      else
+        hipLaunchKernelGGL(k_ritz<false>, dim3(grid_for(s->dim)), dim3(kBlock), 0, s->stream,
+                           (const double*)w.basis, w.z, nl, s->dim, (double*)w.Y, w.st, slot);
+    } else {
+      // second pass as lanczos_plain_c (:374-381): rerun the recurrence, y += Z(it,1) v_it
+      HIPCK(hipMemsetAsync(w.Y, 0, s->dim * vs, s->stream));
+      CK(lanc_load_start(s, vc, v0));
+      CK(vc ? lanc_start<true>(s, threshold, s->stream) : lanc_start<false>(s, threshold, s->stream));
+      for (int it = 0; it < nl; it++) {
+        CK(vc ? lanc_iter<true>(s, path, false, s->stream) : lanc_iter<false>(s, path, false, s->stream));
+        if (vc)
+          hipLaunchKernelGGL(k_axpy_p<true>, dim3(grid_for(s->dim)), dim3(kBlock), 0, s->stream,
+                             (const double2*)w.P, w.z, it, s->dim, (double2*)w.Y);
+        else
+          hipLaunchKernelGGL(k_axpy_p<false>, dim3(grid_for(s->dim)), dim3(kBlock), 0, s->stream,
+                             (const double*)w.P, w.z, it, s->dim, (double*)w.Y);
+      }
+      if (vc)
+        hipLaunchKernelGGL(k_norm<true>, dim3(grid_for(s->dim)), dim3(kBlock), 0, s->stream,
+                           (const double2*)w.Y, s->dim, w.st, slot);
+      else
+        hipLaunchKernelGGL(k_norm<false>, dim3(grid_for(s->dim)), dim3(kBlock), 0, s->stream,
+                           (const double*)w.Y, s->dim, w.st, slot);
+    }
+    if (vc)
+      hipLaunchKernelGGL(k_scale_tmp<true>, dim3(grid_for(s->dim)), dim3(kBlock), 0, s->stream,
+                         (double2*)w.Y, s->dim, w.st);
+    else
+      hipLaunchKernelGGL(k_scale_tmp<false>, dim3(grid_for(s->dim)), dim3(kBlock), 0, s->stream,
+                         (double*)w.Y, s->dim, w.st);
+    HIPCK(hipGetLastError());
+    HIPCK(hipMemcpyAsync(vect, w.Y, s->dim * vs, hipMemcpyDeviceToHost, s->stream));
+    HIPCK(hipStreamSynchronize(s->stream));
+  }
+  return ED_OK;
+}
+
+// ------------------------------------------------- reference-style globals
+static std::mutex g_mu;
+static ed_params g_params;
+static bool g_have_params = false;
+static int g_device = 0;
+static ed_sector* g_cur = nullptr;
+
+int ed_gpu_init(const ed_params* p) {
+  if (!p) return fail(ED_ERR_ARG, "null params");
+  EdModel M;
+  int rc = model_from_params(p, &M);
+  if (rc != ED_OK) return fail(rc, "invalid ed_params");
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_params = *p;
+  g_have_params = true;
+  return ED_OK;
+}
+
+int ed_gpu_set_device(int32_t device) {
+  int n = 0;
+  HIPCK(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n) return fail(ED_ERR_ARG, "bad device");
+  g_device = device;
+  return ED_OK;
+}
+
+int ed_gpu_build_sector(int32_t q1, int32_t q2, int32_t flags, int64_t* dim) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_have_params) return fail(ED_ERR_STATE, "ed_gpu_init not called");
+  if (g_cur) {  // build_Hv_sector on a live sector: replace it
+    sector_free(g_cur);
+    g_cur = nullptr;
+  }
+  CK(ed_sector_create(&g_params, q1, q2, flags, g_device, nullptr, &g_cur));
+  if (dim) *dim = g_cur->dim;
+  return ED_OK;
+}
+
+int ed_gpu_vecdim(int32_t* vecdim) {
+  if (!g_cur || !vecdim) return fail(ED_ERR_STATE, "no current sector");
+  *vecdim = (int32_t)g_cur->dim;  // serial: MpiQ=Dim, MpiR=0 (ED_HAMILTONIAN.f90:141-143)
+  return ED_OK;
+}
+
+int ed_gpu_hxv(const int32_t* nloc, const double* v, double* hv) {
+  if (!g_cur) return fail(ED_ERR_STATE, "ed_gpu_hxv ERROR: Hsector NOT set");
+  if (!nloc) return fail(ED_ERR_ARG, "null nloc");
+  return ed_sector_hxv(g_cur, *nloc, v, hv);
+}
+
+int ed_gpu_dump_csr(int64_t* rowptr, int32_t* cols, double* vals) {
+  if (!g_cur) return fail(ED_ERR_STATE, "no current sector");
+  return ed_sector_dump_csr(g_cur, rowptr, cols, vals);
+}
+
+int ed_gpu_lanc_eigh(int32_t nitermax, double threshold, int32_t ncheck, double* egs, double* vect,
+                     int32_t* nlanc) {
+  if (!g_cur) return fail(ED_ERR_STATE, "no current sector");
+  return ed_sector_lanc_eigh(g_cur, 1, nullptr, nitermax, threshold, ncheck, egs, vect, nlanc);
+}
+
+int ed_gpu_lanc_tridiag(const double* v0, int32_t nitermax, double threshold, double* alfa,
+                        double* beta, int32_t* nlanc) {
+  if (!g_cur) return fail(ED_ERR_STATE, "no current sector");
+  return ed_sector_lanc_tridiag(g_cur, 1, v0, nitermax, threshold, alfa, beta, nlanc);
+}
+
+int ed_gpu_delete_sector(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  // delete_Hv_sector: safe after a direct build (the reference stops in
+  // sp_delete_matrix there, ED_HAMILTONIAN.f90:111-119 / ED_SPARSE_MATRIX.f90:180)
+  if (g_cur) sector_free(g_cur);
+  g_cur = nullptr;
+  return ED_OK;
+}
+
+int ed_gpu_finalize(void) {
+  ed_gpu_delete_sector();
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_have_params = false;
+  return ED_OK;
+}
+
+int ed_gpu_current_sector(ed_sector** out) {
+  if (!out) return fail(ED_ERR_ARG, "null");
+  *out = g_cur;
+  return g_cur ? ED_OK : fail(ED_ERR_STATE, "no current sector");
+}
+
+}  // extern "C"

@@ -1,0 +1,390 @@
+// ed_model.hpp — device-side model constants and the row element generator.
+//
+// The generator is the single source of matrix elements for every device
+// path (stored-H builder, matrix-free H·v, GF seeds): for a basis state m it
+// produces the row of H in the *stored* convention of the reference,
+//   H(i,j) = conj(coeff) * sg,   |k_j> = op |m_i>          (ED_HAMILTONIAN/stored/*.f90)
+// in the exact insertion order of ed_buildH_c, so that the stored matrix
+// reproduces spH0 (ED_SPARSE_MATRIX row-of-arrays) element by element.
+// By hermiticity the same row drives the gather-form matrix-free kernel,
+//   Hv(i) = sum_j H(i,j) v(j),
+// which replaces the reference's scatter loop (ED_HAMILTONIAN_DIRECT_HxV.f90:68-89).
+//
+// FP contraction is disabled in every TU that includes this file (-ffp-contract=off):
+// the diagonal is accumulated one IEEE op at a time in reference order, which
+// makes stored values bit-identical to the reference expression order.
+#pragma once
+#include <stdint.h>
+
+#include "../../include/ed_gpu.h"
+
+#ifndef ED_HD
+#define ED_HD __host__ __device__ __forceinline__
+#endif
+
+namespace edg {
+
+struct EdModel {
+  int32_t ns, norb, nbath, nspin, S, mode, bath, ne, jhflag, hfmode;
+  int32_t stride[ED_MAX_NORB][ED_MAX_NBATH];  // getBathStride, 0-based bit
+  double hloc_re[ED_MAX_NSPIN][ED_MAX_NSPIN][ED_MAX_NORB][ED_MAX_NORB];
+  double hloc_im[ED_MAX_NSPIN][ED_MAX_NSPIN][ED_MAX_NORB][ED_MAX_NORB];
+  double uloc[3], ust, jh, jx, jp, xmu;
+  double e[ED_MAX_NSPIN][ED_MAX_NORB][ED_MAX_NBATH];
+  double u[ED_MAX_NSPIN][ED_MAX_NORB][ED_MAX_NBATH];
+  double d[ED_MAX_NSPIN][ED_MAX_NORB][ED_MAX_NBATH];
+  double hyb_re[ED_MAX_NSPIN][ED_MAX_NORB][ED_MAX_NBATH];  // diag_hybr (STORED_HxV.f90:58-70)
+  double hyb_im[ED_MAX_NSPIN][ED_MAX_NORB][ED_MAX_NBATH];
+  double hb_re[ED_MAX_NSPIN][ED_MAX_NSPIN][ED_MAX_NORB][ED_MAX_NORB][ED_MAX_NBATH];
+  double hb_im[ED_MAX_NSPIN][ED_MAX_NSPIN][ED_MAX_NORB][ED_MAX_NORB][ED_MAX_NBATH];
+};
+
+// Host: fill the model from the C-ABI params.  Returns 0 or an ED_ERR_* code.
+// ed_setup_dimensions ED_SETUP.f90:96-111, getBathStride ED_SETUP.f90:448-465,
+// Jhflag ED_SETUP.f90:289-290.
+inline int model_from_params(const ed_params* p, EdModel* M) {
+  if (!p) return ED_ERR_ARG;
+  if (p->norb < 1 || p->norb > ED_MAX_NORB || p->nspin < 1 || p->nspin > ED_MAX_NSPIN ||
+      p->nbath < 0 || p->nbath > ED_MAX_NBATH)
+    return ED_ERR_ARG;
+  if (p->ed_mode < 0 || p->ed_mode > 2 || p->bath_type < 0 || p->bath_type > 2) return ED_ERR_ARG;
+  if (p->ed_mode == ED_MODE_NONSU2 && p->nspin != 2) return ED_ERR_ARG;  // ed_checks_global
+  if (p->ed_mode == ED_MODE_SUPERC && p->nspin != 1) return ED_ERR_ARG;
+  *M = EdModel{};
+  M->norb = p->norb; M->nbath = p->nbath; M->nspin = p->nspin; M->S = p->nspin - 1;
+  M->mode = p->ed_mode; M->bath = p->bath_type; M->hfmode = p->hfmode ? 1 : 0;
+  M->ns = (p->bath_type == ED_BATH_HYBRID) ? p->nbath + p->norb : (p->nbath + 1) * p->norb;
+  if (M->ns > ED_MAX_NS) return ED_ERR_UNSUPPORTED;
+  M->ne = (p->bath_type == ED_BATH_HYBRID) ? 1 : p->norb;
+  M->jhflag = (p->norb > 1 && (p->jx != 0.0 || p->jp != 0.0)) ? 1 : 0;
+  for (int k = 0; k < p->nbath; k++)
+    for (int o = 0; o < p->norb; o++) {
+      int lev;
+      if (p->bath_type == ED_BATH_HYBRID) lev = p->norb + (k + 1);
+      else if (p->bath_type == ED_BATH_REPLICA) lev = (o + 1) + (k + 1) * p->norb;
+      else lev = p->norb + o * p->nbath + (k + 1);
+      M->stride[o][k] = lev - 1;
+    }
+  for (int a = 0; a < ED_MAX_NSPIN; a++)
+    for (int b = 0; b < ED_MAX_NSPIN; b++)
+      for (int c = 0; c < ED_MAX_NORB; c++)
+        for (int d = 0; d < ED_MAX_NORB; d++) {
+          M->hloc_re[a][b][c][d] = p->imphloc_re[a][b][c][d];
+          M->hloc_im[a][b][c][d] = p->imphloc_im[a][b][c][d];
+          for (int k = 0; k < ED_MAX_NBATH; k++) {
+            M->hb_re[a][b][c][d][k] = p->bath_h_re[a][b][c][d][k];
+            M->hb_im[a][b][c][d][k] = p->bath_h_im[a][b][c][d][k];
+          }
+        }
+  for (int i = 0; i < 3; i++) M->uloc[i] = p->uloc[i];
+  M->ust = p->ust; M->jh = p->jh; M->jx = p->jx; M->jp = p->jp; M->xmu = p->xmu;
+  for (int s = 0; s < ED_MAX_NSPIN; s++)
+    for (int o = 0; o < ED_MAX_NORB; o++)
+      for (int k = 0; k < ED_MAX_NBATH; k++) {
+        M->e[s][o][k] = p->bath_e[s][o][k];
+        M->u[s][o][k] = p->bath_u[s][o][k];
+        M->d[s][o][k] = p->bath_d[s][o][k];
+        if (p->bath_type != ED_BATH_REPLICA) {
+          M->hyb_re[s][o][k] = p->bath_v[s][o][k];
+          M->hyb_im[s][o][k] = 0.0;
+        } else {
+          M->hyb_re[s][o][k] = p->bath_vr_re[k];
+          M->hyb_im[s][o][k] = p->bath_vr_im[k];
+        }
+      }
+  return ED_OK;
+}
+
+// True when every coefficient that can enter H is real.
+inline bool model_is_real(const EdModel& M) {
+  for (int a = 0; a < ED_MAX_NSPIN; a++)
+    for (int b = 0; b < ED_MAX_NSPIN; b++)
+      for (int c = 0; c < ED_MAX_NORB; c++)
+        for (int d = 0; d < ED_MAX_NORB; d++) {
+          if (M.hloc_im[a][b][c][d] != 0.0) return false;
+          for (int k = 0; k < ED_MAX_NBATH; k++)
+            if (M.hb_im[a][b][c][d][k] != 0.0) return false;
+        }
+  for (int s = 0; s < ED_MAX_NSPIN; s++)
+    for (int o = 0; o < ED_MAX_NORB; o++)
+      for (int k = 0; k < ED_MAX_NBATH; k++)
+        if (M.hyb_im[s][o][k] != 0.0) return false;
+  return true;
+}
+
+ED_HD int bit(uint32_t x, int b) { return (int)((x >> b) & 1u); }
+
+// c / cdg (ED_SETUP.f90:1080-1106): Jordan-Wigner sign = (-1)^popcount(bits below b).
+ED_HD double jw_sign(uint32_t in, int b) {
+  uint32_t below = (b == 0) ? 0u : (in & ((1u << b) - 1u));
+  return (__builtin_popcount(below) & 1) ? -1.0 : 1.0;
+}
+
+// Local interaction on the diagonal, stored/Hint.f90:117-155 (= direct/HxVint.f90:1-47).
+// upbits/dwbits: impurity occupations n_{o,up} = bit o of upbits, n_{o,dw} = bit o of dwbits.
+ED_HD double hint_value(const EdModel& M, uint32_t upbits, uint32_t dwbits) {
+  const int norb = M.norb;
+#define nup(o) ((double)bit(upbits, (o)))
+#define ndw(o) ((double)bit(dwbits, (o)))
+  double h = 0.0;
+  for (int o = 0; o < norb; o++) h = h + (M.uloc[o] * nup(o)) * ndw(o);
+  if (norb > 1) {
+    for (int o = 0; o < norb; o++)
+      for (int q = o + 1; q < norb; q++) h = h + M.ust * (nup(o) * ndw(q) + nup(q) * ndw(o));
+    for (int o = 0; o < norb; o++)
+      for (int q = o + 1; q < norb; q++)
+        h = h + (M.ust - M.jh) * (nup(o) * nup(q) + ndw(o) * ndw(q));
+  }
+  if (M.hfmode) {
+    for (int o = 0; o < norb; o++) h = (h - (0.5 * M.uloc[o]) * (nup(o) + ndw(o))) + 0.25 * M.uloc[o];
+    if (norb > 1)
+      for (int o = 0; o < norb; o++)
+        for (int q = o + 1; q < norb; q++) {
+          double nn = ((nup(o) + ndw(o)) + nup(q)) + ndw(q);
+          h = (h - (0.5 * M.ust) * nn) + 0.25 * M.ust;
+          h = (h - (0.5 * (M.ust - M.jh)) * nn) + 0.25 * (M.ust - M.jh);
+        }
+  }
+#undef nup
+#undef ndw
+  return h;
+}
+
+// ---------------------------------------------------------------- generator
+// Acc must provide:
+//   void diag(double re, double im);                 // once, first
+//   void off(uint32_t k, double re, double im);      // off-diagonal, in order
+// `ValuesOnly` accs may ignore arguments; the compiler removes dead math.
+template <class Acc>
+ED_HD void gen_row(const EdModel& M, uint32_t m, Acc& acc) {
+  const int ns = M.ns, norb = M.norb, nbath = M.nbath, S = M.S;
+  // nup(iorb)/ndw(iorb) of the reference, evaluated on the fly (no local arrays:
+  // dynamically indexed arrays would spill to scratch on the GPU)
+#define nup(o) ((double)bit(m, (o)))
+#define ndw(o) ((double)bit(m, (o) + ns))
+  // ---- diagonal: stored/Himp.f90:11-16, merged with Hint.f90:119-155 and
+  //      Hbath.f90:13-27 / :33-40 (sp_insert_element adds into the first slot).
+  double dr = 0.0, di = 0.0;
+  for (int o = 0; o < norb; o++) {
+    dr = dr + M.hloc_re[0][0][o][o] * nup(o);
+    di = di + M.hloc_im[0][0][o][o] * nup(o);
+    dr = dr + M.hloc_re[S][S][o][o] * ndw(o);
+    di = di + M.hloc_im[S][S][o][o] * ndw(o);
+    dr = dr - M.xmu * (nup(o) + ndw(o));
+  }
+  {
+    double h = hint_value(M, m, m >> ns);
+    dr = dr + h;
+    di = di + 0.0;
+  }
+  if (M.bath != ED_BATH_REPLICA) {
+    double h = 0.0;
+    for (int o = 0; o < M.ne; o++)
+      for (int k = 0; k < nbath; k++) {
+        int a = M.stride[o][k];
+        h = h + M.e[0][o][k] * (double)bit(m, a);
+        h = h + M.e[S][o][k] * (double)bit(m, a + ns);
+      }
+    dr = dr + h;
+    di = di + 0.0;
+  } else {
+    double hr = 0.0, hi = 0.0;
+    for (int k = 0; k < nbath; k++)
+      for (int o = 0; o < norb; o++) {
+        int a = M.stride[o][k];
+        double nu = (double)bit(m, a), nd = (double)bit(m, a + ns);
+        hr = hr + M.hb_re[0][0][o][o][k] * nu;
+        hi = hi + M.hb_im[0][0][o][o][k] * nu;
+        hr = hr + M.hb_re[S][S][o][o][k] * nd;
+        hi = hi + M.hb_im[S][S][o][o][k] * nd;
+      }
+    dr = dr + hr;
+    di = di + hi;
+  }
+  acc.diag(dr, di);
+#undef nup
+#undef ndw
+
+  // ---- stored/Himp.f90:27-72 same-spin impurity hops, value conj(h)*sg1*sg2
+  for (int io = 0; io < norb; io++)
+    for (int jo = 0; jo < norb; jo++) {
+      {
+        double hr = M.hloc_re[0][0][io][jo], hi = M.hloc_im[0][0][io][jo];
+        if ((hr != 0.0 || hi != 0.0) && bit(m, jo) == 1 && bit(m, io) == 0) {
+          double s = jw_sign(m, jo);
+          uint32_t k1 = m & ~(1u << jo);
+          double s2 = jw_sign(k1, io);
+          acc.off(k1 | (1u << io), (hr * s) * s2, (-hi * s) * s2);
+        }
+      }
+      {
+        double hr = M.hloc_re[S][S][io][jo], hi = M.hloc_im[S][S][io][jo];
+        int a = io + ns, b = jo + ns;
+        if ((hr != 0.0 || hi != 0.0) && bit(m, b) == 1 && bit(m, a) == 0) {
+          double s = jw_sign(m, b);
+          uint32_t k1 = m & ~(1u << b);
+          double s2 = jw_sign(k1, a);
+          acc.off(k1 | (1u << a), (hr * s) * s2, (-hi * s) * s2);
+        }
+      }
+    }
+  // ---- stored/Himp.f90:74-104 nonSU2 spin-flip impHloc
+  if (M.mode == ED_MODE_NONSU2) {
+    for (int is = 0; is < 2; is++) {
+      int js = 1 - is;
+      for (int io = 0; io < norb; io++)
+        for (int jo = 0; jo < norb; jo++) {
+          double hr = M.hloc_re[is][js][io][jo], hi = M.hloc_im[is][js][io][jo];
+          int a = io + is * ns, b = jo + js * ns;
+          if ((hr != 0.0 || hi != 0.0) && bit(m, b) == 1 && bit(m, a) == 0) {
+            double s = jw_sign(m, b);
+            uint32_t k1 = m & ~(1u << b);
+            double s2 = jw_sign(k1, a);
+            acc.off(k1 | (1u << a), (hr * s) * s2, (-hi * s) * s2);
+          }
+        }
+    }
+  }
+  // ---- stored/Hint.f90:169-229 spin exchange and pair hopping
+  if (norb > 1 && M.jhflag) {
+    for (int io = 0; io < norb; io++)
+      for (int jo = 0; jo < norb; jo++)
+        if (io != jo && bit(m, jo) == 1 && bit(m, io + ns) == 1 && bit(m, jo + ns) == 0 &&
+            bit(m, io) == 0) {
+          double s1 = jw_sign(m, jo);
+          uint32_t k1 = m & ~(1u << jo);
+          double s2 = jw_sign(k1, io + ns);
+          uint32_t k2 = k1 & ~(1u << (io + ns));
+          double s3 = jw_sign(k2, jo + ns);
+          uint32_t k3 = k2 | (1u << (jo + ns));
+          double s4 = jw_sign(k3, io);
+          acc.off(k3 | (1u << io), (((M.jx * s1) * s2) * s3) * s4, 0.0);
+        }
+    for (int io = 0; io < norb; io++)
+      for (int jo = 0; jo < norb; jo++)
+        if (io != jo && bit(m, jo) == 1 && bit(m, jo + ns) == 1 && bit(m, io + ns) == 0 &&
+            bit(m, io) == 0) {
+          double s1 = jw_sign(m, jo);
+          uint32_t k1 = m & ~(1u << jo);
+          double s2 = jw_sign(k1, jo + ns);
+          uint32_t k2 = k1 & ~(1u << (jo + ns));
+          double s3 = jw_sign(k2, io + ns);
+          uint32_t k3 = k2 | (1u << (io + ns));
+          double s4 = jw_sign(k3, io);
+          acc.off(k3 | (1u << io), (((M.jp * s1) * s2) * s3) * s4, 0.0);
+        }
+  }
+  // ---- stored/Hbath.f90:52-135 replica bath hops (same spin, then nonSU2 flips)
+  if (M.bath == ED_BATH_REPLICA) {
+    for (int k = 0; k < nbath; k++)
+      for (int io = 0; io < norb; io++)
+        for (int jo = 0; jo < norb; jo++)
+          for (int sp = 0; sp < 2; sp++) {
+            int ss = sp == 0 ? 0 : S;
+            double hr = M.hb_re[ss][ss][io][jo][k], hi = M.hb_im[ss][ss][io][jo][k];
+            int a = M.stride[io][k] + sp * ns, b = M.stride[jo][k] + sp * ns;
+            if ((hr != 0.0 || hi != 0.0) && bit(m, b) == 1 && bit(m, a) == 0) {
+              double s = jw_sign(m, b);
+              uint32_t k1 = m & ~(1u << b);
+              double s2 = jw_sign(k1, a);
+              acc.off(k1 | (1u << a), (hr * s) * s2, (-hi * s) * s2);
+            }
+          }
+    if (M.mode == ED_MODE_NONSU2) {
+      for (int k = 0; k < nbath; k++)
+        for (int is = 0; is < 2; is++) {
+          int js = 1 - is;
+          for (int io = 0; io < norb; io++)
+            for (int jo = 0; jo < norb; jo++) {
+              double hr = M.hb_re[is][js][io][jo][k], hi = M.hb_im[is][js][io][jo][k];
+              int a = M.stride[io][k] + is * ns, b = M.stride[jo][k] + js * ns;
+              if ((hr != 0.0 || hi != 0.0) && bit(m, b) == 1 && bit(m, a) == 0) {
+                double s = jw_sign(m, b);
+                uint32_t k1 = m & ~(1u << b);
+                double s2 = jw_sign(k1, a);
+                acc.off(k1 | (1u << a), (hr * s) * s2, (-hi * s) * s2);
+              }
+            }
+        }
+    }
+  }
+  // ---- stored/Hbath.f90:142-178 superconducting pair terms
+  if (M.mode == ED_MODE_SUPERC) {
+    for (int o = 0; o < M.ne; o++)
+      for (int k = 0; k < nbath; k++) {
+        int ms = M.stride[o][k];
+        double dd = M.d[0][o][k];
+        if (dd != 0.0 && bit(m, ms) == 1 && bit(m, ms + ns) == 1) {
+          double s1 = jw_sign(m, ms);
+          uint32_t k1 = m & ~(1u << ms);
+          double s2 = jw_sign(k1, ms + ns);
+          acc.off(k1 & ~(1u << (ms + ns)), (dd * s1) * s2, 0.0);
+        }
+        if (dd != 0.0 && bit(m, ms) == 0 && bit(m, ms + ns) == 0) {
+          double s1 = jw_sign(m, ms + ns);
+          uint32_t k1 = m | (1u << (ms + ns));
+          double s2 = jw_sign(k1, ms);
+          acc.off(k1 | (1u << ms), (dd * s1) * s2, 0.0);
+        }
+      }
+  }
+  // ---- stored/Himp_bath.f90:192-249 spin-conserving hybridisation
+  for (int o = 0; o < norb; o++)
+    for (int k = 0; k < nbath; k++) {
+      int ms = M.stride[o][k];
+      for (int sp = 0; sp < 2; sp++) {
+        int ss = sp == 0 ? 0 : S;
+        double hr = M.hyb_re[ss][o][k], hi = M.hyb_im[ss][o][k];
+        bool nz = (hr != 0.0 || hi != 0.0);
+        int a = o + sp * ns, b = ms + sp * ns;  // impurity level, bath level
+        if (nz && bit(m, a) == 1 && bit(m, b) == 0) {
+          double s = jw_sign(m, a);
+          uint32_t k1 = m & ~(1u << a);
+          double s2 = jw_sign(k1, b);
+          acc.off(k1 | (1u << b), (hr * s) * s2, (-hi * s) * s2);
+        }
+        if (nz && bit(m, a) == 0 && bit(m, b) == 1) {
+          double s = jw_sign(m, b);
+          uint32_t k1 = m & ~(1u << b);
+          double s2 = jw_sign(k1, a);
+          acc.off(k1 | (1u << a), (hr * s) * s2, (-hi * s) * s2);
+        }
+      }
+    }
+  // ---- stored/Himp_bath.f90:253-310 nonSU2 spin-flip hybridisation (no u/=0 test)
+  if (M.mode == ED_MODE_NONSU2 && M.bath != ED_BATH_REPLICA) {
+    for (int o = 0; o < norb; o++)
+      for (int k = 0; k < nbath; k++) {
+        int ms = M.stride[o][k];
+        double uu = M.u[0][o][k], ud = M.u[S][o][k];
+        // IMP UP <--> BATH DW
+        if (bit(m, o) == 1 && bit(m, ms + ns) == 0) {
+          double s = jw_sign(m, o);
+          uint32_t k1 = m & ~(1u << o);
+          double s2 = jw_sign(k1, ms + ns);
+          acc.off(k1 | (1u << (ms + ns)), (uu * s) * s2, 0.0);
+        }
+        if (bit(m, o) == 0 && bit(m, ms + ns) == 1) {
+          double s = jw_sign(m, ms + ns);
+          uint32_t k1 = m & ~(1u << (ms + ns));
+          double s2 = jw_sign(k1, o);
+          acc.off(k1 | (1u << o), (uu * s) * s2, 0.0);
+        }
+        // IMP DW <--> BATH UP
+        if (bit(m, o + ns) == 1 && bit(m, ms) == 0) {
+          double s = jw_sign(m, o + ns);
+          uint32_t k1 = m & ~(1u << (o + ns));
+          double s2 = jw_sign(k1, ms);
+          acc.off(k1 | (1u << ms), (ud * s) * s2, 0.0);
+        }
+        if (bit(m, o + ns) == 0 && bit(m, ms) == 1) {
+          double s = jw_sign(m, ms);
+          uint32_t k1 = m & ~(1u << ms);
+          double s2 = jw_sign(k1, o + ns);
+          acc.off(k1 | (1u << (o + ns)), (ud * s) * s2, 0.0);
+        }
+      }
+  }
+}
+
+}  // namespace edg

@@ -1,0 +1,219 @@
+"""Sector Hamiltonian on the MI355X: the host mirror of ED_HAMILTONIAN.
+
+Reference interface mirrored (ED_HAMILTONIAN.f90:9-26):
+  build_Hv_sector(isector)   -> builds the basis and the stored H (or selects
+                                the matrix-free kernel) and binds spHtimesV_cc
+  delete_Hv_sector()         -> frees it (safe after a direct build, which the
+                                reference is not: ED_HAMILTONIAN.f90:111-119)
+  vecDim_Hv_sector(isector)  -> local vector length (serial: the sector dim)
+  spHtimesV_cc(Nloc, v, Hv)  -> cc_sparse_HxV (ED_VARS_GLOBAL.f90:48-54)
+
+Everything computes on the GPU through libedgpu.so; host numpy arrays are
+staged over PCIe (the drop-in level), torch device tensors are used in place.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import numpy as np
+
+from . import _lib
+from ._lib import ED_DIRECT, ED_REAL, ED_STORED, SectorInfo, check
+from .params import EDConfig
+from .sectors import Sector as SectorId
+from .sectors import setup_pointers
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def _tptr(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream_ptr(stream):
+    if stream is None:
+        return None
+    return ctypes.c_void_p(int(getattr(stream, "cuda_stream", stream)))
+
+
+class Sector:
+    """One symmetry sector resident on one GPU (handle API of include/ed_gpu.h)."""
+
+    def __init__(self, cfg: EDConfig, q1: int, q2: int = 0, *, stored: bool = True,
+                 direct: bool = False, real: bool = False, device: int = 0):
+        lib = _lib.load()
+        self.cfg = cfg
+        self._params = cfg.to_ctypes()
+        flags = (ED_STORED if stored else 0) | (ED_DIRECT if direct else 0) | (ED_REAL if real else 0)
+        h = ctypes.c_void_p()
+        check(lib.ed_sector_create(ctypes.byref(self._params), q1, q2, flags, device, None,
+                                   ctypes.byref(h)), "ed_sector_create")
+        self._h = h
+        self.device = device
+        self.real = real
+        info = SectorInfo()
+        check(lib.ed_sector_get_info(self._h, ctypes.byref(info)), "ed_sector_get_info")
+        self.info = info
+        self.dim = int(info.dim)
+        self.nnz = int(info.nnz)
+
+    # ------------------------------------------------------------------ life
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.load().ed_sector_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def handle(self):
+        return self._h
+
+    # -------------------------------------------------------------- queries
+    def map(self) -> np.ndarray:
+        """H%map (ED_SETUP.f90:886-984): the sector's Fock states, ascending."""
+        m = np.zeros(self.dim, dtype=np.uint32)
+        check(_lib.load().ed_sector_map(self._h, _ptr(m)), "ed_sector_map")
+        return m
+
+    def dump_csr(self):
+        """spH0 in reference row order (sp_dump_matrix, ED_SPARSE_MATRIX.f90:331-388)."""
+        rowptr = np.zeros(self.dim + 1, dtype=np.int64)
+        cols = np.zeros(self.nnz, dtype=np.int32)
+        vals = np.zeros(self.nnz, dtype=np.complex128)
+        check(_lib.load().ed_sector_dump_csr(self._h, _ptr(rowptr), _ptr(cols), _ptr(vals)),
+              "ed_sector_dump_csr")
+        return rowptr, cols, vals
+
+    # ------------------------------------------------------------------ H·v
+    def hxv(self, v: np.ndarray) -> np.ndarray:
+        """cc_sparse_HxV on host complex(8) arrays (synchronous)."""
+        v = np.ascontiguousarray(v, dtype=np.complex128)
+        if v.shape != (self.dim,):
+            raise ValueError("spHtimesV_cc: Nloc != dim(isector)")
+        hv = np.empty_like(v)
+        check(_lib.load().ed_sector_hxv(self._h, self.dim, _ptr(v), _ptr(hv)), "ed_sector_hxv")
+        return hv
+
+    def hxv_dev(self, v, hv, path: int = -1, stream=None) -> None:
+        """H·v on torch device tensors (float64 or complex128), async on `stream`.
+
+        path: -1 default, 0 stored SELL-64, 1 matrix-free generic, 2 matrix-free Kronecker.
+        """
+        import torch
+
+        if v.dtype == torch.complex128:
+            vt = 1
+        elif v.dtype == torch.float64:
+            vt = 0
+        else:
+            raise TypeError("vectors must be float64 or complex128")
+        if hv.dtype != v.dtype or v.numel() != self.dim or hv.numel() != self.dim:
+            raise ValueError("shape/dtype mismatch")
+        if not (v.is_contiguous() and hv.is_contiguous()):
+            raise ValueError("vectors must be contiguous")
+        if stream is None:
+            stream = torch.cuda.current_stream(v.device)
+        check(_lib.load().ed_sector_hxv_dev_path(self._h, path, vt, _tptr(v), _tptr(hv),
+                                                 _stream_ptr(stream)), "ed_sector_hxv_dev")
+
+    # -------------------------------------------------------------- Lanczos
+    def lanc_tridiag(self, v0: Optional[np.ndarray], nitermax: int, threshold: float = 1e-13,
+                     real: Optional[bool] = None):
+        """sp_lanc_tridiag: (alfa, beta, nlanc) with beta[0]=0 (blanc(1) unused)."""
+        vt, buf = self._vec_arg(v0, real)
+        a = np.zeros(nitermax)
+        b = np.zeros(nitermax)
+        n = ctypes.c_int32()
+        check(_lib.load().ed_sector_lanc_tridiag(self._h, vt, buf, nitermax, threshold, _ptr(a),
+                                                 _ptr(b), ctypes.byref(n)), "lanc_tridiag")
+        return a, b, int(n.value)
+
+    def lanc_eigh(self, nitermax: int = 512, threshold: float = 1e-12, ncheck: int = 10,
+                  v0: Optional[np.ndarray] = None, vector: bool = True,
+                  real: Optional[bool] = None):
+        """sp_lanc_eigh: ground-state energy (and Ritz vector) by plain Lanczos."""
+        vt, buf = self._vec_arg(v0, real)
+        egs = np.zeros(1)
+        n = ctypes.c_int32()
+        out = None
+        if vector:
+            out = np.zeros(self.dim, dtype=np.complex128 if vt else np.float64)
+        check(_lib.load().ed_sector_lanc_eigh(self._h, vt, buf, nitermax, threshold, ncheck,
+                                              _ptr(egs), None if out is None else _ptr(out),
+                                              ctypes.byref(n)), "lanc_eigh")
+        return float(egs[0]), out, int(n.value)
+
+    def lanc_run(self, niter: int, v0_dev=None, real: Optional[bool] = None):
+        """Fixed-length device Lanczos (benchmark): returns (alpha, beta, ms)."""
+        vt = 0 if (self.real if real is None else real) else 1
+        a = np.zeros(niter)
+        b = np.zeros(niter)
+        ms = ctypes.c_float()
+        check(_lib.load().ed_sector_lanc_run(self._h, vt,
+                                             None if v0_dev is None else _tptr(v0_dev), niter,
+                                             _ptr(a), _ptr(b), ctypes.byref(ms), None),
+              "lanc_run")
+        return a, b, float(ms.value)
+
+    def _vec_arg(self, v0, real):
+        use_real = self.real if real is None else real
+        vt = 0 if use_real else 1
+        if v0 is None:
+            return vt, None
+        arr = np.ascontiguousarray(v0, dtype=np.float64 if vt == 0 else np.complex128)
+        if arr.shape != (self.dim,):
+            raise ValueError("start vector length != dim")
+        self._keep = arr
+        return vt, _ptr(arr)
+
+
+# ------------------------------------------------------------ reference API
+_current: Optional[Sector] = None
+
+
+def build_Hv_sector(cfg: EDConfig, isector: int, *, sparse_H: bool = True,
+                    real: bool = False, device: int = 0) -> Sector:
+    """build_Hv_sector(isector) (ED_HAMILTONIAN.f90:42-103): ed_sparse_H selects
+    stored (T) or matrix-free (F) H·v for the current sector."""
+    global _current
+    sec: SectorId = setup_pointers(cfg)[isector - 1]
+    if _current is not None:
+        _current.close()
+    _current = Sector(cfg, sec.q1, sec.q2, stored=sparse_H, direct=not sparse_H, real=real,
+                      device=device)
+    return _current
+
+
+def delete_Hv_sector() -> None:
+    global _current
+    if _current is not None:
+        _current.close()
+    _current = None
+
+
+def vecDim_Hv_sector(cfg: EDConfig, isector: int) -> int:
+    """Serial vecDim_Hv_sector: MpiQ=Dim, MpiR=0 (ED_HAMILTONIAN.f90:126-149)."""
+    return setup_pointers(cfg)[isector - 1].dim
+
+
+def spHtimesV_cc(Nloc: int, v: np.ndarray, Hv: np.ndarray) -> None:
+    """The procedure bound by build_Hv_sector: Hv = H v, overwriting Hv."""
+    if _current is None:
+        raise RuntimeError("spHtimesV_cc ERROR: Hsector NOT set")
+    if Nloc != _current.dim:
+        raise ValueError("spHtimesV_cc ERROR: Nloc != dim(isector)")
+    Hv[:] = _current.hxv(v)

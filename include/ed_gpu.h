@@ -1,0 +1,180 @@
+/*
+ * ed_gpu.h — C-ABI of the MI355X-native Lanczos H·v hot path for dmft-ed.
+ *
+ * This is the drop-in boundary.  Every entry point is `extern "C"`, takes plain
+ * pointers and sizes, returns an int status (ED_OK = 0) and leaves a message in
+ * ed_gpu_last_error() on failure.  Nothing here mentions torch or HIP types:
+ * streams are passed as `void*` (a hipStream_t, or NULL for the default stream).
+ *
+ * Two layers:
+ *   1. Reference-shaped global API (ed_gpu_init / ed_gpu_build_sector /
+ *      ed_gpu_hxv / ed_gpu_delete_sector ...).  It keeps one "current sector",
+ *      exactly like the module state Hsector/H/spH0 of the reference, so that a
+ *      Fortran procedure pointer with the cc_sparse_HxV interface can call it
+ *      unchanged (see dmft-ed_amd/fortran/ed_gpu_hxv.f90 and INTEGRATION.md).
+ *   2. Handle API (ed_sector_*) used by the sector / Green's-function seed farm,
+ *      where many sectors live at once on several GPUs.
+ *
+ * Reference interfaces replaced (paths relative to the reference root):
+ *   ed_params                 <- effective_bath (ED_VARS_GLOBAL.f90:12-22), impHloc
+ *                                (ED_VARS_GLOBAL.f90:73), Uloc/Ust/Jh/Jx/Jp/xmu/hfmode
+ *                                (ED_INPUT_VARS.f90:17-31), Jhflag (ED_SETUP.f90:289-290)
+ *   ed_gpu_build_sector       <- build_Hv_sector        ED_HAMILTONIAN.f90:42-103
+ *                                (+ build_sector ED_SETUP.f90:886-984,
+ *                                   ed_buildH_c ED_HAMILTONIAN_STORED_HxV.f90:28-113)
+ *   ed_gpu_hxv                <- cc_sparse_HxV          ED_VARS_GLOBAL.f90:48-54
+ *                                = spMatVec_cc          ED_HAMILTONIAN_STORED_HxV.f90:132-143
+ *                                / directMatVec_cc      ED_HAMILTONIAN_DIRECT_HxV.f90:21-92
+ *   ed_gpu_delete_sector      <- delete_Hv_sector       ED_HAMILTONIAN.f90:106-123
+ *                                (safe after a direct build, unlike the reference)
+ *   ed_gpu_vecdim             <- vecDim_Hv_sector       ED_HAMILTONIAN.f90:126-149
+ *   ed_gpu_dump_csr           <- sp_dump_matrix         ED_SPARSE_MATRIX.f90:331-388
+ *                                (row-of-arrays order of sp_insert_element :249-320)
+ *   ed_gpu_lanc_eigh          <- sp_lanc_eigh (SciFortran; spec .repo/PLAIN_LANCZOS.f90:286-385)
+ *   ed_gpu_lanc_tridiag       <- sp_lanc_tridiag (SciFortran; spec .repo/PLAIN_LANCZOS.f90:154-180)
+ */
+#ifndef ED_GPU_H
+#define ED_GPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- limits */
+#define ED_MAX_NORB  3   /* ed_checks_global: Norb<=3  (ED_SETUP.f90:56) */
+#define ED_MAX_NSPIN 2   /* ed_checks_global: Nspin<=2 (ED_SETUP.f90:55) */
+#define ED_MAX_NBATH 32
+#define ED_MAX_NS    16  /* levels per spin: states are 2*Ns <= 32 bit words */
+
+/* ---------------------------------------------------------------- enums */
+#define ED_MODE_NORMAL 0 /* ed_mode='normal' : sectors (nup,ndw)        */
+#define ED_MODE_SUPERC 1 /* ed_mode='superc' : sectors sz = nup-ndw     */
+#define ED_MODE_NONSU2 2 /* ed_mode='nonsu2' : sectors n  = nup+ndw     */
+
+#define ED_BATH_NORMAL  0 /* bath_type='normal'  */
+#define ED_BATH_HYBRID  1 /* bath_type='hybrid'  */
+#define ED_BATH_REPLICA 2 /* bath_type='replica' */
+
+/* build flags (bit set) */
+#define ED_STORED 0x1 /* ed_sparse_H=T: assemble H on the device (SELL-64 layout) */
+#define ED_DIRECT 0x2 /* ed_sparse_H=F: matrix-free H·v, elements regenerated     */
+#define ED_REAL   0x4 /* store H as real(8) (only when impHloc and bath are real) */
+
+/* status codes */
+#define ED_OK              0
+#define ED_ERR_ARG         1
+#define ED_ERR_STATE       2
+#define ED_ERR_HIP         3
+#define ED_ERR_OOM         4
+#define ED_ERR_UNSUPPORTED 5
+
+/* ---------------------------------------------------------------- params
+ * All arrays are C row-major over the MAXIMUM dimensions below; only the
+ * leading [nspin][nspin][norb][norb][nbath] part is read.  Index i of a C array
+ * here is Fortran index i+1 of the reference array.
+ *   imphloc_*[ispin][jspin][iorb][jorb]      = impHloc(ispin+1,jspin+1,iorb+1,jorb+1)
+ *   bath_e[ispin][iorb][k]                   = dmft_bath%e(ispin+1,iorb+1,k+1)
+ *     (bath_type='hybrid': only iorb=0 is used, as size(e,2)=1)
+ *   bath_v/u/d[ispin][iorb][k]               = dmft_bath%v/u/d(...)
+ *   bath_h_*[ispin][jspin][iorb][jorb][k]    = dmft_bath%h(...)   (replica)
+ *   bath_vr_*[k]                             = dmft_bath%vr(k+1)  (replica)
+ */
+typedef struct ed_params {
+  int32_t norb, nspin, nbath;
+  int32_t ed_mode;   /* ED_MODE_*  */
+  int32_t bath_type; /* ED_BATH_*  */
+  int32_t hfmode;    /* logical    */
+  double uloc[3];
+  double ust, jh, jx, jp, xmu;
+  double imphloc_re[ED_MAX_NSPIN][ED_MAX_NSPIN][ED_MAX_NORB][ED_MAX_NORB];
+  double imphloc_im[ED_MAX_NSPIN][ED_MAX_NSPIN][ED_MAX_NORB][ED_MAX_NORB];
+  double bath_e[ED_MAX_NSPIN][ED_MAX_NORB][ED_MAX_NBATH];
+  double bath_v[ED_MAX_NSPIN][ED_MAX_NORB][ED_MAX_NBATH];
+  double bath_u[ED_MAX_NSPIN][ED_MAX_NORB][ED_MAX_NBATH];
+  double bath_d[ED_MAX_NSPIN][ED_MAX_NORB][ED_MAX_NBATH];
+  double bath_h_re[ED_MAX_NSPIN][ED_MAX_NSPIN][ED_MAX_NORB][ED_MAX_NORB][ED_MAX_NBATH];
+  double bath_h_im[ED_MAX_NSPIN][ED_MAX_NSPIN][ED_MAX_NORB][ED_MAX_NORB][ED_MAX_NBATH];
+  double bath_vr_re[ED_MAX_NBATH];
+  double bath_vr_im[ED_MAX_NBATH];
+} ed_params;
+
+typedef struct ed_sector_info {
+  int64_t dim;      /* getDim(isector)                                  */
+  int64_t nnz;      /* stored elements incl. diagonal (0 for direct)    */
+  int64_t padded;   /* SELL-64 slots actually stored (>= nnz - dim)     */
+  int32_t ns;       /* levels per spin                                  */
+  int32_t mode;     /* ED_MODE_*                                        */
+  int32_t q1, q2;   /* (nup,ndw) | (sz,0) | (n,0)                       */
+  int32_t flags;    /* ED_STORED|ED_DIRECT|ED_REAL as built             */
+  int32_t kron;     /* 1 if the direct path uses the (DimUp x DimDw) form */
+  int64_t dimup, dimdw;   /* factor dimensions (normal mode), else 0    */
+  int64_t device_bytes;   /* device memory held by the sector           */
+} ed_sector_info;
+
+typedef struct ed_sector ed_sector; /* opaque */
+
+/* ------------------------------------------------------------ handle API */
+/* Build the sector basis and (ED_STORED) the Hamiltonian on `device`.
+ * q1,q2: (nup,ndw) for normal, (sz,-) for superc, (n,-) for nonsu2. */
+int ed_sector_create(const ed_params* p, int32_t q1, int32_t q2, int32_t flags,
+                     int32_t device, void* stream, ed_sector** out);
+int ed_sector_destroy(ed_sector* s);
+int ed_sector_get_info(const ed_sector* s, ed_sector_info* info);
+
+/* H·v on device pointers (async on `stream`).  vtype: 0 = real(8) vectors,
+ * 1 = complex(8) interleaved vectors.  hv is overwritten (not accumulated),
+ * as spMatVec_cc does (Hv=zero first, STORED_HxV.f90:137). */
+int ed_sector_hxv_dev(ed_sector* s, int32_t vtype, const void* v, void* hv, void* stream);
+/* Same, forcing the matrix-free kernel even on a stored sector (1) or the
+ * stored kernel (0). -1 = default for the sector. */
+int ed_sector_hxv_dev_path(ed_sector* s, int32_t path, int32_t vtype, const void* v,
+                           void* hv, void* stream);
+/* Host-pointer H·v (synchronous, complex(8) vectors of length nloc = dim). */
+int ed_sector_hxv(ed_sector* s, int32_t nloc, const double* v, double* hv);
+
+/* H%map(1:dim): the Fock states of the sector in reference order (uint32). */
+int ed_sector_map(const ed_sector* s, uint32_t* map_host);
+/* Dump the stored H in reference row order (diagonal first, then off-diagonal
+ * elements in insertion order).  rowptr[dim+1], cols[nnz] are 0-based;
+ * vals is complex interleaved (2*nnz doubles).  Requires ED_STORED. */
+int ed_sector_dump_csr(const ed_sector* s, int64_t* rowptr, int32_t* cols, double* vals);
+
+/* Device-resident plain Lanczos (3-term recurrence, no reorthogonalisation).
+ * v0: host start vector (vtype as above) of length dim, or NULL for the
+ * deterministic default start vector.  Outputs on the host. */
+int ed_sector_lanc_tridiag(ed_sector* s, int32_t vtype, const void* v0, int32_t nitermax,
+                           double threshold, double* alfa, double* beta, int32_t* nlanc);
+/* Ground state: returns egs (lowest Ritz value) and, if vect != NULL, the
+ * normalised Ritz vector (host, vtype).  ncheck as lanczos_plain_c. */
+int ed_sector_lanc_eigh(ed_sector* s, int32_t vtype, const void* v0, int32_t nitermax,
+                        double threshold, int32_t ncheck, double* egs, void* vect,
+                        int32_t* nlanc);
+/* Fixed-length Lanczos on device pointers for benchmarking: runs exactly
+ * `niter` iterations (no convergence test) from device vector v0 and writes
+ * alfa/beta (host).  Returns the elapsed device time in ms in *ms (or NULL). */
+int ed_sector_lanc_run(ed_sector* s, int32_t vtype, const void* v0_dev, int32_t niter,
+                       double* alfa, double* beta, float* ms, void* stream);
+
+/* ------------------------------------------------------ reference-style API */
+int ed_gpu_init(const ed_params* p);          /* ed_init_solver parameter hand-over */
+int ed_gpu_set_device(int32_t device);
+int ed_gpu_build_sector(int32_t q1, int32_t q2, int32_t flags, int64_t* dim);
+int ed_gpu_vecdim(int32_t* vecdim);           /* vecDim_Hv_sector of the current sector */
+/* cc_sparse_HxV(Nloc,v,Hv): Nloc by reference, complex(8) host arrays. */
+int ed_gpu_hxv(const int32_t* nloc, const double* v, double* hv);
+int ed_gpu_dump_csr(int64_t* rowptr, int32_t* cols, double* vals);
+int ed_gpu_lanc_eigh(int32_t nitermax, double threshold, int32_t ncheck, double* egs,
+                     double* vect, int32_t* nlanc);
+int ed_gpu_lanc_tridiag(const double* v0, int32_t nitermax, double threshold,
+                        double* alfa, double* beta, int32_t* nlanc);
+int ed_gpu_delete_sector(void);
+int ed_gpu_finalize(void);
+const char* ed_gpu_last_error(void);
+int ed_gpu_current_sector(ed_sector** out);   /* handle of the current sector */
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ED_GPU_H */

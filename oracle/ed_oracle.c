@@ -1,0 +1,1019 @@
+/*
+ * ed_oracle.c — CPU restatement of the dmft-ed Lanczos H·v hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (dmft-ed_amd/) links, loads
+ * or calls this file; only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg do, and only as the checker / CPU baseline.
+ *
+ * Every function restates one reference routine literally (same loops, same
+ * insertion order, same floating-point operation order) and cites it.  Paths
+ * are relative to the reference root.  The reference itself is Fortran that
+ * needs SciFortran + MPI (absent from this image), so it cannot be built here
+ * without writing stand-ins for those libraries; see DESIGN.md "Oracle".
+ *
+ * Parity pinning: the restatement reproduces the reference outputs recorded
+ * in SURVEY.md §6/§8a (sector dims, nnz, ground-state energies) — see
+ * tests/golden/survey_pins.json and tests/test_oracle.py.
+ *
+ * Build: cc -O2 -ffp-contract=off -shared -fPIC (oracle/Makefile).
+ * FP contraction is off on purpose: the reference expressions are evaluated
+ * one IEEE operation at a time, in source order.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../include/ed_gpu.h"
+
+typedef struct { double re, im; } cplx;
+
+/* ------------------------------------------------------------------ model */
+typedef struct {
+  const ed_params* p;
+  int ns, norb, nbath, nspin, S; /* S = Nspin-1 : Fortran index Nspin -> C index */
+  int mode, bath;
+  int jhflag;
+  int stride[ED_MAX_NORB][ED_MAX_NBATH]; /* getBathStride, 0-based bit position */
+  int ne;                                 /* size(dmft_bath%e,2) */
+} model_t;
+
+/* ed_setup_dimensions ED_SETUP.f90:96-111 ; getBathStride ED_SETUP.f90:448-465 */
+static int model_init(model_t* M, const ed_params* p) {
+  memset(M, 0, sizeof(*M));
+  M->p = p;
+  M->norb = p->norb; M->nbath = p->nbath; M->nspin = p->nspin; M->S = p->nspin - 1;
+  M->mode = p->ed_mode; M->bath = p->bath_type;
+  if (p->norb < 1 || p->norb > ED_MAX_NORB || p->nspin < 1 || p->nspin > ED_MAX_NSPIN ||
+      p->nbath < 0 || p->nbath > ED_MAX_NBATH)
+    return -1;
+  switch (p->bath_type) {
+    case ED_BATH_HYBRID: M->ns = p->nbath + p->norb; break;
+    default: M->ns = (p->nbath + 1) * p->norb; break; /* normal and replica */
+  }
+  if (M->ns > ED_MAX_NS) return -1;
+  for (int k = 0; k < p->nbath; k++)
+    for (int o = 0; o < p->norb; o++) {
+      /* Fortran: Norb+(iorb-1)*Nbath+i | Norb+i | iorb+i*Norb  (1-based level) */
+      int lev;
+      if (p->bath_type == ED_BATH_HYBRID) lev = p->norb + (k + 1);
+      else if (p->bath_type == ED_BATH_REPLICA) lev = (o + 1) + (k + 1) * p->norb;
+      else lev = p->norb + o * p->nbath + (k + 1);
+      M->stride[o][k] = lev - 1;
+    }
+  M->ne = (p->bath_type == ED_BATH_HYBRID) ? 1 : p->norb;
+  /* Jhflag: ED_SETUP.f90:289-290 */
+  M->jhflag = (p->norb > 1 && (p->jx != 0.0 || p->jp != 0.0));
+  return 0;
+}
+
+int orc_ns(const ed_params* p) {
+  model_t M;
+  if (model_init(&M, p)) return -1;
+  return M.ns;
+}
+
+static inline int popc(uint32_t x) { return __builtin_popcount(x); }
+static inline int btest(uint32_t x, int b) { return (x >> b) & 1u; }
+
+/* c / cdg  ED_SETUP.f90:1080-1106 (pos here is the 0-based bit = Fortran pos-1) */
+static inline void op_c(int b, uint32_t in, uint32_t* out, double* sg) {
+  double f = 1.0;
+  for (int l = 0; l < b; l++)
+    if (btest(in, l)) f = -f;
+  *sg = f;
+  *out = in & ~(1u << b);
+}
+static inline void op_cdg(int b, uint32_t in, uint32_t* out, double* sg) {
+  double f = 1.0;
+  for (int l = 0; l < b; l++)
+    if (btest(in, l)) f = -f;
+  *sg = f;
+  *out = in | (1u << b);
+}
+
+/* binary_search ED_SETUP.f90:1307-1324 (recursion unrolled; returns 1-based
+ * position, 0 if absent). */
+static int64_t bsearch_ref(const uint32_t* a, int64_t n, uint32_t value) {
+  int64_t base = 0; /* 1-based offset accumulated over right descents */
+  while (1) {
+    if (n == 0) return 0;
+    int64_t mid = n / 2 + 1; /* 1-based */
+    uint32_t am = a[mid - 1];
+    if (am > value) {
+      n = mid - 1;
+    } else if (am < value) {
+      a += mid;
+      n = n - mid;
+      base += mid;
+    } else {
+      return base + mid;
+    }
+  }
+}
+
+/* ------------------------------------------------------------------ basis */
+/* build_sector ED_SETUP.f90:886-984 (Jz_basis=F).  map may be NULL (count). */
+int64_t orc_build_sector(const ed_params* p, int32_t q1, int32_t q2, uint32_t* map) {
+  model_t M;
+  if (model_init(&M, p)) return -1;
+  const int ns = M.ns;
+  const uint32_t nst = 1u << ns;
+  int64_t dim = 0;
+  for (uint32_t idw = 0; idw < nst; idw++) {
+    int ndw_ = popc(idw);
+    if (M.mode == ED_MODE_NORMAL && ndw_ != q2) continue;
+    for (uint32_t iup = 0; iup < nst; iup++) {
+      int nup_ = popc(iup);
+      int keep;
+      if (M.mode == ED_MODE_NORMAL) keep = (nup_ == q1);
+      else if (M.mode == ED_MODE_SUPERC) keep = (nup_ - ndw_ == q1);
+      else keep = (nup_ + ndw_ == q1);
+      if (!keep) continue;
+      if (map) map[dim] = iup + idw * nst;
+      dim++;
+    }
+  }
+  return dim;
+}
+
+/* ------------------------------------------------------------ element emit */
+typedef struct {
+  /* stored row in reference insertion order with sp_insert_element merge
+   * semantics (ED_SPARSE_MATRIX.f90:249-279) */
+  int64_t n, cap;
+  int32_t* cols;
+  cplx* vals;
+  int overflow;
+} rowbuf;
+
+static void row_insert(rowbuf* r, int32_t col, cplx v) {
+  for (int64_t q = 0; q < r->n; q++)
+    if (r->cols[q] == col) { /* column exists: add up (:271) */
+      r->vals[q].re = r->vals[q].re + v.re;
+      r->vals[q].im = r->vals[q].im + v.im;
+      return;
+    }
+  if (r->n >= r->cap) { r->overflow = 1; return; }
+  r->cols[r->n] = col; /* new column: append (:273-276) */
+  r->vals[r->n] = v;
+  r->n++;
+}
+
+#define HLOC_RE(is, js, io, jo) (p->imphloc_re[is][js][io][jo])
+#define HLOC_IM(is, js, io, jo) (p->imphloc_im[is][js][io][jo])
+#define HB_RE(is, js, io, jo, k) (p->bath_h_re[is][js][io][jo][k])
+#define HB_IM(is, js, io, jo, k) (p->bath_h_im[is][js][io][jo][k])
+
+static inline cplx cscale2(cplx a, double s1, double s2) {
+  cplx r;
+  r.re = (a.re * s1) * s2;
+  r.im = (a.im * s1) * s2;
+  return r;
+}
+static inline cplx mkc(double re, double im) { cplx c; c.re = re; c.im = im; return c; }
+
+/* diag_hybr  ED_HAMILTONIAN_STORED_HxV.f90:58-70 */
+static inline cplx diag_hybr(const model_t* M, int ispin, int o, int k) {
+  const ed_params* p = M->p;
+  if (M->bath != ED_BATH_REPLICA) return mkc(p->bath_v[ispin][o][k], 0.0);
+  return mkc(p->bath_vr_re[k], p->bath_vr_im[k]);
+}
+
+/* Hint diagonal (shared by stored Hint.f90:117-155 and direct HxVint.f90:1-47) */
+static double hint_diag(const model_t* M, const double* nup, const double* ndw) {
+  const ed_params* p = M->p;
+  const int norb = M->norb;
+  double h = 0.0;
+  for (int o = 0; o < norb; o++) h = h + (p->uloc[o] * nup[o]) * ndw[o];
+  if (norb > 1) {
+    for (int o = 0; o < norb; o++)
+      for (int q = o + 1; q < norb; q++) h = h + p->ust * (nup[o] * ndw[q] + nup[q] * ndw[o]);
+    for (int o = 0; o < norb; o++)
+      for (int q = o + 1; q < norb; q++)
+        h = h + (p->ust - p->jh) * (nup[o] * nup[q] + ndw[o] * ndw[q]);
+  }
+  if (p->hfmode) {
+    for (int o = 0; o < norb; o++)
+      h = (h - (0.5 * p->uloc[o]) * (nup[o] + ndw[o])) + 0.25 * p->uloc[o];
+    if (norb > 1)
+      for (int o = 0; o < norb; o++)
+        for (int q = o + 1; q < norb; q++) {
+          double nn = ((nup[o] + ndw[o]) + nup[q]) + ndw[q];
+          h = (h - (0.5 * p->ust) * nn) + 0.25 * p->ust;
+          h = (h - (0.5 * (p->ust - p->jh)) * nn) + 0.25 * (p->ust - p->jh);
+        }
+  }
+  return h;
+}
+
+/*
+ * One row of ed_buildH_c (ED_HAMILTONIAN_STORED_HxV.f90:28-113): the four
+ * include loops (stored/Himp.f90, Hint.f90, Hbath.f90, Himp_bath.f90) visit row
+ * i in that order, so the row content is their concatenation with merges.
+ */
+static int stored_row(const model_t* M, const uint32_t* map, int64_t dim, int64_t i,
+                      rowbuf* R) {
+  const ed_params* p = M->p;
+  const int ns = M->ns, norb = M->norb, nbath = M->nbath, S = M->S;
+  const uint32_t m = map[i];
+  double nup[ED_MAX_NORB], ndw[ED_MAX_NORB];
+  uint32_t k1, k2, k3, k4;
+  double sg1, sg2, sg3, sg4;
+  int64_t j;
+  for (int o = 0; o < norb; o++) {
+    nup[o] = (double)btest(m, o);
+    ndw[o] = (double)btest(m, o + ns);
+  }
+#define LOOKUP(state) (j = bsearch_ref(map, dim, (state)))
+#define INSERT(val)                           \
+  do {                                        \
+    if (j == 0) return -2;                    \
+    row_insert(R, (int32_t)(j - 1), (val));   \
+  } while (0)
+
+  /* ---- stored/Himp.f90:10-23  diagonal */
+  {
+    double hr = 0.0, hi = 0.0;
+    for (int o = 0; o < norb; o++) {
+      hr = hr + HLOC_RE(0, 0, o, o) * nup[o];
+      hi = hi + HLOC_IM(0, 0, o, o) * nup[o];
+      hr = hr + HLOC_RE(S, S, o, o) * ndw[o];
+      hi = hi + HLOC_IM(S, S, o, o) * ndw[o];
+      hr = hr - p->xmu * (nup[o] + ndw[o]);
+    }
+    j = i + 1;
+    INSERT(mkc(hr, hi));
+  }
+  /* ---- stored/Himp.f90:27-72  same-spin impurity hops */
+  for (int io = 0; io < norb; io++)
+    for (int jo = 0; jo < norb; jo++) {
+      if ((HLOC_RE(0, 0, io, jo) != 0.0 || HLOC_IM(0, 0, io, jo) != 0.0) && btest(m, jo) == 1 &&
+          btest(m, io) == 0) {
+        op_c(jo, m, &k1, &sg1);
+        op_cdg(io, k1, &k2, &sg2);
+        LOOKUP(k2);
+        INSERT(cscale2(mkc(HLOC_RE(0, 0, io, jo), -HLOC_IM(0, 0, io, jo)), sg1, sg2));
+      }
+      if ((HLOC_RE(S, S, io, jo) != 0.0 || HLOC_IM(S, S, io, jo) != 0.0) &&
+          btest(m, jo + ns) == 1 && btest(m, io + ns) == 0) {
+        op_c(jo + ns, m, &k1, &sg1);
+        op_cdg(io + ns, k1, &k2, &sg2);
+        LOOKUP(k2);
+        INSERT(cscale2(mkc(HLOC_RE(S, S, io, jo), -HLOC_IM(S, S, io, jo)), sg1, sg2));
+      }
+    }
+  /* ---- stored/Himp.f90:74-104  nonSU2 spin-flip part of impHloc */
+  if (M->mode == ED_MODE_NONSU2) {
+    for (int is = 0; is < M->nspin; is++) {
+      int js = 1 - is;
+      for (int io = 0; io < norb; io++)
+        for (int jo = 0; jo < norb; jo++) {
+          int alfa = io + is * ns, beta = jo + js * ns;
+          if ((HLOC_RE(is, js, io, jo) != 0.0 || HLOC_IM(is, js, io, jo) != 0.0) &&
+              btest(m, beta) == 1 && btest(m, alfa) == 0) {
+            op_c(beta, m, &k1, &sg1);
+            op_cdg(alfa, k1, &k2, &sg2);
+            LOOKUP(k2);
+            INSERT(cscale2(mkc(HLOC_RE(is, js, io, jo), -HLOC_IM(is, js, io, jo)), sg1, sg2));
+          }
+        }
+    }
+  }
+  /* ---- stored/Hint.f90:117-162  density-density (+ Hartree) merged on (i,i) */
+  {
+    double h = hint_diag(M, nup, ndw);
+    j = i + 1;
+    INSERT(mkc(h, 0.0));
+  }
+  /* ---- stored/Hint.f90:169-196  spin exchange */
+  if (norb > 1 && M->jhflag) {
+    for (int io = 0; io < norb; io++)
+      for (int jo = 0; jo < norb; jo++) {
+        if (io != jo && btest(m, jo) == 1 && btest(m, io + ns) == 1 && btest(m, jo + ns) == 0 &&
+            btest(m, io) == 0) {
+          op_c(jo, m, &k1, &sg1);
+          op_c(io + ns, k1, &k2, &sg2);
+          op_cdg(jo + ns, k2, &k3, &sg3);
+          op_cdg(io, k3, &k4, &sg4);
+          LOOKUP(k4);
+          double v = (((p->jx * sg1) * sg2) * sg3) * sg4;
+          INSERT(mkc(v, 0.0));
+        }
+      }
+  }
+  /* ---- stored/Hint.f90:202-229  pair hopping */
+  if (norb > 1 && M->jhflag) {
+    for (int io = 0; io < norb; io++)
+      for (int jo = 0; jo < norb; jo++) {
+        if (io != jo && btest(m, jo) == 1 && btest(m, jo + ns) == 1 && btest(m, io + ns) == 0 &&
+            btest(m, io) == 0) {
+          op_c(jo, m, &k1, &sg1);
+          op_c(jo + ns, k1, &k2, &sg2);
+          op_cdg(io + ns, k2, &k3, &sg3);
+          op_cdg(io, k3, &k4, &sg4);
+          LOOKUP(k4);
+          double v = (((p->jp * sg1) * sg2) * sg3) * sg4;
+          INSERT(mkc(v, 0.0));
+        }
+      }
+  }
+  /* ---- stored/Hbath.f90 */
+  if (M->bath != ED_BATH_REPLICA) {
+    /* :10-27 diagonal bath energies */
+    double h = 0.0;
+    for (int o = 0; o < M->ne; o++)
+      for (int k = 0; k < nbath; k++) {
+        int a = M->stride[o][k];
+        h = h + p->bath_e[0][o][k] * (double)btest(m, a);
+        h = h + p->bath_e[S][o][k] * (double)btest(m, a + ns);
+      }
+    j = i + 1;
+    INSERT(mkc(h, 0.0));
+  } else {
+    /* :32-47 replica diagonal */
+    double hr = 0.0, hi = 0.0;
+    for (int k = 0; k < nbath; k++)
+      for (int o = 0; o < norb; o++) {
+        int a = M->stride[o][k];
+        double nu = (double)btest(m, a), nd = (double)btest(m, a + ns);
+        hr = hr + HB_RE(0, 0, o, o, k) * nu;
+        hi = hi + HB_IM(0, 0, o, o, k) * nu;
+        hr = hr + HB_RE(S, S, o, o, k) * nd;
+        hi = hi + HB_IM(S, S, o, o, k) * nd;
+      }
+    j = i + 1;
+    INSERT(mkc(hr, hi));
+    /* :52-102 replica same-spin hops */
+    for (int k = 0; k < nbath; k++)
+      for (int io = 0; io < norb; io++)
+        for (int jo = 0; jo < norb; jo++) {
+          int alfa = M->stride[io][k], beta = M->stride[jo][k];
+          if ((HB_RE(0, 0, io, jo, k) != 0.0 || HB_IM(0, 0, io, jo, k) != 0.0) &&
+              btest(m, beta) == 1 && btest(m, alfa) == 0) {
+            op_c(beta, m, &k1, &sg1);
+            op_cdg(alfa, k1, &k2, &sg2);
+            LOOKUP(k2);
+            INSERT(cscale2(mkc(HB_RE(0, 0, io, jo, k), -HB_IM(0, 0, io, jo, k)), sg1, sg2));
+          }
+          alfa += ns;
+          beta += ns;
+          if ((HB_RE(S, S, io, jo, k) != 0.0 || HB_IM(S, S, io, jo, k) != 0.0) &&
+              btest(m, beta) == 1 && btest(m, alfa) == 0) {
+            op_c(beta, m, &k1, &sg1);
+            op_cdg(alfa, k1, &k2, &sg2);
+            LOOKUP(k2);
+            INSERT(cscale2(mkc(HB_RE(S, S, io, jo, k), -HB_IM(S, S, io, jo, k)), sg1, sg2));
+          }
+        }
+    /* :105-135 replica nonSU2 spin-flip hops */
+    if (M->mode == ED_MODE_NONSU2) {
+      for (int k = 0; k < nbath; k++)
+        for (int is = 0; is < M->nspin; is++) {
+          int js = 1 - is;
+          for (int io = 0; io < norb; io++)
+            for (int jo = 0; jo < norb; jo++) {
+              int alfa = M->stride[io][k] + is * ns, beta = M->stride[jo][k] + js * ns;
+              if ((HB_RE(is, js, io, jo, k) != 0.0 || HB_IM(is, js, io, jo, k) != 0.0) &&
+                  btest(m, beta) == 1 && btest(m, alfa) == 0) {
+                op_c(beta, m, &k1, &sg1);
+                op_cdg(alfa, k1, &k2, &sg2);
+                LOOKUP(k2);
+                INSERT(cscale2(mkc(HB_RE(is, js, io, jo, k), -HB_IM(is, js, io, jo, k)), sg1, sg2));
+              }
+            }
+        }
+    }
+  }
+  /* ---- stored/Hbath.f90:142-178  superconducting pair terms */
+  if (M->mode == ED_MODE_SUPERC) {
+    for (int o = 0; o < M->ne; o++)
+      for (int k = 0; k < nbath; k++) {
+        int ms = M->stride[o][k];
+        double d = p->bath_d[0][o][k];
+        if (d != 0.0 && btest(m, ms) == 1 && btest(m, ms + ns) == 1) {
+          op_c(ms, m, &k1, &sg1);
+          op_c(ms + ns, k1, &k2, &sg2);
+          LOOKUP(k2);
+          INSERT(mkc((d * sg1) * sg2, 0.0));
+        }
+        if (d != 0.0 && btest(m, ms) == 0 && btest(m, ms + ns) == 0) {
+          op_cdg(ms + ns, m, &k1, &sg1);
+          op_cdg(ms, k1, &k2, &sg2);
+          LOOKUP(k2);
+          INSERT(mkc((d * sg1) * sg2, 0.0));
+        }
+      }
+  }
+  /* ---- stored/Himp_bath.f90:192-249  spin-conserving hybridisation */
+  for (int o = 0; o < norb; o++)
+    for (int k = 0; k < nbath; k++) {
+      int ms = M->stride[o][k];
+      cplx hu = diag_hybr(M, 0, o, k), hd = diag_hybr(M, S, o, k);
+      int nzu = (hu.re != 0.0 || hu.im != 0.0), nzd = (hd.re != 0.0 || hd.im != 0.0);
+      if (nzu && btest(m, o) == 1 && btest(m, ms) == 0) {
+        op_c(o, m, &k1, &sg1);
+        op_cdg(ms, k1, &k2, &sg2);
+        LOOKUP(k2);
+        INSERT(cscale2(mkc(hu.re, -hu.im), sg1, sg2));
+      }
+      if (nzu && btest(m, o) == 0 && btest(m, ms) == 1) {
+        op_c(ms, m, &k1, &sg1);
+        op_cdg(o, k1, &k2, &sg2);
+        LOOKUP(k2);
+        INSERT(cscale2(mkc(hu.re, -hu.im), sg1, sg2));
+      }
+      if (nzd && btest(m, o + ns) == 1 && btest(m, ms + ns) == 0) {
+        op_c(o + ns, m, &k1, &sg1);
+        op_cdg(ms + ns, k1, &k2, &sg2);
+        LOOKUP(k2);
+        INSERT(cscale2(mkc(hd.re, -hd.im), sg1, sg2));
+      }
+      if (nzd && btest(m, o + ns) == 0 && btest(m, ms + ns) == 1) {
+        op_c(ms + ns, m, &k1, &sg1);
+        op_cdg(o + ns, k1, &k2, &sg2);
+        LOOKUP(k2);
+        INSERT(cscale2(mkc(hd.re, -hd.im), sg1, sg2));
+      }
+    }
+  /* ---- stored/Himp_bath.f90:253-310  nonSU2 spin-flip hybridisation (inserted even if u=0) */
+  if (M->mode == ED_MODE_NONSU2 && M->bath != ED_BATH_REPLICA) {
+    for (int o = 0; o < norb; o++)
+      for (int k = 0; k < nbath; k++) {
+        int ms = M->stride[o][k];
+        double uu = p->bath_u[0][o][k], ud = p->bath_u[S][o][k];
+        if (btest(m, o) == 1 && btest(m, ms + ns) == 0) {
+          op_c(o, m, &k1, &sg1);
+          op_cdg(ms + ns, k1, &k2, &sg2);
+          LOOKUP(k2);
+          INSERT(mkc((uu * sg1) * sg2, 0.0));
+        }
+        if (btest(m, o) == 0 && btest(m, ms + ns) == 1) {
+          op_c(ms + ns, m, &k1, &sg1);
+          op_cdg(o, k1, &k2, &sg2);
+          LOOKUP(k2);
+          INSERT(mkc((uu * sg1) * sg2, 0.0));
+        }
+        if (btest(m, o + ns) == 1 && btest(m, ms) == 0) {
+          op_c(o + ns, m, &k1, &sg1);
+          op_cdg(ms, k1, &k2, &sg2);
+          LOOKUP(k2);
+          INSERT(mkc((ud * sg1) * sg2, 0.0));
+        }
+        if (btest(m, o + ns) == 0 && btest(m, ms) == 1) {
+          op_c(ms, m, &k1, &sg1);
+          op_cdg(o + ns, k1, &k2, &sg2);
+          LOOKUP(k2);
+          INSERT(mkc((ud * sg1) * sg2, 0.0));
+        }
+      }
+  }
+#undef LOOKUP
+#undef INSERT
+  return R->overflow ? -3 : 0;
+}
+
+/*
+ * ed_buildH_c as a CSR in the row-of-arrays order of spH0.  rowptr[dim+1];
+ * cols/vals (complex interleaved) of capacity `cap`.  With cols == NULL only
+ * counts.  Returns nnz, or <0 on error.
+ */
+int64_t orc_build_csr(const ed_params* p, const uint32_t* map, int64_t dim, int64_t* rowptr,
+                      int32_t* cols, double* vals, int64_t cap) {
+  model_t M;
+  if (model_init(&M, p)) return -1;
+  enum { RMAX = 4096 };
+  int32_t* rc = (int32_t*)malloc(sizeof(int32_t) * RMAX);
+  cplx* rv = (cplx*)malloc(sizeof(cplx) * RMAX);
+  int64_t nnz = 0;
+  if (rowptr) rowptr[0] = 0;
+  for (int64_t i = 0; i < dim; i++) {
+    rowbuf R = {0, RMAX, rc, rv, 0};
+    int st = stored_row(&M, map, dim, i, &R);
+    if (st) { free(rc); free(rv); return st; }
+    if (cols) {
+      if (nnz + R.n > cap) { free(rc); free(rv); return -4; }
+      for (int64_t q = 0; q < R.n; q++) {
+        cols[nnz + q] = rc[q];
+        vals[2 * (nnz + q)] = rv[q].re;
+        vals[2 * (nnz + q) + 1] = rv[q].im;
+      }
+    }
+    nnz += R.n;
+    if (rowptr) rowptr[i + 1] = nnz;
+  }
+  free(rc);
+  free(rv);
+  return nnz;
+}
+
+/* spMatVec_cc ED_HAMILTONIAN_STORED_HxV.f90:132-143 : Hv=0; Hv(i)+=vals(j)*v(cols(j)) */
+void orc_spmv(int64_t dim, const int64_t* rowptr, const int32_t* cols, const double* vals,
+              const double* v, double* hv) {
+  for (int64_t i = 0; i < dim; i++) {
+    double ar = 0.0, ai = 0.0;
+    for (int64_t q = rowptr[i]; q < rowptr[i + 1]; q++) {
+      double hr = vals[2 * q], hi = vals[2 * q + 1];
+      double xr = v[2 * cols[q]], xi = v[2 * cols[q] + 1];
+      double pr = hr * xr - hi * xi;
+      double pi = hr * xi + hi * xr;
+      ar = ar + pr;
+      ai = ai + pi;
+    }
+    hv[2 * i] = ar;
+    hv[2 * i + 1] = ai;
+  }
+}
+
+/* real(8) variant of the same row-gather loop (new-build option):
+ * vals_re holds the real parts of a Hermitian-real H. */
+void orc_spmv_real(int64_t dim, const int64_t* rowptr, const int32_t* cols, const double* vals_re,
+                   const double* v, double* hv) {
+  for (int64_t i = 0; i < dim; i++) {
+    double a = 0.0;
+    for (int64_t q = rowptr[i]; q < rowptr[i + 1]; q++) a = a + vals_re[q] * v[cols[q]];
+    hv[i] = a;
+  }
+}
+
+/* ---------------------------------------------------------------- direct
+ * directMatVec_cc ED_HAMILTONIAN_DIRECT_HxV.f90:21-92 + direct/HxVimp.f90,
+ * HxVint.f90, HxVbath.f90, HxVimp_bath.f90: scatter form, hv(i) += H_ij vin(j)
+ * with H_ij = coeff*sg (not conjugated).
+ */
+int orc_direct_hxv(const ed_params* p, const uint32_t* map, int64_t dim, const double* vin,
+                   double* hv) {
+  model_t M;
+  if (model_init(&M, p)) return -1;
+  const int ns = M.ns, norb = M.norb, nbath = M.nbath, S = M.S;
+  for (int64_t q = 0; q < 2 * dim; q++) hv[q] = 0.0;
+  uint32_t k1, k2, k3, k4;
+  double sg1, sg2, sg3, sg4;
+#define SCAT(ii, hr_, hi_)                                             \
+  do {                                                                 \
+    int64_t _i = (ii);                                                 \
+    if (_i < 0) return -2;                                             \
+    double _hr = (hr_), _hi = (hi_);                                   \
+    double _xr = vin[2 * j], _xi = vin[2 * j + 1];                     \
+    hv[2 * _i] = hv[2 * _i] + (_hr * _xr - _hi * _xi);                 \
+    hv[2 * _i + 1] = hv[2 * _i + 1] + (_hr * _xi + _hi * _xr);         \
+  } while (0)
+#define FIND(state) (bsearch_ref(map, dim, (state)) - 1)
+  for (int64_t j = 0; j < dim; j++) {
+    const uint32_t m = map[j];
+    double nup[ED_MAX_NORB], ndw[ED_MAX_NORB];
+    for (int o = 0; o < norb; o++) {
+      nup[o] = (double)btest(m, o);
+      ndw[o] = (double)btest(m, o + ns);
+    }
+    /* HxVimp.f90:1-11 */
+    {
+      double su = 0.0, sd = 0.0;
+      for (int o = 0; o < norb; o++) su = su + nup[o];
+      for (int o = 0; o < norb; o++) sd = sd + ndw[o];
+      double hr = 0.0 - p->xmu * (su + sd), hi = 0.0;
+      for (int o = 0; o < norb; o++) {
+        hr = hr + HLOC_RE(0, 0, o, o) * nup[o];
+        hi = hi + HLOC_IM(0, 0, o, o) * nup[o];
+        hr = hr + HLOC_RE(S, S, o, o) * ndw[o];
+        hi = hi + HLOC_IM(S, S, o, o) * ndw[o];
+      }
+      SCAT(j, hr, hi);
+    }
+    /* HxVimp.f90:16-49 */
+    for (int io = 0; io < norb; io++)
+      for (int jo = 0; jo < norb; jo++) {
+        if ((HLOC_RE(0, 0, io, jo) != 0.0 || HLOC_IM(0, 0, io, jo) != 0.0) && btest(m, jo) == 1 &&
+            btest(m, io) == 0) {
+          op_c(jo, m, &k1, &sg1);
+          op_cdg(io, k1, &k2, &sg2);
+          cplx h = cscale2(mkc(HLOC_RE(0, 0, io, jo), HLOC_IM(0, 0, io, jo)), sg1, sg2);
+          SCAT(FIND(k2), h.re, h.im);
+        }
+        if ((HLOC_RE(S, S, io, jo) != 0.0 || HLOC_IM(S, S, io, jo) != 0.0) &&
+            btest(m, jo + ns) == 1 && btest(m, io + ns) == 0) {
+          op_c(jo + ns, m, &k1, &sg1);
+          op_cdg(io + ns, k1, &k2, &sg2);
+          cplx h = cscale2(mkc(HLOC_RE(S, S, io, jo), HLOC_IM(S, S, io, jo)), sg1, sg2);
+          SCAT(FIND(k2), h.re, h.im);
+        }
+      }
+    /* HxVimp.f90:52-76 */
+    if (M.mode == ED_MODE_NONSU2) {
+      for (int is = 0; is < M.nspin; is++) {
+        int js = 1 - is;
+        for (int io = 0; io < norb; io++)
+          for (int jo = 0; jo < norb; jo++) {
+            int alfa = io + is * ns, beta = jo + js * ns;
+            if ((HLOC_RE(is, js, io, jo) != 0.0 || HLOC_IM(is, js, io, jo) != 0.0) &&
+                btest(m, beta) == 1 && btest(m, alfa) == 0) {
+              op_c(beta, m, &k1, &sg1);
+              op_cdg(alfa, k1, &k2, &sg2);
+              cplx h = cscale2(mkc(HLOC_RE(is, js, io, jo), HLOC_IM(is, js, io, jo)), sg1, sg2);
+              SCAT(FIND(k2), h.re, h.im);
+            }
+          }
+      }
+    }
+    /* HxVint.f90:1-49 */
+    SCAT(j, hint_diag(&M, nup, ndw), 0.0);
+    /* HxVint.f90:53-98 (only these guard i/=0) */
+    if (norb > 1 && M.jhflag) {
+      for (int io = 0; io < norb; io++)
+        for (int jo = 0; jo < norb; jo++)
+          if (io != jo && btest(m, jo) == 1 && btest(m, io + ns) == 1 && btest(m, jo + ns) == 0 &&
+              btest(m, io) == 0) {
+            op_c(jo, m, &k1, &sg1);
+            op_c(io + ns, k1, &k2, &sg2);
+            op_cdg(jo + ns, k2, &k3, &sg3);
+            op_cdg(io, k3, &k4, &sg4);
+            int64_t ii = FIND(k4);
+            if (ii >= 0) SCAT(ii, (((p->jx * sg1) * sg2) * sg3) * sg4, 0.0);
+          }
+      for (int io = 0; io < norb; io++)
+        for (int jo = 0; jo < norb; jo++)
+          if (io != jo && btest(m, jo) == 1 && btest(m, jo + ns) == 1 && btest(m, io + ns) == 0 &&
+              btest(m, io) == 0) {
+            op_c(jo, m, &k1, &sg1);
+            op_c(jo + ns, k1, &k2, &sg2);
+            op_cdg(io + ns, k2, &k3, &sg3);
+            op_cdg(io, k3, &k4, &sg4);
+            int64_t ii = FIND(k4);
+            if (ii >= 0) SCAT(ii, (((p->jp * sg1) * sg2) * sg3) * sg4, 0.0);
+          }
+    }
+    /* HxVbath.f90 */
+    if (M.bath != ED_BATH_REPLICA) {
+      double h = 0.0;
+      for (int o = 0; o < M.ne; o++)
+        for (int k = 0; k < nbath; k++) {
+          int a = M.stride[o][k];
+          h = h + p->bath_e[0][o][k] * (double)btest(m, a);
+          h = h + p->bath_e[S][o][k] * (double)btest(m, a + ns);
+        }
+      SCAT(j, h, 0.0);
+    } else {
+      double hr = 0.0, hi = 0.0;
+      for (int k = 0; k < nbath; k++)
+        for (int o = 0; o < norb; o++) {
+          int a = M.stride[o][k];
+          double nu = (double)btest(m, a), nd = (double)btest(m, a + ns);
+          hr = hr + HB_RE(0, 0, o, o, k) * nu;
+          hi = hi + HB_IM(0, 0, o, o, k) * nu;
+          hr = hr + HB_RE(S, S, o, o, k) * nd;
+          hi = hi + HB_IM(S, S, o, o, k) * nd;
+        }
+      SCAT(j, hr, hi);
+      for (int k = 0; k < nbath; k++)
+        for (int io = 0; io < norb; io++)
+          for (int jo = 0; jo < norb; jo++) {
+            int alfa = M.stride[io][k], beta = M.stride[jo][k];
+            if ((HB_RE(0, 0, io, jo, k) != 0.0 || HB_IM(0, 0, io, jo, k) != 0.0) &&
+                btest(m, beta) == 1 && btest(m, alfa) == 0) {
+              op_c(beta, m, &k1, &sg1);
+              op_cdg(alfa, k1, &k2, &sg2);
+              cplx h = cscale2(mkc(HB_RE(0, 0, io, jo, k), HB_IM(0, 0, io, jo, k)), sg1, sg2);
+              SCAT(FIND(k2), h.re, h.im);
+            }
+            alfa += ns;
+            beta += ns;
+            if ((HB_RE(S, S, io, jo, k) != 0.0 || HB_IM(S, S, io, jo, k) != 0.0) &&
+                btest(m, beta) == 1 && btest(m, alfa) == 0) {
+              op_c(beta, m, &k1, &sg1);
+              op_cdg(alfa, k1, &k2, &sg2);
+              cplx h = cscale2(mkc(HB_RE(S, S, io, jo, k), HB_IM(S, S, io, jo, k)), sg1, sg2);
+              SCAT(FIND(k2), h.re, h.im);
+            }
+          }
+      if (M.mode == ED_MODE_NONSU2) {
+        for (int k = 0; k < nbath; k++)
+          for (int is = 0; is < M.nspin; is++) {
+            int js = 1 - is;
+            for (int io = 0; io < norb; io++)
+              for (int jo = 0; jo < norb; jo++) {
+                int alfa = M.stride[io][k] + is * ns, beta = M.stride[jo][k] + js * ns;
+                if ((HB_RE(is, js, io, jo, k) != 0.0 || HB_IM(is, js, io, jo, k) != 0.0) &&
+                    btest(m, beta) == 1 && btest(m, alfa) == 0) {
+                  op_c(beta, m, &k1, &sg1);
+                  op_cdg(alfa, k1, &k2, &sg2);
+                  cplx h = cscale2(mkc(HB_RE(is, js, io, jo, k), HB_IM(is, js, io, jo, k)), sg1, sg2);
+                  SCAT(FIND(k2), h.re, h.im);
+                }
+              }
+          }
+      }
+    }
+    if (M.mode == ED_MODE_SUPERC) {
+      for (int o = 0; o < M.ne; o++)
+        for (int k = 0; k < nbath; k++) {
+          int ms = M.stride[o][k];
+          double d = p->bath_d[0][o][k];
+          if (d != 0.0 && btest(m, ms) == 1 && btest(m, ms + ns) == 1) {
+            op_c(ms, m, &k1, &sg1);
+            op_c(ms + ns, k1, &k2, &sg2);
+            SCAT(FIND(k2), (d * sg1) * sg2, 0.0);
+          }
+          if (d != 0.0 && btest(m, ms) == 0 && btest(m, ms + ns) == 0) {
+            op_cdg(ms + ns, m, &k1, &sg1);
+            op_cdg(ms, k1, &k2, &sg2);
+            SCAT(FIND(k2), (d * sg1) * sg2, 0.0);
+          }
+        }
+    }
+    /* HxVimp_bath.f90 */
+    for (int o = 0; o < norb; o++)
+      for (int k = 0; k < nbath; k++) {
+        int ms = M.stride[o][k];
+        cplx hu = diag_hybr(&M, 0, o, k), hd = diag_hybr(&M, S, o, k);
+        int nzu = (hu.re != 0.0 || hu.im != 0.0), nzd = (hd.re != 0.0 || hd.im != 0.0);
+        if (nzu && btest(m, o) == 1 && btest(m, ms) == 0) {
+          op_c(o, m, &k1, &sg1);
+          op_cdg(ms, k1, &k2, &sg2);
+          cplx h = cscale2(hu, sg1, sg2);
+          SCAT(FIND(k2), h.re, h.im);
+        }
+        if (nzu && btest(m, o) == 0 && btest(m, ms) == 1) {
+          op_c(ms, m, &k1, &sg1);
+          op_cdg(o, k1, &k2, &sg2);
+          cplx h = cscale2(hu, sg1, sg2);
+          SCAT(FIND(k2), h.re, h.im);
+        }
+        if (nzd && btest(m, o + ns) == 1 && btest(m, ms + ns) == 0) {
+          op_c(o + ns, m, &k1, &sg1);
+          op_cdg(ms + ns, k1, &k2, &sg2);
+          cplx h = cscale2(hd, sg1, sg2);
+          SCAT(FIND(k2), h.re, h.im);
+        }
+        if (nzd && btest(m, o + ns) == 0 && btest(m, ms + ns) == 1) {
+          op_c(ms + ns, m, &k1, &sg1);
+          op_cdg(o + ns, k1, &k2, &sg2);
+          cplx h = cscale2(hd, sg1, sg2);
+          SCAT(FIND(k2), h.re, h.im);
+        }
+      }
+    if (M.mode == ED_MODE_NONSU2 && M.bath != ED_BATH_REPLICA) {
+      for (int o = 0; o < norb; o++)
+        for (int k = 0; k < nbath; k++) {
+          int ms = M.stride[o][k];
+          double uu = p->bath_u[0][o][k], ud = p->bath_u[S][o][k];
+          if (btest(m, o) == 1 && btest(m, ms + ns) == 0) {
+            op_c(o, m, &k1, &sg1);
+            op_cdg(ms + ns, k1, &k2, &sg2);
+            SCAT(FIND(k2), (uu * sg1) * sg2, 0.0);
+          }
+          if (btest(m, o) == 0 && btest(m, ms + ns) == 1) {
+            op_c(ms + ns, m, &k1, &sg1);
+            op_cdg(o, k1, &k2, &sg2);
+            SCAT(FIND(k2), (uu * sg1) * sg2, 0.0);
+          }
+          if (btest(m, o + ns) == 1 && btest(m, ms) == 0) {
+            op_c(o + ns, m, &k1, &sg1);
+            op_cdg(ms, k1, &k2, &sg2);
+            SCAT(FIND(k2), (ud * sg1) * sg2, 0.0);
+          }
+          if (btest(m, o + ns) == 0 && btest(m, ms) == 1) {
+            op_c(ms, m, &k1, &sg1);
+            op_cdg(o + ns, k1, &k2, &sg2);
+            SCAT(FIND(k2), (ud * sg1) * sg2, 0.0);
+          }
+        }
+    }
+  }
+#undef SCAT
+#undef FIND
+  return 0;
+}
+
+/* ------------------------------------------------------------- Lanczos
+ * lanczos_plain_iteration_c .repo/PLAIN_LANCZOS.f90:87-118, with the H·v
+ * being spMatVec_cc on the CSR above.  State: vin, vout (complex, dim).
+ */
+typedef struct {
+  int64_t dim;
+  const int64_t* rowptr;
+  const int32_t* cols;
+  const double* vals;
+  double* tmp;
+} csr_op;
+
+static double cdot_re(int64_t n, const double* x, const double* y) {
+  /* real part of dot_product(x,y) = sum conj(x)*y, summed in order */
+  double sr = 0.0, si = 0.0;
+  for (int64_t q = 0; q < n; q++) {
+    double xr = x[2 * q], xi = x[2 * q + 1], yr = y[2 * q], yi = y[2 * q + 1];
+    sr = sr + (xr * yr + xi * yi);
+    si = si + (xr * yi - xi * yr);
+  }
+  (void)si;
+  return sr;
+}
+
+static void lanc_iter(const csr_op* H, int iter, double* vin, double* vout, double* a, double* b) {
+  const int64_t n = H->dim;
+  double* tmp = H->tmp;
+  if (iter == 1) {
+    double norm = sqrt(cdot_re(n, vin, vin));
+    for (int64_t q = 0; q < 2 * n; q++) vin[q] = vin[q] / norm;
+    *b = 0.0;
+  }
+  orc_spmv(n, H->rowptr, H->cols, H->vals, vin, tmp);
+  for (int64_t q = 0; q < 2 * n; q++) tmp[q] = tmp[q] - *b * vout[q];
+  *a = cdot_re(n, vin, tmp);
+  for (int64_t q = 0; q < 2 * n; q++) tmp[q] = tmp[q] - *a * vin[q];
+  *b = sqrt(cdot_re(n, tmp, tmp));
+  for (int64_t q = 0; q < 2 * n; q++) vout[q] = vin[q];
+  for (int64_t q = 0; q < 2 * n; q++) vin[q] = tmp[q] / *b;
+}
+
+/* lanczos_plain_tridiag_c .repo/PLAIN_LANCZOS.f90:154-180.
+ * alfa/beta: nitermax entries, beta[0] stays 0 (blanc(1) unused by consumers,
+ * ED_GF_NORMAL.f90:617).  Returns the number of iterations performed. */
+int orc_lanc_tridiag(int64_t dim, const int64_t* rowptr, const int32_t* cols, const double* vals,
+                     const double* v0, int nitermax, double threshold, double* alfa, double* beta) {
+  csr_op H = {dim, rowptr, cols, vals, (double*)malloc(sizeof(double) * 2 * dim)};
+  double* vin = (double*)malloc(sizeof(double) * 2 * dim);
+  double* vout = (double*)calloc(2 * dim, sizeof(double));
+  memcpy(vin, v0, sizeof(double) * 2 * dim);
+  for (int q = 0; q < nitermax; q++) { alfa[q] = 0.0; beta[q] = 0.0; }
+  double a = 0.0, b = 0.0;
+  int iter, done = 0;
+  for (iter = 1; iter <= nitermax; iter++) {
+    lanc_iter(&H, iter, vin, vout, &a, &b);
+    alfa[iter - 1] = a;
+    if (iter < nitermax) beta[iter] = b;
+    done = iter;
+    if (fabs(b) < threshold) break;
+  }
+  free(H.tmp); free(vin); free(vout);
+  return done;
+}
+
+/* pythag / tql2 .repo/PLAIN_LANCZOS.f90:427-605 (EISPACK, also ED_GF_SHARED.f90:76-254).
+ * z is column-major n x n (z[k + n*i] = Z(k+1,i+1)); d, e have n entries, e(1)
+ * (e[0]) is ignored on input. */
+static double pythag(double a, double b) {
+  double p = fmax(fabs(a), fabs(b));
+  if (p != 0.0) {
+    double r = fmin(fabs(a), fabs(b)) / p;
+    r = r * r;
+    for (;;) {
+      double t = 4.0 + r;
+      if (t == 4.0) break;
+      double s = r / t;
+      double u = 1.0 + 2.0 * s;
+      p = u * p;
+      double su = s / u;
+      r = (su * su) * r;
+    }
+  }
+  return p;
+}
+
+int orc_tql2(int n, double* d, double* e, double* z) {
+#define D(i) d[(i)-1]
+#define E(i) e[(i)-1]
+#define Z(k, i) z[((k)-1) + (int64_t)n * ((i)-1)]
+  int ierr = 0;
+  if (n == 1) return 0;
+  for (int i = 2; i <= n; i++) E(i - 1) = E(i);
+  double f = 0.0, tst1 = 0.0;
+  E(n) = 0.0;
+  for (int l = 1; l <= n; l++) {
+    int j = 0;
+    double h = fabs(D(l)) + fabs(E(l));
+    tst1 = fmax(tst1, h);
+    int m;
+    for (m = l; m <= n; m++) {
+      double tst2 = tst1 + fabs(E(m));
+      if (tst2 == tst1) break;
+    }
+    if (m != l) {
+      for (;;) {
+        if (30 <= j) return l;
+        j = j + 1;
+        int l1 = l + 1, l2 = l1 + 1;
+        double g = D(l);
+        double p = (D(l1) - g) / (2.0 * E(l));
+        double r = pythag(p, 1.0);
+        double sr = (p >= 0.0) ? fabs(r) : -fabs(r); /* sign(r,p) */
+        D(l) = E(l) / (p + sr);
+        D(l1) = E(l) * (p + sr);
+        double dl1 = D(l1);
+        h = g - D(l);
+        for (int i = l2; i <= n; i++) D(i) = D(i) - h;
+        f = f + h;
+        p = D(m);
+        double c = 1.0, c2 = c, c3 = c;
+        double el1 = E(l1);
+        double s = 0.0, s2 = 0.0;
+        int mml = m - l;
+        for (int ii = 1; ii <= mml; ii++) {
+          c3 = c2;
+          c2 = c;
+          s2 = s;
+          int i = m - ii;
+          g = c * E(i);
+          h = c * p;
+          r = pythag(p, E(i));
+          E(i + 1) = s * r;
+          s = E(i) / r;
+          c = p / r;
+          p = c * D(i) - s * g;
+          D(i + 1) = h + s * (c * g + s * D(i));
+          for (int k = 1; k <= n; k++) {
+            h = Z(k, i + 1);
+            Z(k, i + 1) = s * Z(k, i) + c * h;
+            Z(k, i) = c * Z(k, i) - s * h;
+          }
+        }
+        p = -s * s2 * c3 * el1 * E(l) / dl1;
+        E(l) = s * p;
+        D(l) = c * p;
+        double tst2 = tst1 + fabs(E(l));
+        if (!(tst2 > tst1)) break;
+      }
+    }
+    D(l) = D(l) + f;
+  }
+  for (int ii = 2; ii <= n; ii++) {
+    int i = ii - 1, k = i;
+    double p = D(i);
+    for (int jj = ii; jj <= n; jj++)
+      if (D(jj) < p) { k = jj; p = D(jj); }
+    if (k != i) {
+      D(k) = D(i);
+      D(i) = p;
+      for (int jj = 1; jj <= n; jj++) {
+        double t = Z(jj, i);
+        Z(jj, i) = Z(jj, k);
+        Z(jj, k) = t;
+      }
+    }
+  }
+  return ierr;
+#undef D
+#undef E
+#undef Z
+}
+
+/* lanczos_plain_c .repo/PLAIN_LANCZOS.f90:286-385 (ground state, convergence
+ * test on the lowest Ritz value every iteration once nlanc >= ncheck).
+ * Deviation (documented): the Ritz vector is accumulated from v_iter (vout
+ * after each call), not from v_iter+1 as the legacy loop at :378-380 does.
+ * vect: complex start vector in, Ritz vector out (may be NULL -> not formed).
+ * Returns nlanc; *egs = lowest Ritz value. */
+int orc_lanc_eigh(int64_t dim, const int64_t* rowptr, const int32_t* cols, const double* vals,
+                  double* vect, int nitermax, double threshold, int ncheck, double* egs) {
+  csr_op H = {dim, rowptr, cols, vals, (double*)malloc(sizeof(double) * 2 * dim)};
+  double* vin = (double*)malloc(sizeof(double) * 2 * dim);
+  double* vout = (double*)calloc(2 * dim, sizeof(double));
+  double* alanc = (double*)calloc(nitermax + 2, sizeof(double));
+  double* blanc = (double*)calloc(nitermax + 2, sizeof(double));
+  double* esave = (double*)calloc(nitermax + 2, sizeof(double));
+  double* diag = (double*)calloc(nitermax + 1, sizeof(double));
+  double* sub = (double*)calloc(nitermax + 1, sizeof(double));
+  memcpy(vin, vect, sizeof(double) * 2 * dim);
+  int nlanc = 0;
+  double a = 0, b = 0;
+  for (int iter = 1; iter <= nitermax; iter++) {
+    lanc_iter(&H, iter, vin, vout, &a, &b);
+    if (fabs(b) < threshold) break;
+    nlanc = nlanc + 1;
+    alanc[iter] = a;      /* alanc(iter) */
+    blanc[iter + 1] = b;  /* blanc(iter+1) */
+    for (int q = 1; q <= nlanc; q++) { diag[q - 1] = alanc[q]; sub[q - 1] = (q >= 2) ? blanc[q] : 0.0; }
+    /* eigenvalues only are needed for the test: run tql2 with a dummy Z */
+    double* Zt = (double*)calloc((size_t)nlanc * nlanc, sizeof(double));
+    for (int q = 0; q < nlanc; q++) Zt[q + (int64_t)nlanc * q] = 1.0;
+    orc_tql2(nlanc, diag, sub, Zt);
+    free(Zt);
+    if (nlanc >= ncheck) {
+      esave[nlanc - (ncheck - 1)] = diag[0];
+      if (nlanc >= ncheck + 1) {
+        double diff = esave[nlanc - (ncheck - 1)] - esave[nlanc - (ncheck - 1) - 1];
+        if (fabs(diff) <= threshold) break;
+      }
+    }
+  }
+  for (int q = 1; q <= nlanc; q++) { diag[q - 1] = alanc[q]; sub[q - 1] = (q >= 2) ? blanc[q] : 0.0; }
+  double* Z = (double*)calloc((size_t)nlanc * nlanc, sizeof(double));
+  for (int q = 0; q < nlanc; q++) Z[q + (int64_t)nlanc * q] = 1.0;
+  orc_tql2(nlanc, diag, sub, Z);
+  *egs = diag[0];
+  if (vect) {
+    double* acc = (double*)calloc(2 * dim, sizeof(double));
+    memset(vout, 0, sizeof(double) * 2 * dim);
+    for (int iter = 1; iter <= nlanc; iter++) {
+      double aa = alanc[iter], bb = blanc[iter];
+      lanc_iter(&H, iter, vect, vout, &aa, &bb); /* second pass, :376-381 */
+      /* after the call vout = v_iter */
+      for (int64_t q = 0; q < 2 * dim; q++) acc[q] = acc[q] + vout[q] * Z[(iter - 1)];
+    }
+    double nrm = sqrt(cdot_re(dim, acc, acc));
+    for (int64_t q = 0; q < 2 * dim; q++) vect[q] = acc[q] / nrm;
+    free(acc);
+  }
+  free(H.tmp); free(vin); free(vout); free(alanc); free(blanc); free(esave); free(diag);
+  free(sub); free(Z);
+  return nlanc;
+}
