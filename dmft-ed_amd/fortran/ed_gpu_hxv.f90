@@ -1,0 +1,191 @@
+!-----------------------------------------------------------------------
+! ED_GPU_HXV — iso_c_binding shim between the reference's Fortran call
+! sites and the MI355X library libedgpu.so (include/ed_gpu.h).
+!
+! The reference binds its H·v through the abstract interface
+!     cc_sparse_HxV(Nloc,v,Hv)            ED_VARS_GLOBAL.f90:48-54
+! and the procedure pointer spHtimesV_cc  ED_VARS_GLOBAL.f90:105,
+! set in build_Hv_sector                  ED_HAMILTONIAN.f90:85-101.
+! gpuMatVec_cc below has exactly that interface, so a new branch of
+! build_Hv_sector can do   spHtimesV_cc => gpuMatVec_cc   and every
+! caller (sp_eigh / sp_lanc_eigh / sp_lanc_tridiag in ED_DIAG.f90 and
+! ED_GF_*.f90) stays unchanged.  See INTEGRATION.md.
+!-----------------------------------------------------------------------
+module ED_GPU_HXV
+  use iso_c_binding
+  implicit none
+  private
+
+  integer, parameter, public :: ED_MAX_NORB = 3, ED_MAX_NSPIN = 2, ED_MAX_NBATH = 32
+  integer, parameter, public :: ED_STORED = 1, ED_DIRECT = 2, ED_REAL = 4
+
+  ! C struct ed_params (include/ed_gpu.h).  C arrays a[I][J][K][L] appear in
+  ! Fortran with reversed dimensions (L,K,J,I).
+  type, bind(C), public :: ed_params_t
+     integer(c_int32_t) :: norb, nspin, nbath, ed_mode, bath_type, hfmode
+     real(c_double)     :: uloc(3), ust, jh, jx, jp, xmu
+     real(c_double)     :: imphloc_re(ED_MAX_NORB,ED_MAX_NORB,ED_MAX_NSPIN,ED_MAX_NSPIN)
+     real(c_double)     :: imphloc_im(ED_MAX_NORB,ED_MAX_NORB,ED_MAX_NSPIN,ED_MAX_NSPIN)
+     real(c_double)     :: bath_e(ED_MAX_NBATH,ED_MAX_NORB,ED_MAX_NSPIN)
+     real(c_double)     :: bath_v(ED_MAX_NBATH,ED_MAX_NORB,ED_MAX_NSPIN)
+     real(c_double)     :: bath_u(ED_MAX_NBATH,ED_MAX_NORB,ED_MAX_NSPIN)
+     real(c_double)     :: bath_d(ED_MAX_NBATH,ED_MAX_NORB,ED_MAX_NSPIN)
+     real(c_double)     :: bath_h_re(ED_MAX_NBATH,ED_MAX_NORB,ED_MAX_NORB,ED_MAX_NSPIN,ED_MAX_NSPIN)
+     real(c_double)     :: bath_h_im(ED_MAX_NBATH,ED_MAX_NORB,ED_MAX_NORB,ED_MAX_NSPIN,ED_MAX_NSPIN)
+     real(c_double)     :: bath_vr_re(ED_MAX_NBATH)
+     real(c_double)     :: bath_vr_im(ED_MAX_NBATH)
+  end type ed_params_t
+
+  interface
+     integer(c_int) function ed_gpu_init(p) bind(C, name="ed_gpu_init")
+       import :: c_int, ed_params_t
+       type(ed_params_t), intent(in) :: p
+     end function ed_gpu_init
+     integer(c_int) function ed_gpu_set_device(dev) bind(C, name="ed_gpu_set_device")
+       import :: c_int, c_int32_t
+       integer(c_int32_t), value :: dev
+     end function ed_gpu_set_device
+     integer(c_int) function ed_gpu_build_sector(q1, q2, flags, dim) bind(C, name="ed_gpu_build_sector")
+       import :: c_int, c_int32_t, c_int64_t
+       integer(c_int32_t), value :: q1, q2, flags
+       integer(c_int64_t), intent(out) :: dim
+     end function ed_gpu_build_sector
+     integer(c_int) function ed_gpu_vecdim(vecdim) bind(C, name="ed_gpu_vecdim")
+       import :: c_int, c_int32_t
+       integer(c_int32_t), intent(out) :: vecdim
+     end function ed_gpu_vecdim
+     ! cc_sparse_HxV: Nloc by reference, complex(8) host arrays
+     integer(c_int) function ed_gpu_hxv(nloc, v, hv) bind(C, name="ed_gpu_hxv")
+       import :: c_int, c_int32_t, c_double_complex
+       integer(c_int32_t), intent(in) :: nloc
+       complex(c_double_complex), intent(in) :: v(*)
+       complex(c_double_complex), intent(out) :: hv(*)
+     end function ed_gpu_hxv
+     integer(c_int) function ed_gpu_lanc_eigh(nitermax, threshold, ncheck, egs, vect, nlanc) &
+          bind(C, name="ed_gpu_lanc_eigh")
+       import :: c_int, c_int32_t, c_double, c_double_complex
+       integer(c_int32_t), value :: nitermax, ncheck
+       real(c_double), value :: threshold
+       real(c_double), intent(out) :: egs
+       complex(c_double_complex), intent(out) :: vect(*)
+       integer(c_int32_t), intent(out) :: nlanc
+     end function ed_gpu_lanc_eigh
+     integer(c_int) function ed_gpu_lanc_tridiag(v0, nitermax, threshold, alfa, beta, nlanc) &
+          bind(C, name="ed_gpu_lanc_tridiag")
+       import :: c_int, c_int32_t, c_double, c_double_complex
+       complex(c_double_complex), intent(in) :: v0(*)
+       integer(c_int32_t), value :: nitermax
+       real(c_double), value :: threshold
+       real(c_double), intent(out) :: alfa(*), beta(*)
+       integer(c_int32_t), intent(out) :: nlanc
+     end function ed_gpu_lanc_tridiag
+     integer(c_int) function ed_gpu_delete_sector() bind(C, name="ed_gpu_delete_sector")
+       import :: c_int
+     end function ed_gpu_delete_sector
+     integer(c_int) function ed_gpu_finalize() bind(C, name="ed_gpu_finalize")
+       import :: c_int
+     end function ed_gpu_finalize
+     type(c_ptr) function ed_gpu_last_error() bind(C, name="ed_gpu_last_error")
+       import :: c_ptr
+     end function ed_gpu_last_error
+     integer(c_size_t) function c_strlen(s) bind(C, name="strlen")
+       import :: c_size_t, c_ptr
+       type(c_ptr), value :: s
+     end function c_strlen
+  end interface
+
+  public :: ed_gpu_init, ed_gpu_set_device, ed_gpu_build_sector, ed_gpu_vecdim, ed_gpu_hxv
+  public :: ed_gpu_lanc_eigh, ed_gpu_lanc_tridiag, ed_gpu_delete_sector, ed_gpu_finalize
+  public :: gpuMatVec_cc
+  public :: ed_gpu_check
+  public :: ed_gpu_pack_params
+
+contains
+
+  !> Same interface as cc_sparse_HxV (ED_VARS_GLOBAL.f90:48-54): Hv = H v.
+  subroutine gpuMatVec_cc(Nloc, v, Hv)
+    integer                    :: Nloc
+    complex(8),dimension(Nloc) :: v
+    complex(8),dimension(Nloc) :: Hv
+    integer(c_int32_t)         :: n
+    n = int(Nloc, c_int32_t)
+    call ed_gpu_check(ed_gpu_hxv(n, v, Hv), "gpuMatVec_cc")
+  end subroutine gpuMatVec_cc
+
+  !> Reference error convention: stop with a message (e.g. STORED_HxV.f90:50).
+  subroutine ed_gpu_check(rc, where)
+    integer(c_int), intent(in) :: rc
+    character(len=*), intent(in) :: where
+    type(c_ptr) :: p
+    character(kind=c_char), pointer :: msg(:)
+    character(len=:), allocatable :: txt
+    integer :: i, n
+    if (rc == 0) return
+    p = ed_gpu_last_error()
+    n = int(c_strlen(p))
+    call c_f_pointer(p, msg, [n])
+    allocate(character(len=n) :: txt)
+    do i = 1, n
+       txt(i:i) = msg(i)
+    enddo
+    write(*,"(A,A,A,I0,A,A)") "ED_GPU ERROR in ", where, " (rc=", rc, "): ", txt
+    stop 1
+  end subroutine ed_gpu_check
+
+  !> Pack the reference's model state (impHloc, dmft_bath components and the
+  !> interaction constants) into the C struct.  Arrays use the reference's
+  !> shapes: impHloc(Nspin,Nspin,Norb,Norb); e,v,u,d(Nspin,Norb|1,Nbath).
+  subroutine ed_gpu_pack_params(p, Norb, Nspin, Nbath, ed_mode, bath_type, hfmode, &
+       Uloc, Ust, Jh, Jx, Jp, xmu, impHloc, e, v, u, d)
+    type(ed_params_t), intent(out)   :: p
+    integer, intent(in)              :: Norb, Nspin, Nbath
+    character(len=*), intent(in)     :: ed_mode, bath_type
+    logical, intent(in)              :: hfmode
+    real(8), intent(in)              :: Uloc(3), Ust, Jh, Jx, Jp, xmu
+    complex(8), intent(in)           :: impHloc(:,:,:,:)
+    real(8), intent(in)              :: e(:,:,:), v(:,:,:)
+    real(8), intent(in), optional    :: u(:,:,:), d(:,:,:)
+    integer :: is, js, io, jo, k
+    p%norb = Norb ; p%nspin = Nspin ; p%nbath = Nbath
+    select case (trim(ed_mode))
+    case ("superc") ; p%ed_mode = 1
+    case ("nonsu2") ; p%ed_mode = 2
+    case default    ; p%ed_mode = 0
+    end select
+    select case (trim(bath_type))
+    case ("hybrid")  ; p%bath_type = 1
+    case ("replica") ; p%bath_type = 2
+    case default     ; p%bath_type = 0
+    end select
+    p%hfmode = merge(1, 0, hfmode)
+    p%uloc = Uloc ; p%ust = Ust ; p%jh = Jh ; p%jx = Jx ; p%jp = Jp ; p%xmu = xmu
+    p%imphloc_re = 0d0 ; p%imphloc_im = 0d0
+    p%bath_e = 0d0 ; p%bath_v = 0d0 ; p%bath_u = 0d0 ; p%bath_d = 0d0
+    p%bath_h_re = 0d0 ; p%bath_h_im = 0d0 ; p%bath_vr_re = 0d0 ; p%bath_vr_im = 0d0
+    do is = 1, Nspin
+       do js = 1, Nspin
+          do io = 1, Norb
+             do jo = 1, Norb
+                p%imphloc_re(jo,io,js,is) = dble(impHloc(is,js,io,jo))
+                p%imphloc_im(jo,io,js,is) = aimag(impHloc(is,js,io,jo))
+             enddo
+          enddo
+       enddo
+    enddo
+    do is = 1, Nspin
+       do io = 1, size(e,2)
+          do k = 1, Nbath
+             p%bath_e(k,io,is) = e(is,io,k)
+             if (present(d)) p%bath_d(k,io,is) = d(is,io,k)
+          enddo
+       enddo
+       do io = 1, size(v,2)
+          do k = 1, Nbath
+             p%bath_v(k,io,is) = v(is,io,k)
+             if (present(u)) p%bath_u(k,io,is) = u(is,io,k)
+          enddo
+       enddo
+    enddo
+  end subroutine ed_gpu_pack_params
+
+end module ED_GPU_HXV

@@ -1,0 +1,50 @@
+"""Launch one H·v kernel repeatedly on a chosen sector (for rocprofv3 runs).
+
+usage: python tools/spmv_probe.py [--sector n28|n28b|c4|c2] [--path 0|1|2] [--complex] [--iters N]
+Prints the HIP-event average per launch on the launch stream.
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "dmft-ed_amd"))
+import torch  # noqa: E402
+
+from edgpu.hamiltonian import Sector  # noqa: E402
+from edgpu.params import make_config  # noqa: E402
+
+SECTORS = {
+    "n28": (dict(Norb=1, Nbath=13), (7, 7)),
+    "n28b": (dict(Norb=2, Nbath=6), (7, 7)),
+    "c4": (dict(Norb=2, Nbath=5), (6, 6)),
+    "c2": (dict(Norb=1, Nbath=7), (4, 4)),
+}
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--sector", default="n28")
+ap.add_argument("--path", type=int, default=0)
+ap.add_argument("--complex", action="store_true")
+ap.add_argument("--iters", type=int, default=20)
+a = ap.parse_args()
+kw, q = SECTORS[a.sector]
+cfg = make_config(bath="random", seed=20251015, **kw)
+real = not a.complex
+with Sector(cfg, q[0], q[1], stored=(a.path == 0), direct=(a.path != 0), real=real) as S:
+    dt = torch.float64 if real else torch.complex128
+    i = torch.arange(1, S.dim + 1, dtype=torch.float64, device="cuda")
+    x = torch.sin(i) if real else torch.complex(torch.sin(i), torch.cos(3 * i))
+    x = x.to(dt).contiguous()
+    y = torch.empty_like(x)
+    st = torch.cuda.current_stream()
+    for _ in range(3):
+        S.hxv_dev(x, y, path=a.path, stream=st)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(a.iters):
+        S.hxv_dev(x, y, path=a.path, stream=st)
+    e1.record(st)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / a.iters
+    print(f"sector={a.sector} dim={S.dim} nnz={S.nnz} padded={S.info.padded} path={a.path} "
+          f"real={real} ms/launch={ms:.5f}")
