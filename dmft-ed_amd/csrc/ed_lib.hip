@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "ed_kernels.hpp"
+#include "ed_persist.hpp"
 #include "ed_tables.hpp"
 
 using namespace edg;
@@ -93,6 +94,8 @@ struct ed_sector {
   LancWS ws;
   int64_t bytes = 0;
   std::vector<void*> allocs;
+  // persistent one-workgroup Lanczos (small sectors)
+  void* d_prun = nullptr;   // PersistRun<HC> in device memory
   // graph cache for Lanczos iterations
   hipGraphExec_t gexec = nullptr;
   int g_path = -2, g_vc = -1, g_chunk = 0;
@@ -124,10 +127,10 @@ static int upload(ed_sector* s, T** p, const std::vector<T>& h) {
 
 static void sector_free(ed_sector* s) {
   if (!s) return;
-  hipSetDevice(s->device);
-  if (s->gexec) hipGraphExecDestroy(s->gexec);
-  for (void* p : s->allocs) hipFree(p);
-  if (s->stream) hipStreamDestroy(s->stream);
+  (void)hipSetDevice(s->device);
+  if (s->gexec) (void)hipGraphExecDestroy(s->gexec);
+  for (void* p : s->allocs) (void)hipFree(p);
+  if (s->stream) (void)hipStreamDestroy(s->stream);
   delete s;
 }
 
@@ -158,9 +161,9 @@ static int build_stored(ed_sector* s) {
   int64_t slots = 0;
   HIPCK(hipMemcpyAsync(&slots, total, sizeof(int64_t), hipMemcpyDeviceToHost, s->stream));
   HIPCK(hipStreamSynchronize(s->stream));
-  hipFree(width);
-  hipFree(bsum);
-  hipFree(total);
+  (void)hipFree(width);
+  (void)hipFree(bsum);
+  (void)hipFree(total);
   s->padded = slots;
   const size_t hv = s->hc ? 16 : 8;
   CK(dalloc(s, &s->d_diag, dim * hv));
@@ -442,7 +445,7 @@ static int lanc_iters(ed_sector* s, int path, bool basis, int n, hipStream_t st)
   if (!s->gexec || s->g_path != path || s->g_vc != (int)VC || s->g_basis != basis ||
       s->g_chunk != chunk) {
     if (s->gexec) {
-      hipGraphExecDestroy(s->gexec);
+      (void)hipGraphExecDestroy(s->gexec);
       s->gexec = nullptr;
     }
     hipGraph_t g;
@@ -453,7 +456,7 @@ static int lanc_iters(ed_sector* s, int path, bool basis, int n, hipStream_t st)
     if (rc != ED_OK) return rc;
     HIPCK(e2);
     HIPCK(hipGraphInstantiate(&s->gexec, g, nullptr, nullptr, 0));
-    hipGraphDestroy(g);
+    (void)hipGraphDestroy(g);
     s->g_path = path;
     s->g_vc = VC;
     s->g_basis = basis;
@@ -462,6 +465,114 @@ static int lanc_iters(ed_sector* s, int path, bool basis, int n, hipStream_t st)
   int k = 0;
   for (; k + chunk <= n; k += chunk) HIPCK(hipGraphLaunch(s->gexec, st));
   for (; k < n; k++) CK((lanc_iter<VC>(s, path, basis, st)));
+  return ED_OK;
+}
+
+// ---------------------------------------------- persistent small-sector path
+static constexpr int64_t kLdsBudget = 150 * 1024;
+
+// Returns the persistent mode (0 stored, 1 Kronecker) or -1 when the sector
+// does not fit one workgroup's LDS / register budget.
+static int persist_mode(const ed_sector* s, int vc, int path) {
+  if (getenv("ED_GPU_NO_PERSIST")) return -1;
+  const int64_t vs = vc ? 16 : 8;
+  if (s->dim > 16 * (int64_t)kPBlock) return -1;
+  int64_t lds = ((s->dim * vs + 15) & ~(int64_t)15);
+  if (path == 0) return lds <= kLdsBudget ? 0 : -1;
+  if (path == 2) {
+    const KronHost& K = s->K;
+    const int64_t hs = s->hc ? 16 : 8;
+    lds += (K.dimup + K.dimdw) * (hs + 1 + 32) + (int64_t)(K.degup * K.dimup + K.degdw * K.dimdw) * (hs + 4) +
+           (int64_t)K.nimp * K.nimp * 8 + 256;
+    return lds <= kLdsBudget ? 1 : -1;
+  }
+  return -1;
+}
+
+static int64_t persist_lds(const ed_sector* s, int vc, int mode) {
+  const int64_t vs = vc ? 16 : 8;
+  int64_t lds = ((s->dim * vs + 15) & ~(int64_t)15);
+  if (mode == 1) {
+    const KronHost& K = s->K;
+    const int64_t hs = s->hc ? 16 : 8;
+    auto al = [](int64_t b) { return (b + 15) & ~(int64_t)15; };
+    lds += al(K.dimup * hs) + al(K.dimdw * hs) + al((int64_t)K.degup * K.dimup * hs) +
+           al((int64_t)K.degdw * K.dimdw * hs) + al((int64_t)K.degup * K.dimup * 4) +
+           al((int64_t)K.degdw * K.dimdw * 4) + al(K.dimup) + al(K.dimdw) + al((int64_t)K.nimp * K.nimp * 8);
+  }
+  return lds;
+}
+
+template <bool HC, bool VC, int MODE, int RPT>
+static int persist_launch_t(ed_sector* s, int64_t lds, hipStream_t st) {
+  auto fn = k_lanc_persist<HC, VC, MODE, RPT>;
+  HIPCK(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(fn, dim3(1), dim3(kPBlock), (size_t)lds, st, (const PersistRun<HC>*)s->d_prun);
+  HIPCK(hipGetLastError());
+  return ED_OK;
+}
+
+template <bool HC, bool VC, int MODE>
+static int persist_launch_m(ed_sector* s, int64_t lds, hipStream_t st) {
+  const int64_t rpt = (s->dim + kPBlock - 1) / kPBlock;
+  if (rpt <= 1) return persist_launch_t<HC, VC, MODE, 1>(s, lds, st);
+  if (rpt <= 2) return persist_launch_t<HC, VC, MODE, 2>(s, lds, st);
+  if (rpt <= 4) return persist_launch_t<HC, VC, MODE, 4>(s, lds, st);
+  if (rpt <= 8) return persist_launch_t<HC, VC, MODE, 8>(s, lds, st);
+  return persist_launch_t<HC, VC, MODE, 16>(s, lds, st);
+}
+
+// Launch `niter` persistent iterations.  first=1 starts from the vector in R.
+template <bool VC>
+static int persist_iters(ed_sector* s, int mode, bool basis, int niter, int first, hipStream_t st) {
+  LancWS& w = s->ws;
+  if (!s->d_prun) CK(dalloc(s, &s->d_prun, sizeof(PersistRun<true>)));
+  auto fill = [&](auto& r) {
+    using RT = std::remove_reference_t<decltype(r)>;
+    using HT = std::remove_const_t<std::remove_pointer_t<decltype(r.diag)>>;
+    memset(&r, 0, sizeof(RT));
+    r.diag = (const HT*)s->d_diag;
+    r.sptr = s->d_sptr;
+    r.cols = s->d_cols;
+    r.vals = (const HT*)s->d_vals;
+    r.dim = s->dim;
+    r.R = w.R;
+    r.P = w.P;
+    r.st = w.st;
+    r.alpha = w.alpha;
+    r.beta = w.beta;
+    r.basis = basis ? w.basis : nullptr;
+    r.niter = niter;
+    r.first = first;
+  };
+  const int64_t lds = persist_lds(s, VC, mode);
+  if (s->hc) {
+    if constexpr (!VC) return fail(ED_ERR_ARG, "complex H needs complex vectors");
+    else {
+      PersistRun<true> r;
+      fill(r);
+      if (mode == 1) r.K = kron_args<true>(s);
+      HIPCK(hipMemcpyAsync(s->d_prun, &r, sizeof(r), hipMemcpyHostToDevice, st));
+      HIPCK(hipStreamSynchronize(st));  // r is a stack temporary
+      return mode == 0 ? persist_launch_m<true, true, 0>(s, lds, st) : persist_launch_m<true, true, 1>(s, lds, st);
+    }
+  }
+  PersistRun<false> r;
+  fill(r);
+  if (mode == 1) r.K = kron_args<false>(s);
+  HIPCK(hipMemcpyAsync(s->d_prun, &r, sizeof(r), hipMemcpyHostToDevice, st));
+  HIPCK(hipStreamSynchronize(st));  // r is a stack temporary
+  return mode == 0 ? persist_launch_m<false, VC, 0>(s, lds, st) : persist_launch_m<false, VC, 1>(s, lds, st);
+}
+
+static int persist_set_thresh(ed_sector* s, double thresh, hipStream_t st) {
+  LancState h;
+  memset(&h, 0, sizeof(h));
+  h.thresh = thresh;
+  HIPCK(hipMemcpyAsync(s->ws.st, &h, sizeof(h), hipMemcpyHostToDevice, st));
+  HIPCK(hipMemsetAsync(s->ws.beta, 0, (s->ws.cap + 2) * sizeof(double), st));
+  HIPCK(hipMemsetAsync(s->ws.alpha, 0, (s->ws.cap + 2) * sizeof(double), st));
+  HIPCK(hipStreamSynchronize(st));
   return ED_OK;
 }
 
@@ -754,46 +865,57 @@ int ed_sector_dump_csr(const ed_sector* s, int64_t* rowptr, int32_t* cols, doubl
   return ED_OK;
 }
 
-// Fixed-length run from a device start vector (benchmark entry point).
-int ed_sector_lanc_run(ed_sector* s, int32_t vtype, const void* v0_dev, int32_t niter,
-                       double* alfa, double* beta, float* ms, void* stream) {
-  if (!s || niter < 1) return fail(ED_ERR_ARG, "bad args");
-  HIPCK(hipSetDevice(s->device));
-  const int vc = vtype ? 1 : 0;
-  if (vc == 0 && s->hc) return fail(ED_ERR_ARG, "complex H needs vtype=1");
-  CK(lanc_prepare(s, vc, niter, false, 0));
-  hipStream_t st = s->stream;
-  const size_t vs = vc ? 16 : 8;
-  if (v0_dev) HIPCK(hipMemcpyAsync(s->ws.R, v0_dev, s->dim * vs, hipMemcpyDeviceToDevice, st));
-  else hipLaunchKernelGGL(k_default_start, dim3(grid_for(s->dim * (vc ? 2 : 1))), dim3(kBlock), 0,
-                          st, (double*)s->ws.R, s->dim * (vc ? 2 : 1));
-  const int path = resolve_path(s, -1);
-  hipEvent_t e0, e1;
-  HIPCK(hipEventCreate(&e0));
-  HIPCK(hipEventCreate(&e1));
-  int rc;
-  if (vc) rc = lanc_start<true>(s, 1e-300, st);
-  else rc = lanc_start<false>(s, 1e-300, st);
-  if (rc == ED_OK) {
-    HIPCK(hipEventRecord(e0, st));
-    rc = vc ? lanc_iters<true>(s, path, false, niter, st) : lanc_iters<false>(s, path, false, niter, st);
-    HIPCK(hipEventRecord(e1, st));
-  }
-  HIPCK(hipStreamSynchronize(st));
-  if (ms) HIPCK(hipEventElapsedTime(ms, e0, e1));
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
-  CK(rc);
-  if (alfa) HIPCK(hipMemcpy(alfa, s->ws.alpha, niter * sizeof(double), hipMemcpyDeviceToHost));
-  if (beta) HIPCK(hipMemcpy(beta, s->ws.beta, niter * sizeof(double), hipMemcpyDeviceToHost));
-  (void)stream;
+int ed_sector_sell_view(const ed_sector* s, ed_sell_view* v) {
+  if (!s || !v) return fail(ED_ERR_ARG, "null");
+  if (!(s->flags & ED_STORED)) return fail(ED_ERR_STATE, "sector was built without ED_STORED");
+  v->dim = s->dim;
+  v->nslice = s->nslice;
+  v->slots = s->padded;
+  v->value_bytes = s->hc ? 16 : 8;
+  v->pad = 0;
+  v->diag = s->d_diag;
+  v->sptr = s->d_sptr;
+  v->cols = s->d_cols;
+  v->vals = s->d_vals;
+  v->rowcnt = s->d_cnt;
   return ED_OK;
 }
 
-static int lanc_load_start(ed_sector* s, int vc, const void* v0) {
+// One Lanczos driver for every entry point: persistent one-workgroup kernel
+// when the sector fits a CU, graph-captured two-kernel recurrence otherwise.
+struct LancDriver {
+  ed_sector* s;
+  int vc, path, pm;
+  bool basis;
+  hipStream_t st;
+  int start(double thresh) {
+    if (pm >= 0) return persist_set_thresh(s, thresh, st);
+    return vc ? lanc_start<true>(s, thresh, st) : lanc_start<false>(s, thresh, st);
+  }
+  int iters(int n, bool first) {
+    if (pm >= 0)
+      return vc ? persist_iters<true>(s, pm, basis, n, first ? 1 : 0, st)
+                : persist_iters<false>(s, pm, basis, n, first ? 1 : 0, st);
+    return vc ? lanc_iters<true>(s, path, basis, n, st) : lanc_iters<false>(s, path, basis, n, st);
+  }
+};
+
+static int make_driver(ed_sector* s, int vtype, bool basis, LancDriver* d) {
+  d->s = s;
+  d->vc = vtype ? 1 : 0;
+  if (d->vc == 0 && s->hc) return fail(ED_ERR_ARG, "complex H needs vtype=1");
+  d->path = resolve_path(s, -1);
+  d->pm = persist_mode(s, d->vc, d->path);
+  d->basis = basis;
+  d->st = s->stream;
+  return ED_OK;
+}
+
+static int lanc_load_start(ed_sector* s, int vc, const void* v0, bool v0_device) {
   const size_t vs = vc ? 16 : 8;
   if (v0) {
-    HIPCK(hipMemcpyAsync(s->ws.R, v0, s->dim * vs, hipMemcpyHostToDevice, s->stream));
+    HIPCK(hipMemcpyAsync(s->ws.R, v0, s->dim * vs,
+                         v0_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s->stream));
   } else {
     hipLaunchKernelGGL(k_default_start, dim3(grid_for(s->dim * (vc ? 2 : 1))), dim3(kBlock), 0,
                        s->stream, (double*)s->ws.R, s->dim * (vc ? 2 : 1));
@@ -802,24 +924,51 @@ static int lanc_load_start(ed_sector* s, int vc, const void* v0) {
   return ED_OK;
 }
 
+// Fixed-length run from a device start vector (benchmark entry point).
+int ed_sector_lanc_run(ed_sector* s, int32_t vtype, const void* v0_dev, int32_t niter,
+                       double* alfa, double* beta, float* ms, void* stream) {
+  (void)stream;
+  if (!s || niter < 1) return fail(ED_ERR_ARG, "bad args");
+  HIPCK(hipSetDevice(s->device));
+  LancDriver d;
+  CK(make_driver(s, vtype, false, &d));
+  CK(lanc_prepare(s, d.vc, niter, false, 0));
+  CK(lanc_load_start(s, d.vc, v0_dev, true));
+  hipEvent_t e0, e1;
+  HIPCK(hipEventCreate(&e0));
+  HIPCK(hipEventCreate(&e1));
+  int rc = d.start(1e-300);
+  if (rc == ED_OK) {
+    HIPCK(hipEventRecord(e0, d.st));
+    rc = d.iters(niter, true);
+    HIPCK(hipEventRecord(e1, d.st));
+  }
+  HIPCK(hipStreamSynchronize(d.st));
+  if (ms && rc == ED_OK) HIPCK(hipEventElapsedTime(ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  CK(rc);
+  if (alfa) HIPCK(hipMemcpy(alfa, s->ws.alpha, niter * sizeof(double), hipMemcpyDeviceToHost));
+  if (beta) HIPCK(hipMemcpy(beta, s->ws.beta, niter * sizeof(double), hipMemcpyDeviceToHost));
+  return ED_OK;
+}
+
 int ed_sector_lanc_tridiag(ed_sector* s, int32_t vtype, const void* v0, int32_t nitermax,
                            double threshold, double* alfa, double* beta, int32_t* nlanc) {
   if (!s || !alfa || !beta || nitermax < 1) return fail(ED_ERR_ARG, "bad args");
   HIPCK(hipSetDevice(s->device));
-  const int vc = vtype ? 1 : 0;
-  if (vc == 0 && s->hc) return fail(ED_ERR_ARG, "complex H needs vtype=1");
-  CK(lanc_prepare(s, vc, nitermax, false, 0));
-  CK(lanc_load_start(s, vc, v0));
-  const int path = resolve_path(s, -1);
-  CK(vc ? lanc_start<true>(s, threshold, s->stream) : lanc_start<false>(s, threshold, s->stream));
-  CK(vc ? lanc_iters<true>(s, path, false, nitermax, s->stream)
-        : lanc_iters<false>(s, path, false, nitermax, s->stream));
+  LancDriver d;
+  CK(make_driver(s, vtype, false, &d));
+  CK(lanc_prepare(s, d.vc, nitermax, false, 0));
+  CK(lanc_load_start(s, d.vc, v0, false));
+  CK(d.start(threshold));
+  CK(d.iters(nitermax, true));
   std::vector<double> a(nitermax + 1), b(nitermax + 2);
-  HIPCK(hipMemcpyAsync(a.data(), s->ws.alpha, nitermax * 8, hipMemcpyDeviceToHost, s->stream));
-  HIPCK(hipMemcpyAsync(b.data(), s->ws.beta, (nitermax + 1) * 8, hipMemcpyDeviceToHost, s->stream));
+  HIPCK(hipMemcpyAsync(a.data(), s->ws.alpha, nitermax * 8, hipMemcpyDeviceToHost, d.st));
+  HIPCK(hipMemcpyAsync(b.data(), s->ws.beta, (nitermax + 1) * 8, hipMemcpyDeviceToHost, d.st));
   LancState hs;
-  HIPCK(hipMemcpyAsync(&hs, s->ws.st, sizeof(hs), hipMemcpyDeviceToHost, s->stream));
-  HIPCK(hipStreamSynchronize(s->stream));
+  HIPCK(hipMemcpyAsync(&hs, s->ws.st, sizeof(hs), hipMemcpyDeviceToHost, d.st));
+  HIPCK(hipStreamSynchronize(d.st));
   // lanczos_plain_tridiag_c: alanc(iter)=a; if(iter<nitermax)blanc(iter+1)=b; exit if |b|<thr
   int n = hs.iter;
   for (int q = 0; q < nitermax; q++) {
@@ -838,31 +987,30 @@ int ed_sector_lanc_eigh(ed_sector* s, int32_t vtype, const void* v0, int32_t nit
   if (ncheck < 1) ncheck = 10;
   HIPCK(hipSetDevice(s->device));
   const int vc = vtype ? 1 : 0;
-  if (vc == 0 && s->hc) return fail(ED_ERR_ARG, "complex H needs vtype=1");
   const size_t vs = vc ? 16 : 8;
   // keep the Krylov basis when it fits in 1/4 of free memory (no second pass)
   size_t fr = 0, tot = 0;
   HIPCK(hipMemGetInfo(&fr, &tot));
   const bool keep = vect && ((double)nitermax * s->dim * vs < 0.25 * (double)fr);
+  LancDriver d;
+  CK(make_driver(s, vtype, keep, &d));
   CK(lanc_prepare(s, vc, nitermax, keep, keep ? nitermax : 0));
-  CK(lanc_load_start(s, vc, v0));
-  const int path = resolve_path(s, -1);
-  CK(vc ? lanc_start<true>(s, threshold, s->stream) : lanc_start<false>(s, threshold, s->stream));
+  CK(lanc_load_start(s, vc, v0, false));
+  CK(d.start(threshold));
   // lanczos_plain_c convergence test, evaluated on the host between chunks
   std::vector<double> a(nitermax + 2, 0.0), b(nitermax + 2, 0.0), esave;
   int done_iters = 0, nl = 0;
   bool stop = false;
-  const int chunk = 32;
+  const int chunk = d.pm >= 0 ? 64 : 32;
   while (!stop && done_iters < nitermax) {
     int n = std::min(chunk, nitermax - done_iters);
     const int expected = done_iters + n;
-    CK(vc ? lanc_iters<true>(s, path, keep, n, s->stream)
-          : lanc_iters<false>(s, path, keep, n, s->stream));
-    HIPCK(hipMemcpyAsync(a.data(), s->ws.alpha, nitermax * 8, hipMemcpyDeviceToHost, s->stream));
-    HIPCK(hipMemcpyAsync(b.data(), s->ws.beta, (nitermax + 1) * 8, hipMemcpyDeviceToHost, s->stream));
+    CK(d.iters(n, done_iters == 0));
+    HIPCK(hipMemcpyAsync(a.data(), s->ws.alpha, nitermax * 8, hipMemcpyDeviceToHost, d.st));
+    HIPCK(hipMemcpyAsync(b.data(), s->ws.beta, (nitermax + 1) * 8, hipMemcpyDeviceToHost, d.st));
     LancState hs;
-    HIPCK(hipMemcpyAsync(&hs, s->ws.st, sizeof(hs), hipMemcpyDeviceToHost, s->stream));
-    HIPCK(hipStreamSynchronize(s->stream));
+    HIPCK(hipMemcpyAsync(&hs, s->ws.st, sizeof(hs), hipMemcpyDeviceToHost, d.st));
+    HIPCK(hipStreamSynchronize(d.st));
     int have = hs.iter;
     for (int it = done_iters + 1; it <= have && !stop; it++) {
       // iteration `it`: a = a[it-1], b = b[it]
@@ -879,11 +1027,11 @@ int ed_sector_lanc_eigh(ed_sector* s, int32_t vtype, const void* v0, int32_t nit
     done_iters = have;
   }
   // Ritz value and vector of the truncated tridiagonal (nl iterations)
-  std::vector<double> d(a.begin(), a.begin() + nl), e(nl, 0.0), z((size_t)nl * nl, 0.0);
+  std::vector<double> dg(a.begin(), a.begin() + nl), e(nl, 0.0), z((size_t)nl * nl, 0.0);
   for (int q = 1; q < nl; q++) e[q] = b[q];
   for (int q = 0; q < nl; q++) z[q + (size_t)nl * q] = 1.0;
-  if (nl > 0) tql2(nl, d.data(), e.data(), z.data());
-  *egs = nl > 0 ? d[0] : 0.0;
+  if (nl > 0) tql2(nl, dg.data(), e.data(), z.data());
+  *egs = nl > 0 ? dg[0] : 0.0;
   if (nlanc) *nlanc = nl;
   if (vect && nl > 0) {
     LancWS& w = s->ws;
@@ -898,11 +1046,12 @@ int ed_sector_lanc_eigh(ed_sector* s, int32_t vtype, const void* v0, int32_t nit
                            (const double*)w.basis, w.z, nl, s->dim, (double*)w.Y, w.st, slot);
     } else {
       // second pass as lanczos_plain_c (:374-381): rerun the recurrence, y += Z(it,1) v_it
+      // (multi-kernel recurrence: its P buffer holds v_it after each step)
       HIPCK(hipMemsetAsync(w.Y, 0, s->dim * vs, s->stream));
-      CK(lanc_load_start(s, vc, v0));
+      CK(lanc_load_start(s, vc, v0, false));
       CK(vc ? lanc_start<true>(s, threshold, s->stream) : lanc_start<false>(s, threshold, s->stream));
       for (int it = 0; it < nl; it++) {
-        CK(vc ? lanc_iter<true>(s, path, false, s->stream) : lanc_iter<false>(s, path, false, s->stream));
+        CK(vc ? lanc_iter<true>(s, d.path, false, s->stream) : lanc_iter<false>(s, d.path, false, s->stream));
         if (vc)
           hipLaunchKernelGGL(k_axpy_p<true>, dim3(grid_for(s->dim)), dim3(kBlock), 0, s->stream,
                              (const double2*)w.P, w.z, it, s->dim, (double2*)w.Y);

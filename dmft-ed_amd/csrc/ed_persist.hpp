@@ -1,0 +1,252 @@
+// ed_persist.hpp — one-workgroup persistent Lanczos for small sectors.
+//
+// For sectors whose Lanczos vector fits in LDS (configs[1]: dim 4,900 real =
+// 39 KB) the per-iteration cost of the multi-kernel recurrence is launch and
+// grid-reduction latency, not bandwidth (≈10 µs per iteration for 4,900 rows).
+// Here one 1024-thread workgroup (16 wavefronts, one CU) runs many
+// iterations of the .repo/PLAIN_LANCZOS.f90:87-118 recurrence without leaving
+// the CU:
+//   * v (the current normalised Lanczos vector) lives in LDS and is gathered
+//     by the H·v; p = v_{k-1} and w live in registers of the thread that owns
+//     the row (row i = tid + r*1024, r < RPT);
+//   * H is the stored SELL-64 matrix streamed from L2 (MODE 0, same element
+//     order as k_spmv -> same H·v bits) or the Kronecker tables copied into
+//     LDS (MODE 1, normal mode without Jx/Jp);
+//   * alpha and beta are block reductions (wave shuffles + 16-entry LDS),
+//     three barriers per iteration, no global synchronisation.
+// Independent runs (GF seeds, sector replicas) use one workgroup each
+// (blockIdx.x indexes PersistRun[]), so up to 256 chains run side by side.
+#pragma once
+#include "ed_kernels.hpp"
+
+namespace edg {
+
+constexpr int kPBlock = 1024;
+
+template <bool HC>
+struct PersistRun {
+  using H = val_t<HC>;
+  // stored matrix (MODE 0)
+  const H* diag;
+  const int64_t* sptr;
+  const int32_t* cols;
+  const H* vals;
+  // Kronecker tables (MODE 1)
+  KronArgs<HC> K;
+  int64_t dim;
+  void* R;           // in: start vector (first) or saved v; out: saved v
+  void* P;           // saved p
+  LancState* st;     // beta, iter, done, thresh
+  double* alpha;     // [niter_total]
+  double* beta;      // [niter_total+1]
+  void* basis;       // optional Krylov basis (column k = v_k), or null
+  int niter;         // iterations in this launch
+  int first;         // 1: R holds the unnormalised start vector
+};
+
+__device__ __forceinline__ double pblock_sum(double v, double* ws) {
+  v = wave_sum(v);
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) ws[wv] = v;
+  __syncthreads();
+  double t = 0.0;
+#pragma unroll
+  for (int w = 0; w < kPBlock / 64; w++) t = t + ws[w];
+  __syncthreads();
+  return t;
+}
+
+template <bool HC, bool VC, int MODE, int RPT>
+__global__ void __launch_bounds__(kPBlock) k_lanc_persist(const PersistRun<HC>* __restrict__ runs) {
+  using V = val_t<VC>;
+  using H = val_t<HC>;
+  const PersistRun<HC> a = runs[blockIdx.x];
+  extern __shared__ __align__(16) unsigned char smem[];
+  __shared__ double ws[kPBlock / 64];
+  V* vl = (V*)smem;
+  const int64_t dim = a.dim;
+  const int tid = threadIdx.x;
+  V* Rg = (V*)a.R;
+  V* Pg = (V*)a.P;
+  LancState* st = a.st;
+
+  // --- Kronecker tables into LDS (after v)
+  const H* aup = nullptr;
+  const H* adw = nullptr;
+  const H* upv = nullptr;
+  const H* dwv = nullptr;
+  const int32_t* upc = nullptr;
+  const int32_t* dwc = nullptr;
+  const uint8_t* impu = nullptr;
+  const uint8_t* impd = nullptr;
+  const double* uimp = nullptr;
+  if constexpr (MODE == 1) {
+    const KronArgs<HC>& K = a.K;
+    unsigned char* q = smem + ((dim * sizeof(V) + 15) & ~(int64_t)15);
+    auto carve = [&](int64_t bytes) {
+      unsigned char* r = q;
+      q += (bytes + 15) & ~(int64_t)15;
+      return r;
+    };
+    H* s_aup = (H*)carve(K.dimup * sizeof(H));
+    H* s_adw = (H*)carve(K.dimdw * sizeof(H));
+    H* s_upv = (H*)carve((int64_t)K.degup * K.dimup * sizeof(H));
+    H* s_dwv = (H*)carve((int64_t)K.degdw * K.dimdw * sizeof(H));
+    int32_t* s_upc = (int32_t*)carve((int64_t)K.degup * K.dimup * 4);
+    int32_t* s_dwc = (int32_t*)carve((int64_t)K.degdw * K.dimdw * 4);
+    uint8_t* s_impu = (uint8_t*)carve(K.dimup);
+    uint8_t* s_impd = (uint8_t*)carve(K.dimdw);
+    double* s_uimp = (double*)carve((int64_t)K.nimp * K.nimp * 8);
+    for (int64_t t = tid; t < K.dimup; t += kPBlock) { s_aup[t] = K.aup[t]; s_impu[t] = K.impu[t]; }
+    for (int64_t t = tid; t < K.dimdw; t += kPBlock) { s_adw[t] = K.adw[t]; s_impd[t] = K.impd[t]; }
+    for (int64_t t = tid; t < (int64_t)K.degup * K.dimup; t += kPBlock) { s_upv[t] = K.upv[t]; s_upc[t] = K.upc[t]; }
+    for (int64_t t = tid; t < (int64_t)K.degdw * K.dimdw; t += kPBlock) { s_dwv[t] = K.dwv[t]; s_dwc[t] = K.dwc[t]; }
+    for (int t = tid; t < K.nimp * K.nimp; t += kPBlock) s_uimp[t] = K.uimp[t];
+    aup = s_aup; adw = s_adw; upv = s_upv; dwv = s_dwv; upc = s_upc; dwc = s_dwc;
+    impu = s_impu; impd = s_impd; uimp = s_uimp;
+  }
+
+  // --- state in
+  V p[RPT];
+  int32_t iw[RPT], iu[RPT];
+  double b;
+  int it0;
+  {
+    double nrm = 0.0;
+#pragma unroll
+    for (int r = 0; r < RPT; r++) {
+      const int64_t i = tid + (int64_t)r * kPBlock;
+      p[r] = vzero<V>();
+      if (i < dim) {
+        V x = Rg[i];
+        vl[i] = x;
+        if (a.first) nrm += redot(x, x);
+        else p[r] = Pg[i];
+        if constexpr (MODE == 1) {
+          iw[r] = (int32_t)(i / a.K.dimup);
+          iu[r] = (int32_t)(i - (int64_t)iw[r] * a.K.dimup);
+        }
+      }
+    }
+    if (a.first) {
+      double n2 = pblock_sum(nrm, ws);  // includes barrier: vl complete
+      if (n2 == 0.0) {                  // lanczos_plain_iteration: "norm =0!!"
+        if (tid == 0) { st->iter = 0; st->done = 1; st->beta = 0.0; }
+        return;
+      }
+      const double inv = 1.0 / sqrt(n2);
+#pragma unroll
+      for (int r = 0; r < RPT; r++) {
+        const int64_t i = tid + (int64_t)r * kPBlock;
+        if (i < dim) vl[i] = scl(inv, vl[i]);
+      }
+      b = 0.0;
+      it0 = 0;
+      if (tid == 0) {
+        st->iter = 0;
+        st->done = 0;
+        st->beta = 0.0;
+      }
+    } else {
+      b = st->beta;
+      it0 = st->iter;
+    }
+    __syncthreads();
+  }
+  if (st->done && !a.first) return;
+
+  for (int k = 0; k < a.niter; k++) {
+    const int it = it0 + k;
+    // ---- w = H v - b p ; alpha partial
+    V w[RPT];
+    double ap = 0.0;
+#pragma unroll
+    for (int r = 0; r < RPT; r++) {
+      const int64_t i = tid + (int64_t)r * kPBlock;
+      w[r] = vzero<V>();
+      if (i < dim) {
+        const V xi = vl[i];
+        V acc;
+        if constexpr (MODE == 0) {
+          const int64_t s = i >> 6, s0 = a.sptr[s];
+          const int wd = (int)((a.sptr[s + 1] - s0) >> 6);
+          const int64_t base = s0 + (i & 63);
+          acc = add(vzero<V>(), mul(a.diag[i], xi));
+          for (int kk = 0; kk < wd; kk++) {
+            const int64_t q = base + 64 * (int64_t)kk;
+            acc = add(acc, mul(a.vals[q], vl[a.cols[q]]));
+          }
+        } else {
+          const int64_t du = a.K.dimup, dd = a.K.dimdw;
+          auto d = add(add(aup[iu[r]], adw[iw[r]]),
+                       mk<HC>(uimp[impu[iu[r]] * a.K.nimp + impd[iw[r]]], 0.0));
+          acc = mul(d, xi);
+          const V* xrow = vl + (int64_t)iw[r] * du;
+          for (int kk = 0; kk < a.K.degup; kk++) {
+            const int64_t q = (int64_t)kk * du + iu[r];
+            acc = add(acc, mul(upv[q], xrow[upc[q]]));
+          }
+          for (int kk = 0; kk < a.K.degdw; kk++) {
+            const int64_t q = (int64_t)kk * dd + iw[r];
+            acc = add(acc, mul(dwv[q], vl[(int64_t)dwc[q] * du + iu[r]]));
+          }
+        }
+        w[r] = sub(acc, scl(b, p[r]));
+        ap += redot(xi, w[r]);
+        if (a.basis) ((V*)a.basis)[(int64_t)it * dim + i] = xi;
+      }
+    }
+    const double alpha = pblock_sum(ap, ws);
+    // ---- w -= alpha v ; beta
+    double bp = 0.0;
+#pragma unroll
+    for (int r = 0; r < RPT; r++) {
+      const int64_t i = tid + (int64_t)r * kPBlock;
+      if (i < dim) {
+        w[r] = sub(w[r], scl(alpha, vl[i]));
+        bp += redot(w[r], w[r]);
+      }
+    }
+    const double bn = sqrt(pblock_sum(bp, ws));
+    if (tid == 0) {
+      a.alpha[it] = alpha;
+      a.beta[it + 1] = bn;
+    }
+    const bool stop = bn < st->thresh;
+    // ---- p <- v ; v <- w / b
+    const double inv = 1.0 / bn;
+#pragma unroll
+    for (int r = 0; r < RPT; r++) {
+      const int64_t i = tid + (int64_t)r * kPBlock;
+      if (i < dim) {
+        p[r] = vl[i];
+        vl[i] = scl(inv, w[r]);
+      }
+    }
+    b = bn;
+    __syncthreads();
+    if (stop) {
+      if (tid == 0) {
+        st->done = 1;
+        st->iter = it + 1;
+        st->beta = bn;
+      }
+      return;
+    }
+  }
+  // ---- state out
+#pragma unroll
+  for (int r = 0; r < RPT; r++) {
+    const int64_t i = tid + (int64_t)r * kPBlock;
+    if (i < dim) {
+      Rg[i] = vl[i];
+      Pg[i] = p[r];
+    }
+  }
+  if (tid == 0) {
+    st->iter = it0 + a.niter;
+    st->beta = b;
+  }
+}
+
+}  // namespace edg

@@ -141,6 +141,21 @@ int ed_sector_map(const ed_sector* s, uint32_t* map_host);
  * vals is complex interleaved (2*nnz doubles).  Requires ED_STORED. */
 int ed_sector_dump_csr(const ed_sector* s, int64_t* rowptr, int32_t* cols, double* vals);
 
+/* Read-only view of the device SELL-64 arrays of a stored sector (for
+ * inspection / kernel experiments).  Entry k of row r lives at
+ * sptr[r/64] + 64*k + r%64; the diagonal is separate.  vals/diag are real(8)
+ * when value_bytes == 8, complex(8) interleaved when 16. */
+typedef struct ed_sell_view {
+  int64_t dim, nslice, slots;
+  int32_t value_bytes, pad;
+  const void* diag;
+  const int64_t* sptr;
+  const int32_t* cols;
+  const void* vals;
+  const uint16_t* rowcnt;
+} ed_sell_view;
+int ed_sector_sell_view(const ed_sector* s, ed_sell_view* view);
+
 /* Device-resident plain Lanczos (3-term recurrence, no reorthogonalisation).
  * v0: host start vector (vtype as above) of length dim, or NULL for the
  * deterministic default start vector.  Outputs on the host. */

@@ -24,9 +24,15 @@ def _e0_scipy(csr, dim):
     return float(sla.eigsh(A, k=1, which="SA", tol=1e-14)[0][0])
 
 
+@pytest.mark.parametrize("persist", [True, False], ids=["persistent", "multikernel"])
 @pytest.mark.parametrize("name,factory,sectors", CASES, ids=[c[0] for c in CASES])
-def test_tridiag_and_ground_state(name, factory, sectors):
+def test_tridiag_and_ground_state(name, factory, sectors, persist, monkeypatch):
+    """Both device recurrences: the one-workgroup persistent kernel (default for
+    sectors that fit one CU's LDS) and the graph-captured two-kernel one."""
     from edgpu.hamiltonian import Sector
+
+    if not persist:
+        monkeypatch.setenv("ED_GPU_NO_PERSIST", "1")
 
     cfg = factory()
     orc = Oracle(cfg)
@@ -69,3 +75,22 @@ def test_real_lanczos_c2():
     with Sector(cfg, 4, 4, stored=False, direct=True, real=True) as S:
         e1, _, _ = S.lanc_eigh(nitermax=512, threshold=1e-12, vector=False)
         assert abs(e1 - e0) <= 1e-10 * abs(e0)
+
+
+@pytest.mark.parametrize("path", ["stored", "kron"])
+def test_persistent_matches_multikernel(path, monkeypatch):
+    """Same start vector, same sector: the two recurrences agree step by step
+    (first 40 steps to 1e-9; only the reduction order differs)."""
+    from edgpu.hamiltonian import Sector
+    from cases import c2
+
+    cfg = c2()
+    kw = dict(stored=True) if path == "stored" else dict(stored=False, direct=True)
+    with Sector(cfg, 4, 4, real=True, **kw) as S:
+        v0 = np.sin(np.arange(1, S.dim + 1, dtype=np.float64))
+        a1, b1, n1 = S.lanc_tridiag(v0, 60)
+        monkeypatch.setenv("ED_GPU_NO_PERSIST", "1")
+        a2, b2, n2 = S.lanc_tridiag(v0, 60)
+    assert n1 == n2 == 60
+    np.testing.assert_allclose(a1[:40], a2[:40], rtol=1e-9, atol=1e-11)
+    np.testing.assert_allclose(b1[:40], b2[:40], rtol=1e-9, atol=1e-11)
