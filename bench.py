@@ -144,6 +144,15 @@ def main():
     iters_total = args.steps * args.niter * world
     value = iters_total / dt
 
+    # configs[2]: the same sector through the matrix-free kernel (rank-local, untimed by the
+    # barrier bracket above; device time of the same 512-iteration runs)
+    Sd = Sector(cfg, 4, 4, stored=False, direct=True, real=True, device=dev)
+    for _ in range(2):
+        Sd.lanc_run(args.niter, v0_dev=v0)
+    dms = [Sd.lanc_run(args.niter, v0_dev=v0)[2] for _ in range(5)]
+    direct_ips = args.niter / (min(dms) * 1e-3)
+    Sd.close()
+
     out = None
     if rank == 0:
         # SpMV GB/s on the headline sector (L2-resident; launch-latency bound)
@@ -179,6 +188,8 @@ def main():
                                    f"stored real(8) H, plain Lanczos {args.niter} iters/step",
                        "parallelism": f"sector replicas x{world}"},
             "device_ms_per_step": round(dev_ms / args.steps, 4),
+            "direct_iters_per_s": round(direct_ips, 1),
+            "direct_note": "configs[2]: same sector, matrix-free H·v (Kronecker form, tables in LDS), one GPU",
             "spmv_gbs_c2": round(gbs2, 1),
             "spmv_ms_c2": round(ms2, 5),
             "roofline": roof,

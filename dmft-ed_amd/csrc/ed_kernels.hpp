@@ -321,7 +321,31 @@ struct EpiLancA {
 };
 
 // ------------------------------------------------------------- stored H·v
-template <bool HC, bool VC, class Epi>
+// Matrix-stream loads; NT=1 marks them non-temporal (used when the matrix does
+// not fit the 256 MB Infinity Cache, so caching it only evicts v).
+template <int NT, class T>
+__device__ __forceinline__ T ldm(const T* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <int NT>
+__device__ __forceinline__ double2 ldm2(const double2* p) {
+  if constexpr (NT) {
+    const double* q = (const double*)p;
+    return make_double2(__builtin_nontemporal_load(q), __builtin_nontemporal_load(q + 1));
+  } else {
+    return *p;
+  }
+}
+template <int NT> __device__ __forceinline__ double ldh(const double* p) { return ldm<NT>(p); }
+template <int NT> __device__ __forceinline__ double2 ldh(const double2* p) { return ldm2<NT>(p); }
+
+// One thread per row; the row's entries are fetched in chunks of kChunk with
+// every column and value load of a chunk issued before the gathers (measured
+// +10-14 % over a plain loop on the Nlevels=28 sector), summed in row order.
+constexpr int kChunk = 16;
+
+template <bool HC, bool VC, int NT, class Epi>
 __global__ void __launch_bounds__(kBlock) k_spmv(const val_t<HC>* __restrict__ diag,
                                                  const int64_t* __restrict__ sptr,
                                                  const int32_t* __restrict__ cols,
@@ -329,6 +353,7 @@ __global__ void __launch_bounds__(kBlock) k_spmv(const val_t<HC>* __restrict__ d
                                                  const val_t<VC>* __restrict__ x, int64_t dim,
                                                  int64_t nslice, Epi epi) {
   using V = val_t<VC>;
+  using H = val_t<HC>;
   if (epi.skip()) return;
   epi.prepare();
   double part = 0.0;
@@ -338,14 +363,25 @@ __global__ void __launch_bounds__(kBlock) k_spmv(const val_t<HC>* __restrict__ d
       const int64_t s = i >> 6;
       const int64_t s0 = sptr[s];
       const int w = (int)((sptr[s + 1] - s0) >> 6);
-      const int64_t base = s0 + (i & 63);
+      const int32_t* cp = cols + s0 + (i & 63);
+      const H* vp = vals + s0 + (i & 63);
       const V xi = x[i];
       // spMatVec_cc: Hv=0; Hv(i)=Hv(i)+vals(j)*v(cols(j)), diagonal first
-      V acc = add(vzero<V>(), mul(diag[i], xi));
-#pragma unroll 4
-      for (int k = 0; k < w; k++) {
-        const int64_t q = base + 64 * (int64_t)k;
-        acc = add(acc, mul(vals[q], x[cols[q]]));
+      V acc = add(vzero<V>(), mul(ldh<NT>(diag + i), xi));
+      for (int k0 = 0; k0 < w; k0 += kChunk) {
+        int32_t c[kChunk];
+        H h[kChunk];
+#pragma unroll
+        for (int k = 0; k < kChunk; k++) c[k] = (k0 + k < w) ? ldm<NT>(cp + 64 * (k0 + k)) : (int32_t)i;
+#pragma unroll
+        for (int k = 0; k < kChunk; k++)
+          h[k] = (k0 + k < w) ? ldh<NT>(vp + 64 * (k0 + k)) : mk<HC>(0.0, 0.0);
+        V g[kChunk];
+#pragma unroll
+        for (int k = 0; k < kChunk; k++) g[k] = x[c[k]];
+#pragma unroll
+        for (int k = 0; k < kChunk; k++)
+          if (k0 + k < w) acc = add(acc, mul(h[k], g[k]));
       }
       part += epi.row(i, acc, xi);
     }

@@ -39,7 +39,7 @@ static int fail(int code, const std::string& msg) {
     if (r_ != ED_OK) return r_; \
   } while (0)
 
-static constexpr int kMaxGrid = 8192;
+static constexpr int kMaxGrid = 65536;  // one thread per row up to 16.7 M rows
 static inline int grid_for(int64_t nthreads) {
   int64_t b = (nthreads + kBlock - 1) / kBlock;
   return (int)std::max<int64_t>(1, std::min<int64_t>(b, kMaxGrid));
@@ -336,9 +336,16 @@ static int launch_hxv_t(ed_sector* s, int path, const void* x, Epi epi, hipStrea
   const int64_t dim = s->dim, ns = s->nslice;
   const int g = grid_for(ns * 64);
   if (path == 0) {
-    hipLaunchKernelGGL((k_spmv<HC, VC, Epi>), dim3(g), dim3(kBlock), 0, st,
-                       (const val_t<HC>*)s->d_diag, s->d_sptr, s->d_cols,
-                       (const val_t<HC>*)s->d_vals, (const V*)x, dim, ns, epi);
+    // non-temporal matrix loads once the matrix cannot stay in the 256 MB MALL
+    const int64_t mbytes = s->padded * (4 + (HC ? 16 : 8)) + dim * (HC ? 16 : 8);
+    if (mbytes > (int64_t)192 << 20)
+      hipLaunchKernelGGL((k_spmv<HC, VC, 1, Epi>), dim3(g), dim3(kBlock), 0, st,
+                         (const val_t<HC>*)s->d_diag, s->d_sptr, s->d_cols,
+                         (const val_t<HC>*)s->d_vals, (const V*)x, dim, ns, epi);
+    else
+      hipLaunchKernelGGL((k_spmv<HC, VC, 0, Epi>), dim3(g), dim3(kBlock), 0, st,
+                         (const val_t<HC>*)s->d_diag, s->d_sptr, s->d_cols,
+                         (const val_t<HC>*)s->d_vals, (const V*)x, dim, ns, epi);
   } else if (path == 1) {
     DevIndex idx{s->d_off, s->d_rank, s->T.ns, s->T.nst - 1};
     hipLaunchKernelGGL((k_direct<HC, VC, Epi>), dim3(g), dim3(kBlock), 0, st, s->Md, s->d_map, idx,

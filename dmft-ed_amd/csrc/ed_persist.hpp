@@ -22,6 +22,7 @@
 namespace edg {
 
 constexpr int kPBlock = 1024;
+constexpr int kPChunk = 16;
 
 template <bool HC>
 struct PersistRun {
@@ -170,11 +171,20 @@ __global__ void __launch_bounds__(kPBlock) k_lanc_persist(const PersistRun<HC>* 
         if constexpr (MODE == 0) {
           const int64_t s = i >> 6, s0 = a.sptr[s];
           const int wd = (int)((a.sptr[s + 1] - s0) >> 6);
-          const int64_t base = s0 + (i & 63);
+          const int32_t* cp = a.cols + s0 + (i & 63);
+          const H* vp = a.vals + s0 + (i & 63);
           acc = add(vzero<V>(), mul(a.diag[i], xi));
-          for (int kk = 0; kk < wd; kk++) {
-            const int64_t q = base + 64 * (int64_t)kk;
-            acc = add(acc, mul(a.vals[q], vl[a.cols[q]]));
+          for (int k0 = 0; k0 < wd; k0 += kPChunk) {
+            int32_t c[kPChunk];
+            H h[kPChunk];
+#pragma unroll
+            for (int kk = 0; kk < kPChunk; kk++) c[kk] = (k0 + kk < wd) ? cp[64 * (k0 + kk)] : 0;
+#pragma unroll
+            for (int kk = 0; kk < kPChunk; kk++)
+              h[kk] = (k0 + kk < wd) ? vp[64 * (k0 + kk)] : mk<HC>(0.0, 0.0);
+#pragma unroll
+            for (int kk = 0; kk < kPChunk; kk++)
+              if (k0 + kk < wd) acc = add(acc, mul(h[kk], vl[c[kk]]));
           }
         } else {
           const int64_t du = a.K.dimup, dd = a.K.dimdw;
