@@ -81,31 +81,55 @@ __device__ __forceinline__ double block_sum(double v) {
 
 struct RedSlot {
   double* partials;       // [gridDim.x]
-  unsigned int* counter;  // zero on entry; reset by the last block
+  unsigned int* counter;  // zero on entry; reset by the last block.  nullptr:
+                          // two-pass mode (plain partial stores, a one-block
+                          // finishing kernel sums them after the boundary)
 };
+
+// Largest grid that finishes its reduction in-kernel: one ticket word takes
+// ~88 atomics/us (MI355X_MICROARCH.md, row "dequeue"), so thousands of blocks
+// would serialise on it; beyond this the finishing kernel is cheaper.
+constexpr int kTicketMaxBlocks = 128;
+
+// Two-pass mode, pass 1: block partial -> partials[blockIdx.x].
+__device__ __forceinline__ void block_partial(double v, double* partials) {
+  double s = block_sum(v);
+  if (threadIdx.x == 0) partials[blockIdx.x] = s;
+}
+// Pass 2 (one 256-thread block): the same fixed-order sum as grid_reduce_last.
+__device__ __forceinline__ double sum_partials(const double* partials, int n) {
+  double a = 0.0;
+  for (int b = threadIdx.x; b < n; b += kBlock) a = a + partials[b];
+  return block_sum(a);
+}
 
 // Block-partial sum -> partials; the last block to arrive (atomic ticket)
 // returns true with the full sum in *total (fixed order: independent of
 // arrival order).
+//
+// Hand-off protocol (MI355X_MICROARCH.md, "Valid forms", first table row):
+// one lane per block stores its partial write-through (relaxed agent-scope
+// atomic store = global_store ... sc1), drains it with s_waitcnt vmcnt(0),
+// then takes a ticket with an agent-scope atomic add; the block whose add
+// returns gridDim-1 reads every partial with sc1 loads (relaxed agent-scope
+// atomic loads) after a workgroup barrier.  No release/acquire fence: a
+// release fence (buffer_wbl2) per block writes back the XCD L2's dirty lines
+// and, with thousands of blocks that just wrote H·v outputs, serialises the
+// kernel (measured 7x slower Lanczos steps on the c4 sector).
 __device__ __forceinline__ bool grid_reduce_last(double v, RedSlot slot, double* total) {
   __shared__ int amlast;
   double s = block_sum(v);
   if (threadIdx.x == 0) {
-    slot.partials[blockIdx.x] = s;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __hip_atomic_store(slot.partials + blockIdx.x, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    unsigned int t = atomicAdd(slot.counter, 1u);
+    unsigned int t = __hip_atomic_fetch_add(slot.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     amlast = (t == gridDim.x - 1);
   }
   __syncthreads();
   if (!amlast) return false;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
   double a = 0.0;
-  for (unsigned int b = threadIdx.x; b < gridDim.x; b += kBlock) a = a + slot.partials[b];
+  for (unsigned int b = threadIdx.x; b < gridDim.x; b += kBlock)
+    a = a + __hip_atomic_load(slot.partials + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   *total = block_sum(a);
   if (threadIdx.x == 0) *slot.counter = 0u;
   return true;
@@ -312,6 +336,10 @@ struct EpiLancA {
     return redot(v, w);
   }
   __device__ __forceinline__ void finish(double part) {
+    if (!slot.counter) {
+      block_partial(part, slot.partials);
+      return;
+    }
     double tot;
     if (grid_reduce_last(part, slot, &tot) && threadIdx.x == 0) {
       st->alpha = tot;
@@ -319,6 +347,32 @@ struct EpiLancA {
     }
   }
 };
+
+// Two-pass finishing kernels of one Lanczos step (one block of kBlock threads).
+__global__ void __launch_bounds__(kBlock) k_lanc_fin_a(const double* __restrict__ partials, int n,
+                                                       LancState* st, double* alpha_out) {
+  if (st->done) return;
+  const double tot = sum_partials(partials, n);
+  if (threadIdx.x == 0) {
+    st->alpha = tot;
+    alpha_out[st->iter] = tot;
+  }
+}
+__device__ __forceinline__ void lanc_set_beta(double tot, LancState* st, double* beta_out) {
+  const double b = sqrt(tot);
+  const int it = st->iter;
+  beta_out[it + 1] = b;
+  st->beta = b;
+  st->invb = 1.0 / b;
+  st->iter = it + 1;
+  if (b < st->thresh) st->done = 1;
+}
+__global__ void __launch_bounds__(kBlock) k_lanc_fin_b(const double* __restrict__ partials, int n,
+                                                       LancState* st, double* beta_out) {
+  if (st->done) return;
+  const double tot = sum_partials(partials, n);
+  if (threadIdx.x == 0) lanc_set_beta(tot, st, beta_out);
+}
 
 // ------------------------------------------------------------- stored H·v
 // Matrix-stream loads; NT=1 marks them non-temporal (used when the matrix does
@@ -527,16 +581,12 @@ __global__ void __launch_bounds__(kBlock) k_lanc_b(const val_t<VC>* __restrict__
     R[i] = w;
     part += redot(w, w);
   }
-  double tot;
-  if (grid_reduce_last(part, slot, &tot) && threadIdx.x == 0) {
-    double b = sqrt(tot);
-    int it = st->iter;
-    beta_out[it + 1] = b;
-    st->beta = b;
-    st->invb = 1.0 / b;
-    st->iter = it + 1;
-    if (b < st->thresh) st->done = 1;
+  if (!slot.counter) {
+    block_partial(part, slot.partials);
+    return;
   }
+  double tot;
+  if (grid_reduce_last(part, slot, &tot) && threadIdx.x == 0) lanc_set_beta(tot, st, beta_out);
 }
 
 // Ritz vector from the stored Krylov basis: y = sum_k z_k v_k; st->tmp = ||y||.

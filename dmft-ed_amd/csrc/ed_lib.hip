@@ -44,6 +44,9 @@ static inline int grid_for(int64_t nthreads) {
   int64_t b = (nthreads + kBlock - 1) / kBlock;
   return (int)std::max<int64_t>(1, std::min<int64_t>(b, kMaxGrid));
 }
+// one-off grid reductions (in-kernel ticket): few enough blocks that the
+// ticket word does not serialise (grid-strided kernels)
+static inline int grid_once(int64_t nthreads) { return std::min(grid_for(nthreads), 512); }
 
 // -------------------------------------------------------------- sector obj
 struct KronHost {
@@ -414,7 +417,7 @@ static int lanc_start(ed_sector* s, double thresh, hipStream_t st) {
   RedSlot slot{w.partials, w.counter};
   HIPCK(hipMemsetAsync(w.beta, 0, (w.cap + 2) * sizeof(double), st));
   HIPCK(hipMemsetAsync(w.alpha, 0, (w.cap + 2) * sizeof(double), st));
-  hipLaunchKernelGGL(k_lanc_init<VC>, dim3(grid_for(s->dim)), dim3(kBlock), 0, st,
+  hipLaunchKernelGGL(k_lanc_init<VC>, dim3(grid_once(s->dim)), dim3(kBlock), 0, st,
                      (const val_t<VC>*)w.R, (val_t<VC>*)w.P, s->dim, w.st, thresh, slot);
   HIPCK(hipGetLastError());
   return ED_OK;
@@ -423,6 +426,8 @@ static int lanc_start(ed_sector* s, double thresh, hipStream_t st) {
 template <bool VC>
 static int lanc_iter(ed_sector* s, int path, bool basis, hipStream_t st) {
   LancWS& w = s->ws;
+  const int g1 = grid_for(s->nslice * 64), g2 = grid_for(s->dim);
+  const bool two1 = g1 > kTicketMaxBlocks, two2 = g2 > kTicketMaxBlocks;
   EpiLancA<VC> e;
   e.st = w.st;
   e.P = (val_t<VC>*)w.P;
@@ -430,12 +435,13 @@ static int lanc_iter(ed_sector* s, int path, bool basis, hipStream_t st) {
   e.basis = basis ? (val_t<VC>*)w.basis : nullptr;
   e.dim = s->dim;
   e.alpha_out = w.alpha;
-  e.slot = RedSlot{w.partials, w.counter};
+  e.slot = RedSlot{w.partials, two1 ? nullptr : w.counter};
   CK(launch_hxv<VC>(s, path, w.R, e, st));
-  RedSlot slot2{w.partials, w.counter + 1};
-  hipLaunchKernelGGL(k_lanc_b<VC>, dim3(grid_for(s->dim)), dim3(kBlock), 0, st,
-                     (const val_t<VC>*)w.W, (const val_t<VC>*)w.P, (val_t<VC>*)w.R, s->dim, w.st,
-                     w.beta, slot2);
+  if (two1) hipLaunchKernelGGL(k_lanc_fin_a, dim3(1), dim3(kBlock), 0, st, w.partials, g1, w.st, w.alpha);
+  RedSlot slot2{w.partials, two2 ? nullptr : w.counter + 1};
+  hipLaunchKernelGGL(k_lanc_b<VC>, dim3(g2), dim3(kBlock), 0, st, (const val_t<VC>*)w.W,
+                     (const val_t<VC>*)w.P, (val_t<VC>*)w.R, s->dim, w.st, w.beta, slot2);
+  if (two2) hipLaunchKernelGGL(k_lanc_fin_b, dim3(1), dim3(kBlock), 0, st, w.partials, g2, w.st, w.beta);
   HIPCK(hipGetLastError());
   return ED_OK;
 }
@@ -483,9 +489,15 @@ static constexpr int64_t kLdsBudget = 150 * 1024;
 static int persist_mode(const ed_sector* s, int vc, int path) {
   if (getenv("ED_GPU_NO_PERSIST")) return -1;
   const int64_t vs = vc ? 16 : 8;
-  if (s->dim > 16 * (int64_t)kPBlock) return -1;
+  // rows per thread beyond which the register-resident p/w arrays spill
+  // (-Rpass-analysis: 0-8 B/lane scratch up to 8 real / 5 complex rows)
+  const int64_t rpt_max = (vc || s->hc) ? 5 : 8;
+  if (s->dim > rpt_max * (int64_t)kPBlock) return -1;
   int64_t lds = ((s->dim * vs + 15) & ~(int64_t)15);
-  if (path == 0) return lds <= kLdsBudget ? 0 : -1;
+  // stored mode streams the matrix from L2 through one CU (~40-50 GB/s): the
+  // graph-captured multi-kernel recurrence is faster there (measured c2: 9.8 vs
+  // 8.9 us/step), so it is opt-in
+  if (path == 0) return (getenv("ED_GPU_PERSIST_STORED") && lds <= kLdsBudget) ? 0 : -1;
   if (path == 2) {
     const KronHost& K = s->K;
     const int64_t hs = s->hc ? 16 : 8;
@@ -521,12 +533,19 @@ static int persist_launch_t(ed_sector* s, int64_t lds, hipStream_t st) {
 
 template <bool HC, bool VC, int MODE>
 static int persist_launch_m(ed_sector* s, int64_t lds, hipStream_t st) {
-  const int64_t rpt = (s->dim + kPBlock - 1) / kPBlock;
-  if (rpt <= 1) return persist_launch_t<HC, VC, MODE, 1>(s, lds, st);
-  if (rpt <= 2) return persist_launch_t<HC, VC, MODE, 2>(s, lds, st);
-  if (rpt <= 4) return persist_launch_t<HC, VC, MODE, 4>(s, lds, st);
-  if (rpt <= 8) return persist_launch_t<HC, VC, MODE, 8>(s, lds, st);
-  return persist_launch_t<HC, VC, MODE, 16>(s, lds, st);
+  const int64_t rpt = (s->dim + kPBlock - 1) / kPBlock;  // rows per thread, exact
+  switch (rpt) {
+    case 1: return persist_launch_t<HC, VC, MODE, 1>(s, lds, st);
+    case 2: return persist_launch_t<HC, VC, MODE, 2>(s, lds, st);
+    case 3: return persist_launch_t<HC, VC, MODE, 3>(s, lds, st);
+    case 4: return persist_launch_t<HC, VC, MODE, 4>(s, lds, st);
+    case 5: return persist_launch_t<HC, VC, MODE, 5>(s, lds, st);
+    case 6: return persist_launch_t<HC, VC, MODE, 6>(s, lds, st);
+    case 7: case 8: return persist_launch_t<HC, VC, MODE, 8>(s, lds, st);
+    case 9: case 10: return persist_launch_t<HC, VC, MODE, 10>(s, lds, st);
+    case 11: case 12: return persist_launch_t<HC, VC, MODE, 12>(s, lds, st);
+    default: return persist_launch_t<HC, VC, MODE, 16>(s, lds, st);
+  }
 }
 
 // Launch `niter` persistent iterations.  first=1 starts from the vector in R.
@@ -1046,10 +1065,10 @@ int ed_sector_lanc_eigh(ed_sector* s, int32_t vtype, const void* v0, int32_t nit
     RedSlot slot{w.partials, w.counter + 2};
     if (keep) {
       if (vc)
-        hipLaunchKernelGGL(k_ritz<true>, dim3(grid_for(s->dim)), dim3(kBlock), 0, s->stream,
+        hipLaunchKernelGGL(k_ritz<true>, dim3(grid_once(s->dim)), dim3(kBlock), 0, s->stream,
                            (const double2*)w.basis, w.z, nl, s->dim, (double2*)w.Y, w.st, slot);
       else
-        hipLaunchKernelGGL(k_ritz<false>, dim3(grid_for(s->dim)), dim3(kBlock), 0, s->stream,
+        hipLaunchKernelGGL(k_ritz<false>, dim3(grid_once(s->dim)), dim3(kBlock), 0, s->stream,
                            (const double*)w.basis, w.z, nl, s->dim, (double*)w.Y, w.st, slot);
     } else {
       // second pass as lanczos_plain_c (:374-381): rerun the recurrence, y += Z(it,1) v_it
@@ -1067,10 +1086,10 @@ int ed_sector_lanc_eigh(ed_sector* s, int32_t vtype, const void* v0, int32_t nit
                              (const double*)w.P, w.z, it, s->dim, (double*)w.Y);
       }
       if (vc)
-        hipLaunchKernelGGL(k_norm<true>, dim3(grid_for(s->dim)), dim3(kBlock), 0, s->stream,
+        hipLaunchKernelGGL(k_norm<true>, dim3(grid_once(s->dim)), dim3(kBlock), 0, s->stream,
                            (const double2*)w.Y, s->dim, w.st, slot);
       else
-        hipLaunchKernelGGL(k_norm<false>, dim3(grid_for(s->dim)), dim3(kBlock), 0, s->stream,
+        hipLaunchKernelGGL(k_norm<false>, dim3(grid_once(s->dim)), dim3(kBlock), 0, s->stream,
                            (const double*)w.Y, s->dim, w.st, slot);
     }
     if (vc)

@@ -22,7 +22,7 @@
 namespace edg {
 
 constexpr int kPBlock = 1024;
-constexpr int kPChunk = 16;
+constexpr int kPChunk = 8;
 
 template <bool HC>
 struct PersistRun {
@@ -61,7 +61,7 @@ template <bool HC, bool VC, int MODE, int RPT>
 __global__ void __launch_bounds__(kPBlock) k_lanc_persist(const PersistRun<HC>* __restrict__ runs) {
   using V = val_t<VC>;
   using H = val_t<HC>;
-  const PersistRun<HC> a = runs[blockIdx.x];
+  const PersistRun<HC>& a = runs[blockIdx.x];  // uniform: scalar loads, no VGPR copy
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ double ws[kPBlock / 64];
   V* vl = (V*)smem;
@@ -109,7 +109,7 @@ __global__ void __launch_bounds__(kPBlock) k_lanc_persist(const PersistRun<HC>* 
 
   // --- state in
   V p[RPT];
-  int32_t iw[RPT], iu[RPT];
+  uint32_t rix[RPT];  // Kronecker row index packed (iw << 16) | iu  (DimUp, DimDw < 2^16)
   double b;
   int it0;
   {
@@ -124,8 +124,8 @@ __global__ void __launch_bounds__(kPBlock) k_lanc_persist(const PersistRun<HC>* 
         if (a.first) nrm += redot(x, x);
         else p[r] = Pg[i];
         if constexpr (MODE == 1) {
-          iw[r] = (int32_t)(i / a.K.dimup);
-          iu[r] = (int32_t)(i - (int64_t)iw[r] * a.K.dimup);
+          const uint32_t w_ = (uint32_t)(i / a.K.dimup);
+          rix[r] = (w_ << 16) | (uint32_t)(i - (int64_t)w_ * a.K.dimup);
         }
       }
     }
@@ -155,6 +155,10 @@ __global__ void __launch_bounds__(kPBlock) k_lanc_persist(const PersistRun<HC>* 
     __syncthreads();
   }
   if (st->done && !a.first) return;
+  const double thresh = st->thresh;   // hoisted: a global read per iteration costs ~1 µs
+  double* const alpha_out = a.alpha;
+  double* const beta_out = a.beta;
+  V* const basis = (V*)a.basis;
 
   for (int k = 0; k < a.niter; k++) {
     const int it = it0 + k;
@@ -187,23 +191,23 @@ __global__ void __launch_bounds__(kPBlock) k_lanc_persist(const PersistRun<HC>* 
               if (k0 + kk < wd) acc = add(acc, mul(h[kk], vl[c[kk]]));
           }
         } else {
-          const int64_t du = a.K.dimup, dd = a.K.dimdw;
-          auto d = add(add(aup[iu[r]], adw[iw[r]]),
-                       mk<HC>(uimp[impu[iu[r]] * a.K.nimp + impd[iw[r]]], 0.0));
+          const int du = (int)a.K.dimup, dd = (int)a.K.dimdw;
+          const int iwr = (int)(rix[r] >> 16), iur = (int)(rix[r] & 0xffffu);
+          auto d = add(add(aup[iur], adw[iwr]), mk<HC>(uimp[impu[iur] * a.K.nimp + impd[iwr]], 0.0));
           acc = mul(d, xi);
-          const V* xrow = vl + (int64_t)iw[r] * du;
+          const V* xrow = vl + iwr * du;
           for (int kk = 0; kk < a.K.degup; kk++) {
-            const int64_t q = (int64_t)kk * du + iu[r];
+            const int q = kk * du + iur;
             acc = add(acc, mul(upv[q], xrow[upc[q]]));
           }
           for (int kk = 0; kk < a.K.degdw; kk++) {
-            const int64_t q = (int64_t)kk * dd + iw[r];
-            acc = add(acc, mul(dwv[q], vl[(int64_t)dwc[q] * du + iu[r]]));
+            const int q = kk * dd + iwr;
+            acc = add(acc, mul(dwv[q], vl[dwc[q] * du + iur]));
           }
         }
         w[r] = sub(acc, scl(b, p[r]));
         ap += redot(xi, w[r]);
-        if (a.basis) ((V*)a.basis)[(int64_t)it * dim + i] = xi;
+        if (basis) basis[(int64_t)it * dim + i] = xi;
       }
     }
     const double alpha = pblock_sum(ap, ws);
@@ -219,10 +223,10 @@ __global__ void __launch_bounds__(kPBlock) k_lanc_persist(const PersistRun<HC>* 
     }
     const double bn = sqrt(pblock_sum(bp, ws));
     if (tid == 0) {
-      a.alpha[it] = alpha;
-      a.beta[it + 1] = bn;
+      alpha_out[it] = alpha;
+      beta_out[it + 1] = bn;
     }
-    const bool stop = bn < st->thresh;
+    const bool stop = bn < thresh;
     // ---- p <- v ; v <- w / b
     const double inv = 1.0 / bn;
 #pragma unroll

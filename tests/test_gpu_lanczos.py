@@ -33,6 +33,8 @@ def test_tridiag_and_ground_state(name, factory, sectors, persist, monkeypatch):
 
     if not persist:
         monkeypatch.setenv("ED_GPU_NO_PERSIST", "1")
+    else:
+        monkeypatch.setenv("ED_GPU_PERSIST_STORED", "1")   # cover the opt-in stored mode too
 
     cfg = factory()
     orc = Oracle(cfg)
@@ -86,6 +88,7 @@ def test_persistent_matches_multikernel(path, monkeypatch):
 
     cfg = c2()
     kw = dict(stored=True) if path == "stored" else dict(stored=False, direct=True)
+    monkeypatch.setenv("ED_GPU_PERSIST_STORED", "1")
     with Sector(cfg, 4, 4, real=True, **kw) as S:
         v0 = np.sin(np.arange(1, S.dim + 1, dtype=np.float64))
         a1, b1, n1 = S.lanc_tridiag(v0, 60)
