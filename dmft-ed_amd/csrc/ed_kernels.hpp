@@ -537,6 +537,26 @@ __global__ void __launch_bounds__(kBlock) k_kron(KronArgs<HC> K, const val_t<VC>
   epi.finish(part);
 }
 
+// ------------------------------------------------ GF seeds: c / c^+ |state>
+// One thread per source row; every target row is hit at most once (the
+// operator is injective on the Fock basis), so plain stores suffice.
+template <bool VC>
+__global__ void __launch_bounds__(kBlock) k_apply_op(const uint32_t* __restrict__ map_src,
+                                                     int64_t dim_src, DevIndex idx_dst, int op,
+                                                     int level, const val_t<VC>* __restrict__ x,
+                                                     val_t<VC>* __restrict__ y) {
+  for (int64_t m = (int64_t)blockIdx.x * kBlock + threadIdx.x; m < dim_src;
+       m += (int64_t)gridDim.x * kBlock) {
+    const uint32_t st = map_src[m];
+    const int occ = bit(st, level);
+    if ((op == 1 && occ == 0) || (op == 0 && occ == 1)) {
+      const double sg = jw_sign(st, level);
+      const uint32_t t = st ^ (1u << level);
+      y[idx_dst(t)] = scl(sg, x[m]);
+    }
+  }
+}
+
 // ------------------------------------------------------------ Lanczos misc
 // Start: R holds v0.  P <- 0; b_1 = ||R|| -> st.  (iteration 1 normalises, :96-101)
 template <bool VC>

@@ -1006,6 +1006,72 @@ int ed_sector_lanc_tridiag(ed_sector* s, int32_t vtype, const void* v0, int32_t 
   return ED_OK;
 }
 
+int ed_sector_apply_op(const ed_sector* src, const ed_sector* dst, int32_t op, int32_t level,
+                       int32_t vtype, const void* src_vec, void* dst_vec, void* stream) {
+  if (!src || !dst || !src_vec || !dst_vec) return fail(ED_ERR_ARG, "null");
+  if (src->device != dst->device) return fail(ED_ERR_ARG, "sectors on different devices");
+  if (op != 0 && op != 1) return fail(ED_ERR_ARG, "op must be 0 (c) or 1 (c^+)");
+  if (level < 0 || level >= 2 * src->Mh.ns || src->Mh.ns != dst->Mh.ns)
+    return fail(ED_ERR_ARG, "level outside the 2*Ns Fock levels / mismatched models");
+  // dst must be exactly the sector the operator maps src into (getCsector /
+  // getCDGsector, ED_SETUP.f90:464-495, 590-619, 750-768); otherwise targets
+  // would fall outside dst's index tables
+  {
+    const int ns = src->Mh.ns, d = op == 1 ? 1 : -1, up = level < ns;
+    int e1 = src->T.q1, e2 = src->T.q2;
+    if (src->Mh.mode == ED_MODE_NORMAL) {
+      if (up) e1 += d; else e2 += d;
+    } else if (src->Mh.mode == ED_MODE_SUPERC) {
+      e1 += up ? d : -d;
+    } else {
+      e1 += d;
+    }
+    if (dst->Mh.mode != src->Mh.mode || dst->T.q1 != e1 || dst->T.q2 != e2)
+      return fail(ED_ERR_ARG, "dst is not the sector reached by the operator");
+    if (vtype == 0 && (src->hc || dst->hc)) return fail(ED_ERR_ARG, "complex sectors need vtype=1");
+  }
+  HIPCK(hipSetDevice(src->device));
+  hipStream_t st = (hipStream_t)stream;
+  const size_t vs = vtype ? 16 : 8;
+  HIPCK(hipMemsetAsync(dst_vec, 0, dst->dim * vs, st));
+  DevIndex idx{dst->d_off, dst->d_rank, dst->T.ns, dst->T.nst - 1};
+  if (vtype)
+    hipLaunchKernelGGL(k_apply_op<true>, dim3(grid_for(src->dim)), dim3(kBlock), 0, st, src->d_map,
+                       src->dim, idx, op, level, (const double2*)src_vec, (double2*)dst_vec);
+  else
+    hipLaunchKernelGGL(k_apply_op<false>, dim3(grid_for(src->dim)), dim3(kBlock), 0, st, src->d_map,
+                       src->dim, idx, op, level, (const double*)src_vec, (double*)dst_vec);
+  HIPCK(hipGetLastError());
+  return ED_OK;
+}
+
+int ed_sector_lanc_tridiag_dev(ed_sector* s, int32_t vtype, const void* v0_dev, int32_t nitermax,
+                               double threshold, double* alfa, double* beta, int32_t* nlanc) {
+  if (!s || !alfa || !beta || !v0_dev || nitermax < 1) return fail(ED_ERR_ARG, "bad args");
+  HIPCK(hipSetDevice(s->device));
+  LancDriver d;
+  CK(make_driver(s, vtype, false, &d));
+  CK(lanc_prepare(s, d.vc, nitermax, false, 0));
+  HIPCK(hipDeviceSynchronize());  // v0 may come from another stream
+  CK(lanc_load_start(s, d.vc, v0_dev, true));
+  CK(d.start(threshold));
+  CK(d.iters(nitermax, true));
+  std::vector<double> a(nitermax + 1), b(nitermax + 2);
+  HIPCK(hipMemcpyAsync(a.data(), s->ws.alpha, nitermax * 8, hipMemcpyDeviceToHost, d.st));
+  HIPCK(hipMemcpyAsync(b.data(), s->ws.beta, (nitermax + 1) * 8, hipMemcpyDeviceToHost, d.st));
+  LancState hs;
+  HIPCK(hipMemcpyAsync(&hs, s->ws.st, sizeof(hs), hipMemcpyDeviceToHost, d.st));
+  HIPCK(hipStreamSynchronize(d.st));
+  int n = hs.iter;
+  for (int q = 0; q < nitermax; q++) {
+    alfa[q] = q < n ? a[q] : 0.0;
+    beta[q] = (q >= 1 && q <= n) ? b[q] : 0.0;
+  }
+  beta[0] = 0.0;
+  if (nlanc) *nlanc = n;
+  return ED_OK;
+}
+
 int ed_sector_lanc_eigh(ed_sector* s, int32_t vtype, const void* v0, int32_t nitermax,
                         double threshold, int32_t ncheck, double* egs, void* vect,
                         int32_t* nlanc) {

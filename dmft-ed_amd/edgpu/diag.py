@@ -1,0 +1,173 @@
+"""Sector loop of the impurity diagonalisation: ed_diag_c (ED_DIAG.f90:49-251).
+
+For every symmetry sector (reference isector order):
+  * Neigen / Nitermax / Nblock as ED_DIAG.f90:88-97;
+  * dim <= max(lanc_dim_threshold, MpiSize) or Neigen == dim: dense path —
+    H dumped from the device sector (sp_dump_matrix) and diagonalised with
+    LAPACK on the host, as the reference does on its master rank (:187-212);
+  * lanc_method="lanczos": device-resident plain Lanczos (sp_lanc_eigh, :173-180);
+  * lanc_method="arpack" : implicitly restarted Lanczos (ARPACK via scipy)
+    on the host with every H·v on the GPU (sp_eigh, :145-167; SURVEY §7
+    step 6: the ARPACK path stays on the host with a device H·v).
+The T=0 state list follows :217-236 (gs_threshold window, 10*gs_threshold
+reset).  Sectors can be restricted (the farm hands each rank its subset);
+`state_list` replays the list logic in isector order over gathered
+eigenvalues, so a farmed run reproduces the serial list exactly.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, Iterable, List, Optional, Tuple
+
+import numpy as np
+
+from .hamiltonian import Sector
+from .params import EDConfig
+from .sectors import Sector as SectorId
+from .sectors import setup_pointers
+
+
+@dataclass
+class DiagOptions:
+    """ED_INPUT_VARS defaults (ED_INPUT_VARS.f90:166-176, :179)."""
+
+    lanc_method: str = "arpack"
+    lanc_nstates_sector: int = 6
+    lanc_niter: int = 512
+    lanc_ncv_factor: int = 3
+    lanc_ncv_add: int = 5
+    lanc_tolerance: float = 1e-12
+    lanc_dim_threshold: int = 256
+    gs_threshold: float = 1e-9
+    mpi_size: int = 1
+    keep_vectors: bool = True
+
+
+@dataclass
+class SectorResult:
+    isector: int
+    q: Tuple[int, int]
+    dim: int
+    eigenvalues: np.ndarray          # the Neigen lowest (or all, dense)
+    neigen: int
+    vectors: Optional[np.ndarray] = None   # (dim, Neigen) host copy, if kept
+    method: str = ""
+
+
+@dataclass
+class StateList:
+    """state_list at T=0: energies, sectors and (optionally) vectors."""
+
+    energies: List[float] = field(default_factory=list)
+    sectors: List[int] = field(default_factory=list)
+    vectors: List[Optional[np.ndarray]] = field(default_factory=list)
+
+    @property
+    def emin(self) -> float:
+        return min(self.energies)
+
+    @property
+    def size(self) -> int:
+        return len(self.energies)
+
+
+def lanczos_params(dim: int, opt: DiagOptions) -> Tuple[int, int, int]:
+    """(Neigen, Nitermax, Nblock), ED_DIAG.f90:88-97 (neigen_sector from
+    setup_pointers: min(dim, lanc_nstates_sector))."""
+    neigen_sector = min(dim, opt.lanc_nstates_sector)
+    if opt.lanc_method == "lanczos":
+        return 1, min(dim, opt.lanc_niter), 1
+    neigen = min(dim, neigen_sector)
+    nitermax = min(dim, opt.lanc_niter)
+    nblock = min(dim, opt.lanc_ncv_factor * max(neigen, opt.lanc_nstates_sector) + opt.lanc_ncv_add)
+    return neigen, nitermax, nblock
+
+
+def _start_vector(dim: int, cplx: bool) -> np.ndarray:
+    i = np.arange(1, dim + 1, dtype=np.float64)
+    return (np.sin(i) + 1j * np.cos(3.0 * i)) if cplx else np.sin(i)
+
+
+def solve_sector(cfg: EDConfig, sec: SectorId, opt: DiagOptions, device: int = 0) -> SectorResult:
+    dim = sec.dim
+    neigen, nitermax, nblock = lanczos_params(dim, opt)
+    lanc_solve = not (neigen == dim or dim <= max(opt.lanc_dim_threshold, opt.mpi_size))
+    real = cfg.is_real()
+    q = (sec.q1, sec.q2)
+    if not lanc_solve:
+        with Sector(cfg, sec.q1, sec.q2, stored=True, real=real, device=device) as S:
+            rp, cols, vals = S.dump_csr()
+        H = np.zeros((dim, dim), dtype=np.complex128)
+        rows = np.repeat(np.arange(dim), np.diff(rp))
+        np.add.at(H, (rows, cols), vals)
+        if real:
+            H = H.real
+        w, v = np.linalg.eigh(H)
+        vec = v[:, :neigen] if opt.keep_vectors else None
+        return SectorResult(sec.isector, q, dim, w, neigen, vec, "dense")
+    with Sector(cfg, sec.q1, sec.q2, stored=True, real=real, device=device) as S:
+        if opt.lanc_method == "lanczos":
+            e0, vec, _ = S.lanc_eigh(nitermax=nitermax, threshold=opt.lanc_tolerance,
+                                     v0=_start_vector(dim, not real), vector=opt.keep_vectors)
+            vecs = vec[:, None] if vec is not None else None
+            return SectorResult(sec.isector, q, dim, np.array([e0]), 1, vecs, "lanczos")
+        import scipy.sparse.linalg as sla
+
+        dt = np.float64 if real else np.complex128
+        if real:
+            import torch
+
+            xd = torch.empty(dim, dtype=torch.float64, device=f"cuda:{device}")
+            yd = torch.empty_like(xd)
+
+            def mv(x):
+                xd.copy_(torch.from_numpy(np.ascontiguousarray(x, dtype=np.float64).ravel()))
+                S.hxv_dev(xd, yd)
+                return yd.cpu().numpy()
+        else:
+            def mv(x):
+                return S.hxv(np.asarray(x, dtype=np.complex128).ravel())
+        op = sla.LinearOperator((dim, dim), matvec=mv, dtype=dt)
+        w, v = sla.eigsh(op, k=neigen, which="SA", ncv=max(nblock, neigen + 1),
+                         maxiter=max(nitermax, 10) * dim, tol=opt.lanc_tolerance,
+                         v0=_start_vector(dim, not real).astype(dt))
+        order = np.argsort(w)
+        w, v = w[order], v[:, order]
+        return SectorResult(sec.isector, q, dim, w, neigen, v if opt.keep_vectors else None, "arpack")
+
+
+def state_list(results: Iterable[SectorResult], opt: DiagOptions) -> StateList:
+    """T=0 state list, ED_DIAG.f90:224-235, replayed in isector order."""
+    sl = StateList()
+    oldzero = 1000.0
+    for r in sorted(results, key=lambda r: r.isector):
+        for i in range(r.neigen):
+            enemin = float(r.eigenvalues[i])
+            vec = r.vectors[:, i] if r.vectors is not None else None
+            if enemin < oldzero - 10.0 * opt.gs_threshold:
+                oldzero = enemin
+                sl = StateList()
+                sl.energies.append(enemin); sl.sectors.append(r.isector); sl.vectors.append(vec)
+            elif abs(enemin - oldzero) <= opt.gs_threshold:
+                oldzero = min(oldzero, enemin)
+                sl.energies.append(enemin); sl.sectors.append(r.isector); sl.vectors.append(vec)
+    return sl
+
+
+def ed_diag(cfg: EDConfig, opt: Optional[DiagOptions] = None,
+            sectors: Optional[Iterable[int]] = None, device: int = 0):
+    """Diagonalise all (or the given) sectors; returns (results, state_list)."""
+    opt = opt or DiagOptions()
+    secs = setup_pointers(cfg)
+    pick = set(sectors) if sectors is not None else None
+    results: List[SectorResult] = []
+    for sec in secs:
+        if pick is not None and sec.isector not in pick:
+            continue
+        results.append(solve_sector(cfg, sec, opt, device))
+    return results, state_list(results, opt)
+
+
+def eigenvalues_table(results: Iterable[SectorResult]) -> Dict[int, np.ndarray]:
+    """eigenvalues_list.ed content (ED_DIAG.f90:238-242): Neigen per sector."""
+    return {r.isector: np.asarray(r.eigenvalues[: r.neigen]) for r in results}

@@ -1,0 +1,137 @@
+"""Sector / seed farm over ranks: one process per GPU, torch.distributed.
+
+The reference loops over sectors on every rank and splits each sector's rows
+across MPI ranks, with an MPI_Allgatherv of the whole vector on every H·v
+(ED_HAMILTONIAN_STORED_HxV.f90:147-197).  Sectors are independent
+(ED_DIAG.f90:71-249), so here whole sectors go to ranks instead:
+
+  * longest-processing-time partition by an H·v cost model (dim x elements/row);
+  * each rank diagonalises its sectors on its own GPU — no collective in the
+    data path;
+  * one all_gather of the per-sector eigenvalues (KB), after which every rank
+    replays the T=0 state-list logic in isector order, so the result is
+    identical to the serial loop;
+  * ground-state vectors stay on their owner rank; `broadcast_vector` ships one
+    to every rank (RCCL broadcast over xGMI, 16*dim bytes) for the
+    Green's-function seed farm.
+
+The collective backend is whatever process group is initialised (nccl = RCCL
+on the GPU box, gloo in the CPU tests).
+"""
+from __future__ import annotations
+
+from typing import Callable, Dict, List, Optional, Sequence
+
+import numpy as np
+
+from .diag import DiagOptions, SectorResult, StateList, lanczos_params, state_list
+from .params import EDConfig
+from .sectors import Sector as SectorId
+from .sectors import setup_pointers
+
+
+def _dist():
+    try:
+        import torch.distributed as dist
+
+        if dist.is_available() and dist.is_initialized():
+            return dist
+    except Exception:
+        pass
+    return None
+
+
+def sector_cost(cfg: EDConfig, sec: SectorId, opt: DiagOptions) -> float:
+    """Work model: dense sectors ~ dim^3 (LAPACK), Lanczos sectors ~
+    Nitermax x dim x (1 + elements per row); elements/row ~ 1 + 2*Norb*Nbath
+    hops (normal bath) — only the ranking matters for LPT."""
+    neigen, nitermax, _ = lanczos_params(sec.dim, opt)
+    if neigen == sec.dim or sec.dim <= max(opt.lanc_dim_threshold, opt.mpi_size):
+        return float(sec.dim) ** 3 / 1e3
+    per_row = 1.0 + cfg.Norb * cfg.Nbath
+    return float(nitermax) * sec.dim * per_row
+
+
+def lpt_partition(costs: Sequence[float], nranks: int) -> List[List[int]]:
+    """Longest processing time first: items (indices) to the least-loaded rank."""
+    order = sorted(range(len(costs)), key=lambda i: (-costs[i], i))
+    loads = [0.0] * nranks
+    parts: List[List[int]] = [[] for _ in range(nranks)]
+    for i in order:
+        r = min(range(nranks), key=lambda k: (loads[k], k))
+        parts[r].append(i)
+        loads[r] += costs[i]
+    return [sorted(p) for p in parts]
+
+
+class FarmResult:
+    def __init__(self, states: StateList, owners: List[int], tables: Dict[int, np.ndarray],
+                 local: Dict[int, SectorResult], assignment: List[List[int]]):
+        self.states = states          # vectors present only for states owned by this rank
+        self.owners = owners          # rank owning each state's vector
+        self.eigenvalues = tables     # isector -> Neigen eigenvalues (all ranks)
+        self.local = local            # isector -> SectorResult solved here
+        self.assignment = assignment  # rank -> isectors
+
+
+def farm_diag(cfg: EDConfig, opt: Optional[DiagOptions] = None, *, device: int = 0,
+              sectors: Optional[Sequence[int]] = None,
+              solver: Optional[Callable[[EDConfig, SectorId, DiagOptions, int], SectorResult]] = None
+              ) -> FarmResult:
+    """ed_diag over all ranks of the default process group (or serially)."""
+    from .diag import solve_sector
+
+    opt = opt or DiagOptions()
+    solver = solver or solve_sector
+    dist = _dist()
+    rank = dist.get_rank() if dist else 0
+    world = dist.get_world_size() if dist else 1
+    secs = [s for s in setup_pointers(cfg) if sectors is None or s.isector in set(sectors)]
+    parts = lpt_partition([sector_cost(cfg, s, opt) for s in secs], world)
+    assignment = [[secs[i].isector for i in p] for p in parts]
+    local: Dict[int, SectorResult] = {}
+    for i in parts[rank]:
+        r = solver(cfg, secs[i], opt, device)
+        local[r.isector] = r
+    # gather eigenvalues (tiny) from every rank
+    mine = {k: (v.q, v.dim, v.neigen, np.asarray(v.eigenvalues[: max(v.neigen, 1)])) for k, v in local.items()}
+    if dist:
+        allt: List[Optional[dict]] = [None] * world
+        dist.all_gather_object(allt, mine)
+    else:
+        allt = [mine]
+    merged: Dict[int, tuple] = {}
+    owner_of: Dict[int, int] = {}
+    for rk, t in enumerate(allt):
+        for k, v in t.items():
+            merged[k] = v
+            owner_of[k] = rk
+    shadows = []
+    for k, (q, dim, neigen, ev) in merged.items():
+        loc = local.get(k)
+        shadows.append(SectorResult(k, q, dim, ev, neigen, loc.vectors if loc is not None else None))
+    states = state_list(shadows, opt)
+    owners = [owner_of[s] for s in states.sectors]
+    tables = {k: v[3] for k, v in merged.items()}
+    return FarmResult(states, owners, tables, local, assignment)
+
+
+def broadcast_vector(vec: Optional[np.ndarray], owner: int, dim: int, cplx: bool,
+                     device: Optional[int] = None) -> np.ndarray:
+    """Ship one eigenvector from its owner to every rank (RCCL broadcast on GPU
+    tensors when the backend is nccl; host tensors for gloo)."""
+    dist = _dist()
+    if dist is None:
+        return vec
+    import torch
+
+    dt = torch.complex128 if cplx else torch.float64
+    on_gpu = dist.get_backend() == "nccl"
+    dev = torch.device("cuda", device if device is not None else torch.cuda.current_device()) if on_gpu \
+        else torch.device("cpu")
+    if dist.get_rank() == owner:
+        t = torch.from_numpy(np.ascontiguousarray(vec).astype(np.complex128 if cplx else np.float64)).to(dev)
+    else:
+        t = torch.empty(dim, dtype=dt, device=dev)
+    dist.broadcast(t, src=owner)
+    return t.cpu().numpy()

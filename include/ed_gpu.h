@@ -172,6 +172,18 @@ int ed_sector_lanc_eigh(ed_sector* s, int32_t vtype, const void* v0, int32_t nit
 int ed_sector_lanc_run(ed_sector* s, int32_t vtype, const void* v0_dev, int32_t niter,
                        double* alfa, double* beta, float* ms, void* stream);
 
+/* Green's-function seed (ED_GF_NORMAL.f90:159-174 / :216-229):
+ *   dst(j) = sg * src(m)  for every basis state m of `src` with the level
+ *   free (op = 1, c^+) or occupied (op = 0, c), |j> = op_level |m>,
+ *   sg the Jordan-Wigner sign of c / cdg (ED_SETUP.f90:1080-1106).
+ * `level` is the 0-based bit (Fortran position - 1).  dst is zeroed first.
+ * Device pointers, async on `stream`; both sectors on the same device. */
+int ed_sector_apply_op(const ed_sector* src, const ed_sector* dst, int32_t op, int32_t level,
+                       int32_t vtype, const void* src_vec, void* dst_vec, void* stream);
+/* sp_lanc_tridiag from a device start vector (not modified). */
+int ed_sector_lanc_tridiag_dev(ed_sector* s, int32_t vtype, const void* v0_dev, int32_t nitermax,
+                               double threshold, double* alfa, double* beta, int32_t* nlanc);
+
 /* ------------------------------------------------------ reference-style API */
 int ed_gpu_init(const ed_params* p);          /* ed_init_solver parameter hand-over */
 int ed_gpu_set_device(int32_t device);

@@ -1,0 +1,68 @@
+"""CPU Green's function from the oracle pieces (test infrastructure): seeds by
+the reference's vvinit loop (ED_GF_NORMAL.f90:159-174, binary search on the
+target H%map), tridiagonalisation by the oracle's lanczos_plain_tridiag_c,
+poles as add_to_lanczos_gf_normal (:580-632)."""
+import numpy as np
+
+from edgpu.gf import matsubara, realaxis, tridiag_poles
+from edgpu.sectors import c_sector, cdg_sector, setup_pointers
+from oracle.oracle import Oracle, lanc_tridiag
+
+
+def _popcount_below(states, level):
+    m = states & np.uint32((1 << level) - 1)
+    c = np.zeros_like(m, dtype=np.int64)
+    for b in range(level):
+        c += (m >> np.uint32(b)) & np.uint32(1)
+    return c
+
+
+def seed(orc, hmap_i, jsec, op, level, vec):
+    hmap_j = orc.build_sector(jsec.q1, jsec.q2)
+    occ = (hmap_i >> np.uint32(level)) & np.uint32(1)
+    sel = (occ == 0) if op == 1 else (occ == 1)
+    st = hmap_i[sel]
+    sg = 1.0 - 2.0 * (_popcount_below(st, level) % 2)
+    tgt = st ^ np.uint32(1 << level)
+    j = np.searchsorted(hmap_j, tgt)
+    assert np.all(hmap_j[j] == tgt)
+    v = np.zeros(len(hmap_j), dtype=np.complex128)
+    v[j] = sg * vec[sel]
+    return hmap_j, v
+
+
+def build_gf_normal_oracle(cfg, states, gopt):
+    orc = Oracle(cfg)
+    Ns, No, Nsp = cfg.Ns, cfg.Norb, cfg.Nspin
+    wm = matsubara(gopt.beta, gopt.Lmats)
+    wr = realaxis(gopt.wini, gopt.wfin, gopt.Lreal)
+    Gm = np.zeros((Nsp, Nsp, No, No, gopt.Lmats), dtype=np.complex128)
+    Gr = np.zeros((Nsp, Nsp, No, No, gopt.Lreal), dtype=np.complex128)
+    secs = setup_pointers(cfg)
+    zeta = float(len(states.energies))
+    rec = []
+    for ispin in range(Nsp):
+        for iorb in range(No):
+            isite = iorb + ispin * Ns
+            for e_i, isec, vec in zip(states.energies, states.sectors, states.vectors):
+                sec = secs[isec - 1]
+                hmap_i = orc.build_sector(sec.q1, sec.q2)
+                for op, isign, jsec in ((1, 1, cdg_sector(cfg, sec, ispin)), (0, -1, c_sector(cfg, sec, ispin))):
+                    if jsec is None:
+                        continue
+                    hmap_j, v = seed(orc, hmap_i, jsec, op, isite, vec)
+                    norm2 = float(np.vdot(v, v).real)
+                    if norm2 == 0.0:
+                        continue
+                    v = v / np.sqrt(norm2)
+                    csr = orc.build_csr(hmap_j)
+                    nlanc = min(len(hmap_j), gopt.lanc_nGFiter)
+                    a, b, n = lanc_tridiag(csr, v, nlanc, gopt.threshold)
+                    E, z2 = tridiag_poles(a, b, nlanc)
+                    rec.append(dict(ispin=ispin, iorb=iorb, isector=isec, op=op, norm2=norm2,
+                                    alfa=a, beta=b, nlanc=n))
+                    de = E - e_i
+                    peso = norm2 / zeta * z2
+                    Gm[ispin, ispin, iorb, iorb] += (peso[None] / ((1j * wm)[:, None] - isign * de[None])).sum(1)
+                    Gr[ispin, ispin, iorb, iorb] += (peso[None] / ((wr + 1j * gopt.eps)[:, None] - isign * de[None])).sum(1)
+    return Gm, Gr, rec

@@ -1,0 +1,85 @@
+"""Sector farm logic on CPU: LPT partition, world_size-2 gloo runs reproduce the
+serial state list exactly, vector broadcast over the process group."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from edgpu.diag import DiagOptions
+from edgpu.farm import farm_diag, lpt_partition, sector_cost
+from edgpu.params import make_config
+from edgpu.sectors import setup_pointers
+
+
+def test_lpt_partition_balances_c4():
+    cfg = make_config(Norb=2, Nbath=5)           # configs[3]: 169 sectors
+    opt = DiagOptions()
+    secs = setup_pointers(cfg)
+    costs = [sector_cost(cfg, s, opt) for s in secs]
+    for n in (1, 2, 4, 8):
+        parts = lpt_partition(costs, n)
+        assert sorted(i for p in parts for i in p) == list(range(len(secs)))
+        loads = [sum(costs[i] for i in p) for p in parts]
+        # LPT bound: max load <= mean + largest item
+        assert max(loads) <= sum(costs) / n + max(costs) + 1e-9
+        if n == 8:
+            assert max(loads) / (sum(costs) / n) < 1.05   # ~8x achievable
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q, cfg_kw, method):
+    import torch.distributed as dist
+    from oracle_solver import solve_sector_oracle
+    from edgpu.farm import broadcast_vector
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = make_config(**cfg_kw)
+    res = farm_diag(cfg, DiagOptions(lanc_method=method), solver=solve_sector_oracle)
+    gs_owner = res.owners[0]
+    v = res.states.vectors[0] if rank == gs_owner else None
+    dim = [s for s in setup_pointers(cfg) if s.isector == res.states.sectors[0]][0].dim
+    vb = broadcast_vector(v, gs_owner, dim, cplx=True)
+    q.put((rank, res.states.energies, res.states.sectors, res.owners, res.assignment,
+           float(np.linalg.norm(vb))))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("cfg_kw,method", [
+    (dict(Norb=1, Nbath=4), "arpack"),                 # configs[0]: all sectors dense
+    (dict(Norb=1, Nbath=5), "lanczos"),                # sectors > 256 through the Lanczos branch
+    (dict(Norb=1, Nbath=3, Nspin=2, ed_mode="nonsu2"), "arpack"),
+])
+def test_gloo_farm_matches_serial(cfg_kw, method):
+    from oracle_solver import solve_sector_oracle
+
+    cfg = make_config(**cfg_kw)
+    serial = farm_diag(cfg, DiagOptions(lanc_method=method), solver=solve_sector_oracle)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, cfg_kw, method)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=300) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    out.sort()
+    for rank, en, secs, owners, assignment, vnorm in out:
+        assert secs == serial.states.sectors
+        np.testing.assert_allclose(en, serial.states.energies, rtol=0, atol=1e-12)
+        assert abs(vnorm - 1.0) < 1e-10           # broadcast delivered the owner's unit vector
+    # both ranks got work and the assignment covers every sector once
+    assign = out[0][4]
+    assert all(len(a) > 0 for a in assign)
+    assert sorted(i for a in assign for i in a) == [s.isector for s in setup_pointers(cfg)]
