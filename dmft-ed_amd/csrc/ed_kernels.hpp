@@ -118,6 +118,9 @@ __device__ __forceinline__ double sum_partials(const double* partials, int n) {
 // kernel (measured 7x slower Lanczos steps on the c4 sector).
 __device__ __forceinline__ bool grid_reduce_last(double v, RedSlot slot, double* total) {
   __shared__ int amlast;
+  // every storing wave drains its (write-through) stores before the block's
+  // ticket (R1: the signalling lane signals behind a workgroup barrier)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   double s = block_sum(v);
   if (threadIdx.x == 0) {
     __hip_atomic_store(slot.partials + blockIdx.x, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -348,6 +351,80 @@ struct EpiLancA {
   }
 };
 
+// sc1 (write-through, L1-bypassing) element stores / loads for vectors handed
+// from every block to the last block of the same kernel.
+__device__ __forceinline__ void st_wt(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_wt(double2* p, double2 v) {
+  __hip_atomic_store((double*)p, v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store((double*)p + 1, v.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_wt(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double2 ld_wt(const double2* p) {
+  return make_double2(__hip_atomic_load((const double*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                      __hip_atomic_load((const double*)p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+__device__ __forceinline__ void lanc_set_beta(double tot, LancState* st, double* beta_out);
+
+// Whole Lanczos step in ONE kernel, for grids of at most kTicketMaxBlocks
+// blocks (small sectors, where launch and reduction latency dominate): part A
+// as EpiLancA but P and W stored write-through; the last block to take the
+// ticket holds alpha and runs part B (w -= alpha v, R <- w, beta = |w|) over
+// all rows itself, reading P/W with sc1 loads.  Saves one launch and one
+// grid reduction per step.
+template <bool VC>
+struct EpiLancFused {
+  using V = val_t<VC>;
+  LancState* st;
+  V* P;
+  V* W;
+  V* R;
+  V* basis;
+  int64_t dim;
+  double* alpha_out;
+  double* beta_out;
+  RedSlot slot;
+  double invb, b;
+  V* bcol;
+  __device__ __forceinline__ bool skip() const { return st->done != 0; }
+  __device__ __forceinline__ void prepare() {
+    invb = st->invb;
+    b = st->beta;
+    bcol = basis ? basis + (int64_t)st->iter * dim : nullptr;
+  }
+  __device__ __forceinline__ double row(int64_t i, V acc, V xi) {
+    V v = scl(invb, xi);
+    V h = scl(invb, acc);
+    V w = sub(h, scl(b, P[i]));
+    st_wt(P + i, v);
+    st_wt(W + i, w);
+    if (bcol) bcol[i] = v;
+    return redot(v, w);
+  }
+  __device__ __forceinline__ void finish(double part) {
+    double alpha;
+    if (!grid_reduce_last(part, slot, &alpha)) return;
+    // last block: R is no longer read by anyone (every block took its ticket
+    // after its gathers completed)
+    double np = 0.0;
+    for (int64_t i = threadIdx.x; i < dim; i += kBlock) {
+      V w = sub(ld_wt(W + i), scl(alpha, ld_wt(P + i)));
+      R[i] = w;
+      np += redot(w, w);
+    }
+    const double tot = block_sum(np);
+    if (threadIdx.x == 0) {
+      st->alpha = alpha;
+      alpha_out[st->iter] = alpha;
+      lanc_set_beta(tot, st, beta_out);
+    }
+  }
+};
+
 // Two-pass finishing kernels of one Lanczos step (one block of kBlock threads).
 __global__ void __launch_bounds__(kBlock) k_lanc_fin_a(const double* __restrict__ partials, int n,
                                                        LancState* st, double* alpha_out) {
@@ -359,6 +436,7 @@ __global__ void __launch_bounds__(kBlock) k_lanc_fin_a(const double* __restrict_
   }
 }
 __device__ __forceinline__ void lanc_set_beta(double tot, LancState* st, double* beta_out) {
+  // (defined here, declared above EpiLancFused)
   const double b = sqrt(tot);
   const int it = st->iter;
   beta_out[it + 1] = b;

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <string.h>
 
 #include <algorithm>
@@ -371,11 +372,19 @@ static int launch_hxv(ed_sector* s, int path, const void* x, Epi epi, hipStream_
 }
 
 // ------------------------------------------------------------ Lanczos
+static void drop_graph(ed_sector* s) {
+  // a captured graph bakes in buffer pointers: any workspace reallocation
+  // invalidates it
+  if (s->gexec) (void)hipGraphExecDestroy(s->gexec);
+  s->gexec = nullptr;
+}
+
 static int lanc_prepare(ed_sector* s, int vc, int cap, bool want_basis, int basis_cols) {
   LancWS& w = s->ws;
   const size_t vs = vc ? 16 : 8;
   if (w.vc != vc) {
     if (w.vc != -1) return fail(ED_ERR_STATE, "Lanczos workspace already bound to another vtype");
+    drop_graph(s);
     CK(dalloc(s, &w.R, s->dim * vs));
     CK(dalloc(s, &w.P, s->dim * vs));
     CK(dalloc(s, &w.W, s->dim * vs));
@@ -383,16 +392,18 @@ static int lanc_prepare(ed_sector* s, int vc, int cap, bool want_basis, int basi
     CK(dalloc_t(s, &w.st, 1));
     CK(dalloc_t(s, &w.partials, kMaxGrid));
     CK(dalloc_t(s, &w.counter, 4));
-    HIPCK(hipMemset(w.counter, 0, 4 * sizeof(unsigned int)));
+    HIPCK(hipMemsetAsync(w.counter, 0, 4 * sizeof(unsigned int), s->stream));  // stream-ordered: s->stream does not sync with the null stream
     w.vc = vc;
   }
   if (cap > w.cap) {
+    drop_graph(s);
     CK(dalloc_t(s, &w.alpha, cap + 2));
     CK(dalloc_t(s, &w.beta, cap + 2));
     CK(dalloc_t(s, &w.z, cap + 2));
     w.cap = cap;
   }
   if (want_basis && basis_cols > w.basis_cols) {
+    drop_graph(s);
     CK(dalloc(s, &w.basis, (size_t)basis_cols * s->dim * vs));
     w.basis_cols = basis_cols;
   }
@@ -428,6 +439,21 @@ static int lanc_iter(ed_sector* s, int path, bool basis, hipStream_t st) {
   LancWS& w = s->ws;
   const int g1 = grid_for(s->nslice * 64), g2 = grid_for(s->dim);
   const bool two1 = g1 > kTicketMaxBlocks, two2 = g2 > kTicketMaxBlocks;
+  // single-kernel step: opt-in (measured slower on c2: 13.0 vs 8.9 us/step —
+  // the last block's serial sc1 pass over all rows is latency-bound)
+  if (!two1 && getenv("ED_GPU_FUSED_STEP")) {
+    EpiLancFused<VC> f;
+    f.st = w.st;
+    f.P = (val_t<VC>*)w.P;
+    f.W = (val_t<VC>*)w.W;
+    f.R = (val_t<VC>*)w.R;
+    f.basis = basis ? (val_t<VC>*)w.basis : nullptr;
+    f.dim = s->dim;
+    f.alpha_out = w.alpha;
+    f.beta_out = w.beta;
+    f.slot = RedSlot{w.partials, w.counter};
+    return launch_hxv<VC>(s, path, w.R, f, st);
+  }
   EpiLancA<VC> e;
   e.st = w.st;
   e.P = (val_t<VC>*)w.P;
@@ -1117,6 +1143,15 @@ int ed_sector_lanc_eigh(ed_sector* s, int32_t vtype, const void* v0, int32_t nit
     if (hs.done) stop = true;
     if (have < expected && !hs.done) return fail(ED_ERR_STATE, "Lanczos iteration count mismatch");
     done_iters = have;
+  }
+  if (nl == 0) {
+    LancState hs;
+    HIPCK(hipMemcpy(&hs, s->ws.st, sizeof(hs), hipMemcpyDeviceToHost));
+    char msg[256];
+    snprintf(msg, sizeof msg,
+             "Lanczos made no step: iter=%d done=%d beta0=%g b[1]=%g a[0]=%g path=%d pm=%d keep=%d",
+             hs.iter, hs.done, hs.beta, b[1], a[0], d.path, d.pm, (int)keep);
+    return fail(ED_ERR_STATE, msg);
   }
   // Ritz value and vector of the truncated tridiagonal (nl iterations)
   std::vector<double> dg(a.begin(), a.begin() + nl), e(nl, 0.0), z((size_t)nl * nl, 0.0);

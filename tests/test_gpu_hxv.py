@@ -130,3 +130,34 @@ def test_complex_vr_stored_semantics():
         S.hxv_dev(xd, out, path=2)
         torch.cuda.synchronize()
         assert _rel(out.cpu().numpy(), ref) < 1e-13
+
+
+@pytest.mark.parametrize("pin", ["n28_norb1", "n28_norb2"])
+def test_full_size_roofline_sectors(pin):
+    """Nlevels=28 (7,7) sectors at full size (dim 11,778,624): nnz pins of the
+    reference run, size-independent properties: hermiticity <x,Hy> = <Hx,y>,
+    stored == generic matrix-free bit for bit, Kronecker to 1e-13."""
+    import json
+    import os
+
+    from edgpu.hamiltonian import Sector
+    from edgpu.params import make_config
+
+    pins = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "survey_pins.json")))
+    p = [x for x in pins["sectors"] if x["name"] == pin][0]
+    cfg = make_config(bath="random", seed=1, **p["config"])
+    with Sector(cfg, *p["sector"], stored=True, direct=True, real=True) as S:
+        assert S.dim == p["dim"] and S.nnz == p["nnz"]
+        g = torch.Generator(device="cuda:0").manual_seed(0)
+        x = torch.rand(S.dim, dtype=torch.float64, device="cuda:0", generator=g)
+        y = torch.rand(S.dim, dtype=torch.float64, device="cuda:0", generator=g)
+        hx, hy = torch.empty_like(x), torch.empty_like(x)
+        S.hxv_dev(x, hx, path=0)
+        S.hxv_dev(y, hy, path=0)
+        a, b = torch.dot(y, hx).item(), torch.dot(hy, x).item()
+        assert abs(a - b) <= 1e-12 * abs(a)
+        h1 = torch.empty_like(x)
+        S.hxv_dev(x, h1, path=1)
+        assert torch.equal(h1, hx)
+        S.hxv_dev(x, h1, path=2)
+        assert (h1 - hx).abs().max().item() <= 1e-13 * hx.abs().max().item()

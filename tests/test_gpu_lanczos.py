@@ -97,3 +97,37 @@ def test_persistent_matches_multikernel(path, monkeypatch):
     assert n1 == n2 == 60
     np.testing.assert_allclose(a1[:40], a2[:40], rtol=1e-9, atol=1e-11)
     np.testing.assert_allclose(b1[:40], b2[:40], rtol=1e-9, atol=1e-11)
+
+
+def test_fused_step_matches_two_kernel(monkeypatch):
+    """Single-kernel step (small grids) vs the two-kernel step: same recurrence."""
+    from edgpu.hamiltonian import Sector
+    from cases import c5
+
+    cfg = c5()
+    with Sector(cfg, 7, 0, stored=True) as S:
+        v0 = np.sin(np.arange(1, S.dim + 1, dtype=np.float64)) + 0j
+        monkeypatch.setenv("ED_GPU_NO_PERSIST", "1")
+        monkeypatch.setenv("ED_GPU_FUSED_STEP", "1")
+        a1, b1, n1 = S.lanc_tridiag(v0, 50)
+        monkeypatch.delenv("ED_GPU_FUSED_STEP")
+        a2, b2, n2 = S.lanc_tridiag(v0, 50)
+    np.testing.assert_allclose(a1[:30], a2[:30], rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(b1[:30], b2[:30], rtol=1e-10, atol=1e-12)
+
+
+def test_c4_half_filled_ground_state_pin():
+    """configs[3] half-filled sector at full size: nnz and E0 of the reference
+    run through the large-grid (two-pass reduction) recurrence."""
+    from edgpu.hamiltonian import Sector
+    from edgpu.params import make_config
+
+    cfg = make_config(Norb=2, Nbath=5)
+    for kw in (dict(stored=True), dict(stored=False, direct=True)):
+        with Sector(cfg, 6, 6, real=True, **kw) as S:
+            assert S.dim == 853776
+            if kw.get("stored"):
+                assert S.nnz == 10167696
+            e0, vec, n = S.lanc_eigh(nitermax=512, threshold=1e-12)
+            assert abs(e0 - (-14.70964221)) < 5e-9
+            assert abs(np.linalg.norm(vec) - 1.0) < 1e-10
