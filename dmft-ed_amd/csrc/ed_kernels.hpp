@@ -635,6 +635,30 @@ __global__ void __launch_bounds__(kBlock) k_apply_op(const uint32_t* __restrict_
   }
 }
 
+template <bool VC>
+__global__ void __launch_bounds__(kBlock) k_apply_op_acc(const uint32_t* __restrict__ map_src,
+                                                         int64_t dim_src, DevIndex idx_dst, int op,
+                                                         int level, double cr, double ci,
+                                                         const val_t<VC>* __restrict__ x,
+                                                         val_t<VC>* __restrict__ y) {
+  for (int64_t m = (int64_t)blockIdx.x * kBlock + threadIdx.x; m < dim_src;
+       m += (int64_t)gridDim.x * kBlock) {
+    const uint32_t st = map_src[m];
+    const int occ = bit(st, level);
+    if ((op == 1 && occ == 0) || (op == 0 && occ == 1)) {
+      const double sg = jw_sign(st, level);
+      const int32_t j = idx_dst(st ^ (1u << level));
+      if constexpr (VC) {
+        const double2 v = x[m];
+        const double2 t = make_double2(sg * (cr * v.x - ci * v.y), sg * (cr * v.y + ci * v.x));
+        y[j] = make_double2(y[j].x + t.x, y[j].y + t.y);
+      } else {
+        y[j] = y[j] + cr * (sg * x[m]);
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------ Lanczos misc
 // Start: R holds v0.  P <- 0; b_1 = ||R|| -> st.  (iteration 1 normalises, :96-101)
 template <bool VC>

@@ -118,6 +118,14 @@ static int dalloc(ed_sector* s, void** p, size_t n) {
   s->bytes += (int64_t)n;
   return ED_OK;
 }
+static void dfree(ed_sector* s, void** p, size_t n) {
+  if (!*p) return;
+  auto it = std::find(s->allocs.begin(), s->allocs.end(), *p);
+  if (it != s->allocs.end()) s->allocs.erase(it);
+  (void)hipFree(*p);
+  s->bytes -= (int64_t)n;
+  *p = nullptr;
+}
 template <class T>
 static int dalloc_t(ed_sector* s, T** p, size_t count) {
   return dalloc(s, (void**)p, count * sizeof(T));
@@ -383,8 +391,23 @@ static int lanc_prepare(ed_sector* s, int vc, int cap, bool want_basis, int basi
   LancWS& w = s->ws;
   const size_t vs = vc ? 16 : 8;
   if (w.vc != vc) {
-    if (w.vc != -1) return fail(ED_ERR_STATE, "Lanczos workspace already bound to another vtype");
     drop_graph(s);
+    if (w.vc != -1) {  // switching real <-> complex vectors: re-size the vector buffers
+      HIPCK(hipStreamSynchronize(s->stream));
+      const size_t ovs = w.vc ? 16 : 8;
+      dfree(s, &w.R, s->dim * ovs);
+      dfree(s, &w.P, s->dim * ovs);
+      dfree(s, &w.W, s->dim * ovs);
+      dfree(s, &w.Y, s->dim * ovs);
+      dfree(s, &w.basis, (size_t)w.basis_cols * s->dim * ovs);
+      w.basis_cols = 0;
+      CK(dalloc(s, &w.R, s->dim * vs));
+      CK(dalloc(s, &w.P, s->dim * vs));
+      CK(dalloc(s, &w.W, s->dim * vs));
+      CK(dalloc(s, &w.Y, s->dim * vs));
+      w.vc = vc;
+      goto sized;
+    }
     CK(dalloc(s, &w.R, s->dim * vs));
     CK(dalloc(s, &w.P, s->dim * vs));
     CK(dalloc(s, &w.W, s->dim * vs));
@@ -395,6 +418,7 @@ static int lanc_prepare(ed_sector* s, int vc, int cap, bool want_basis, int basi
     HIPCK(hipMemsetAsync(w.counter, 0, 4 * sizeof(unsigned int), s->stream));  // stream-ordered: s->stream does not sync with the null stream
     w.vc = vc;
   }
+sized:
   if (cap > w.cap) {
     drop_graph(s);
     CK(dalloc_t(s, &w.alpha, cap + 2));
@@ -1032,30 +1056,33 @@ int ed_sector_lanc_tridiag(ed_sector* s, int32_t vtype, const void* v0, int32_t 
   return ED_OK;
 }
 
-int ed_sector_apply_op(const ed_sector* src, const ed_sector* dst, int32_t op, int32_t level,
-                       int32_t vtype, const void* src_vec, void* dst_vec, void* stream) {
-  if (!src || !dst || !src_vec || !dst_vec) return fail(ED_ERR_ARG, "null");
+// dst must be exactly the sector the operator maps src into (getCsector /
+// getCDGsector, ED_SETUP.f90:464-495, 590-619, 750-768); otherwise targets
+// would fall outside dst's index tables
+static int check_op_target(const ed_sector* src, const ed_sector* dst, int32_t op, int32_t level) {
+  if (!src || !dst) return fail(ED_ERR_ARG, "null");
   if (src->device != dst->device) return fail(ED_ERR_ARG, "sectors on different devices");
   if (op != 0 && op != 1) return fail(ED_ERR_ARG, "op must be 0 (c) or 1 (c^+)");
   if (level < 0 || level >= 2 * src->Mh.ns || src->Mh.ns != dst->Mh.ns)
     return fail(ED_ERR_ARG, "level outside the 2*Ns Fock levels / mismatched models");
-  // dst must be exactly the sector the operator maps src into (getCsector /
-  // getCDGsector, ED_SETUP.f90:464-495, 590-619, 750-768); otherwise targets
-  // would fall outside dst's index tables
-  {
-    const int ns = src->Mh.ns, d = op == 1 ? 1 : -1, up = level < ns;
-    int e1 = src->T.q1, e2 = src->T.q2;
-    if (src->Mh.mode == ED_MODE_NORMAL) {
-      if (up) e1 += d; else e2 += d;
-    } else if (src->Mh.mode == ED_MODE_SUPERC) {
-      e1 += up ? d : -d;
-    } else {
-      e1 += d;
-    }
-    if (dst->Mh.mode != src->Mh.mode || dst->T.q1 != e1 || dst->T.q2 != e2)
-      return fail(ED_ERR_ARG, "dst is not the sector reached by the operator");
-    if (vtype == 0 && (src->hc || dst->hc)) return fail(ED_ERR_ARG, "complex sectors need vtype=1");
+  const int ns = src->Mh.ns, d = op == 1 ? 1 : -1, up = level < ns;
+  int e1 = src->T.q1, e2 = src->T.q2;
+  if (src->Mh.mode == ED_MODE_NORMAL) {
+    if (up) e1 += d; else e2 += d;
+  } else if (src->Mh.mode == ED_MODE_SUPERC) {
+    e1 += up ? d : -d;
+  } else {
+    e1 += d;
   }
+  if (dst->Mh.mode != src->Mh.mode || dst->T.q1 != e1 || dst->T.q2 != e2)
+    return fail(ED_ERR_ARG, "dst is not the sector reached by the operator");
+  return ED_OK;
+}
+
+int ed_sector_apply_op(const ed_sector* src, const ed_sector* dst, int32_t op, int32_t level,
+                       int32_t vtype, const void* src_vec, void* dst_vec, void* stream) {
+  if (!src_vec || !dst_vec) return fail(ED_ERR_ARG, "null");
+  CK(check_op_target(src, dst, op, level));
   HIPCK(hipSetDevice(src->device));
   hipStream_t st = (hipStream_t)stream;
   const size_t vs = vtype ? 16 : 8;
@@ -1067,6 +1094,27 @@ int ed_sector_apply_op(const ed_sector* src, const ed_sector* dst, int32_t op, i
   else
     hipLaunchKernelGGL(k_apply_op<false>, dim3(grid_for(src->dim)), dim3(kBlock), 0, st, src->d_map,
                        src->dim, idx, op, level, (const double*)src_vec, (double*)dst_vec);
+  HIPCK(hipGetLastError());
+  return ED_OK;
+}
+
+int ed_sector_apply_op_acc(const ed_sector* src, const ed_sector* dst, int32_t op, int32_t level,
+                           double coef_re, double coef_im, int32_t vtype, const void* src_vec,
+                           void* dst_vec, void* stream) {
+  if (!src_vec || !dst_vec) return fail(ED_ERR_ARG, "null");
+  if (!vtype && coef_im != 0.0) return fail(ED_ERR_ARG, "complex coefficient needs vtype=1");
+  CK(check_op_target(src, dst, op, level));
+  HIPCK(hipSetDevice(src->device));
+  hipStream_t st = (hipStream_t)stream;
+  DevIndex idx{dst->d_off, dst->d_rank, dst->T.ns, dst->T.nst - 1};
+  if (vtype)
+    hipLaunchKernelGGL(k_apply_op_acc<true>, dim3(grid_for(src->dim)), dim3(kBlock), 0, st,
+                       src->d_map, src->dim, idx, op, level, coef_re, coef_im,
+                       (const double2*)src_vec, (double2*)dst_vec);
+  else
+    hipLaunchKernelGGL(k_apply_op_acc<false>, dim3(grid_for(src->dim)), dim3(kBlock), 0, st,
+                       src->d_map, src->dim, idx, op, level, coef_re, coef_im,
+                       (const double*)src_vec, (double*)dst_vec);
   HIPCK(hipGetLastError());
   return ED_OK;
 }

@@ -90,19 +90,28 @@ def add_poles(G_mats, G_real, peso_bz: float, Ei: float, E: np.ndarray, z2: np.n
     G_real += (peso[None, :] / ((wr + 1j * eps)[:, None] - isign * de[None, :])).sum(1)
 
 
-def _seed(src: Sector, dst: Sector, op: int, level: int, vec: np.ndarray, real: bool):
-    """apply c (op=0) / c+ (op=1) on the device; returns (normalised seed, norm2)."""
+def _seed(src: Sector, dst: Sector, op: int, terms, vec: np.ndarray, cplx: bool):
+    """Seed sum_t coef_t * op_{level_t}|vec> on the device (first term assigned,
+    the rest accumulated, as the vvinit loops of ED_GF_NORMAL/ED_GF_NONSU2);
+    returns (normalised seed, norm2)."""
     import torch
 
+    real = not cplx
     dt = torch.float64 if real else torch.complex128
     dev = f"cuda:{src.device}"
     x = torch.from_numpy(np.ascontiguousarray(vec.astype(np.float64 if real else np.complex128))).to(dev)
     y = torch.empty(dst.dim, dtype=dt, device=dev)
     st = torch.cuda.current_stream(x.device)
-    check(_lib.load().ed_sector_apply_op(src.handle, dst.handle, op, level, 0 if real else 1,
-                                         ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(y.data_ptr()),
-                                         ctypes.c_void_p(st.cuda_stream)), "ed_sector_apply_op")
-    norm2 = float(torch.sum(y.abs() ** 2).item()) if not real else float(torch.dot(y, y).item())
+    L = _lib.load()
+    vt = 0 if real else 1
+    xp, yp, sp = ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(y.data_ptr()), ctypes.c_void_p(st.cuda_stream)
+    (lvl0, c0), rest = terms[0], terms[1:]
+    assert c0 == 1
+    check(L.ed_sector_apply_op(src.handle, dst.handle, op, lvl0, vt, xp, yp, sp), "ed_sector_apply_op")
+    for lvl, c in rest:
+        check(L.ed_sector_apply_op_acc(src.handle, dst.handle, op, lvl, float(np.real(c)), float(np.imag(c)),
+                                       vt, xp, yp, sp), "ed_sector_apply_op_acc")
+    norm2 = float(torch.sum(y.abs() ** 2).item())
     if norm2 > 0:
         y = y / np.sqrt(norm2)
     torch.cuda.synchronize(x.device)
@@ -121,43 +130,124 @@ def _tridiag_dev(S: Sector, seed, nlanc: int, real: bool, threshold: float):
     return a, b, int(n.value)
 
 
-def build_gf_normal(cfg: EDConfig, states: StateList, gopt: Optional[GFOptions] = None,
-                    device: int = 0, record: Optional[list] = None):
-    """impGmats, impGreal of shape (Nspin, Nspin, Norb, Norb, L): diagonal part."""
+def _target(cfg: EDConfig, sec, op: int, ispin: int):
+    return cdg_sector(cfg, sec, ispin) if op == 1 else c_sector(cfg, sec, ispin)
+
+
+class _SectorCache:
+    """Device sectors reused across the seeds of one GF build (the reference
+    rebuilds them per seed with build_Hv_sector / delete_Hv_sector)."""
+
+    def __init__(self, cfg, gopt, device):
+        self.cfg, self.gopt, self.device, self.d = cfg, gopt, device, {}
+
+    def get(self, sec, hamiltonian: bool) -> Sector:
+        key = (sec.q1, sec.q2, hamiltonian)
+        if key not in self.d:
+            stored = hamiltonian and self.gopt.sparse_H
+            self.d[key] = Sector(self.cfg, sec.q1, sec.q2, stored=stored, direct=not stored,
+                                 real=self.cfg.is_real(), device=self.device)
+        return self.d[key]
+
+    def close(self):
+        for S in self.d.values():
+            S.close()
+        self.d.clear()
+
+
+def _channel(cfg, states, gopt, G_m, G_r, seeds, wm, wr, device, record, tag, cache=None):
+    """One G component: for every kept state and every seed spec
+    (op, isign, spin-of-first-level, terms, weight) run one tridiagonalisation
+    and add its poles (add_to_lanczos_gf_normal / _nonsu2)."""
+    own = cache is None
+    cache = cache or _SectorCache(cfg, gopt, device)
+    secs = setup_pointers(cfg)
+    zeta = float(states.size)       # T=0: zeta_function = state_list%size (ED_DIAG.f90:411)
+    real_h = cfg.is_real()
+    for e_i, isec, vec in zip(states.energies, states.sectors, states.vectors):
+        if vec is None:
+            raise ValueError("the Green's function needs the state vectors (keep_vectors=True)")
+        sec = secs[isec - 1]
+        for op, isign, ispin, terms, weight in seeds:
+            jsec = _target(cfg, sec, op, ispin)
+            if jsec is None:
+                continue
+            cplx = (not real_h) or np.iscomplexobj(vec) or any(np.imag(c) != 0 for _, c in terms)
+            HI, HJ = cache.get(sec, False), cache.get(jsec, True)
+            seed, norm2 = _seed(HI, HJ, op, terms, vec, cplx)
+            if norm2 == 0.0:
+                continue
+            nlanc = min(HJ.dim, gopt.lanc_nGFiter)
+            a, b, n = _tridiag_dev(HJ, seed, nlanc, not cplx, gopt.threshold)
+            # the reference diagonalises all nlanc entries (unset ones stay 0)
+            E, z2 = tridiag_poles(a, b, nlanc)
+            if record is not None:
+                record.append(dict(channel=tag, isector=isec, op=op, norm2=norm2, alfa=a, beta=b, nlanc=n))
+            add_poles(G_m, G_r, weight * norm2 / zeta, e_i, E, z2, isign, wm, wr, gopt.eps)
+    if own:
+        cache.close()
+
+
+def build_gf(cfg: EDConfig, states: StateList, gopt: Optional[GFOptions] = None, device: int = 0,
+             record: Optional[list] = None):
+    """impGmats, impGreal (Nspin, Nspin, Norb, Norb, L) for ed_mode normal
+    (diagonal components, build_gf_normal) and nonsu2 (build_gf_nonsu2,
+    ED_GF_NONSU2.f90:18-333, bath_type normal/hybrid: diagonal components plus
+    the spin-off-diagonal ones from the mixed seeds and the 0.5*(G - (1+i)G_ii -
+    (1+i)G_jj) recombination)."""
     gopt = gopt or GFOptions()
+    if cfg.ed_mode == "superc":
+        raise NotImplementedError("superc Green's function (ED_GF_SUPERC) is outside this hot path")
     Ns, No, Nsp = cfg.Ns, cfg.Norb, cfg.Nspin
     wm = matsubara(gopt.beta, gopt.Lmats)
     wr = realaxis(gopt.wini, gopt.wfin, gopt.Lreal)
     Gm = np.zeros((Nsp, Nsp, No, No, gopt.Lmats), dtype=np.complex128)
     Gr = np.zeros((Nsp, Nsp, No, No, gopt.Lreal), dtype=np.complex128)
-    real = cfg.is_real()
-    secs = setup_pointers(cfg)
-    zeta = float(states.size)                 # T=0: zeta_function = state_list%size (ED_DIAG.f90:411)
+    site = lambda o, s: o + s * Ns          # impIndex(iorb,ispin), 0-based bit
+    cache = _SectorCache(cfg, gopt, device)
+    try:
+        _build(cfg, states, gopt, device, record, Gm, Gr, wm, wr, site, cache)
+    finally:
+        cache.close()
+    return Gm, Gr
+
+
+def _build(cfg, states, gopt, device, record, Gm, Gr, wm, wr, site, cache):
+    No, Nsp = cfg.Norb, cfg.Nspin
     for ispin in range(Nsp):
         for iorb in range(No):
-            isite = iorb + ispin * Ns          # impIndex(iorb,ispin), 0-based bit
-            for e_i, isec, vec in zip(states.energies, states.sectors, states.vectors):
-                if vec is None:
-                    raise ValueError("build_gf_normal needs the state vectors (keep_vectors=True)")
-                sec = secs[isec - 1]
-                with Sector(cfg, sec.q1, sec.q2, stored=False, direct=True, real=real,
-                            device=device) as HI:
-                    for op, isign, jsec in ((1, +1, cdg_sector(cfg, sec, ispin)),
-                                            (0, -1, c_sector(cfg, sec, ispin))):
-                        if jsec is None:
-                            continue
-                        with Sector(cfg, jsec.q1, jsec.q2, stored=gopt.sparse_H,
-                                    direct=not gopt.sparse_H, real=real, device=device) as HJ:
-                            seed, norm2 = _seed(HI, HJ, op, isite, vec, real)
-                            if norm2 == 0.0:
-                                continue
-                            nlanc = min(HJ.dim, gopt.lanc_nGFiter)
-                            a, b, n = _tridiag_dev(HJ, seed, nlanc, real, gopt.threshold)
-                        # the reference diagonalises all nlanc entries (unset ones stay 0)
-                        E, z2 = tridiag_poles(a, b, nlanc)
-                        if record is not None:
-                            record.append(dict(ispin=ispin, iorb=iorb, isector=isec, op=op,
-                                               norm2=norm2, alfa=a, beta=b, nlanc=n))
-                        add_poles(Gm[ispin, ispin, iorb, iorb], Gr[ispin, ispin, iorb, iorb],
-                                  norm2 / zeta, e_i, E, z2, isign, wm, wr, gopt.eps)
+            i = site(iorb, ispin)
+            seeds = [(1, +1, ispin, [(i, 1)], 1.0), (0, -1, ispin, [(i, 1)], 1.0)]
+            _channel(cfg, states, gopt, Gm[ispin, ispin, iorb, iorb], Gr[ispin, ispin, iorb, iorb],
+                     seeds, wm, wr, device, record, ("diag", ispin, iorb), cache)
+    if cfg.ed_mode == "nonsu2" and cfg.bath_type in ("normal", "hybrid"):
+        pairs = [(s1, s2, o) for s1 in range(Nsp) for s2 in range(Nsp) for o in range(No) if s1 != s2]
+        for ispin, jspin, iorb in pairs:
+            i, j = site(iorb, ispin), site(iorb, jspin)
+            seeds = [
+                (1, +1, ispin, [(i, 1), (j, 1)], 1.0),         # (c+_i + c+_j)|gs>      :571-595
+                (0, -1, ispin, [(i, 1), (j, 1)], 1.0),         # (c_i + c_j)|gs>        :654-678
+                (1, +1, ispin, [(i, 1), (j, 1j)], 1j),         # (c+_i + i c+_j)|gs>    :739-763, cnorm2=i*norm2
+                (0, -1, ispin, [(i, 1), (j, -1j)], 1j),        # (c_i - i c_j)|gs>      :823-847
+            ]
+            _channel(cfg, states, gopt, Gm[ispin, jspin, iorb, iorb], Gr[ispin, jspin, iorb, iorb],
+                     seeds, wm, wr, device, record, ("mix", ispin, jspin, iorb), cache)
+        for ispin, jspin, iorb in pairs:               # build_gf_nonsu2 :35-48
+            for G in (Gm, Gr):
+                G[ispin, jspin, iorb, iorb] = 0.5 * (G[ispin, jspin, iorb, iorb]
+                                                     - (1 + 1j) * G[ispin, ispin, iorb, iorb]
+                                                     - (1 + 1j) * G[jspin, jspin, iorb, iorb])
+
+
+def build_gf_normal(cfg: EDConfig, states: StateList, gopt: Optional[GFOptions] = None,
+                    device: int = 0, record: Optional[list] = None):
+    """build_gf_normal (ED_GF_NORMAL.f90:18-92), diagonal components."""
+    if cfg.ed_mode != "normal":
+        raise ValueError("build_gf_normal needs ed_mode='normal'")
+    rec = [] if record is not None else None
+    Gm, Gr = build_gf(cfg, states, gopt, device, rec)
+    if record is not None:
+        for r in rec:
+            _, ispin, iorb = r["channel"]
+            record.append(dict(r, ispin=ispin, iorb=iorb))
     return Gm, Gr

@@ -180,6 +180,12 @@ int ed_sector_lanc_run(ed_sector* s, int32_t vtype, const void* v0_dev, int32_t 
  * Device pointers, async on `stream`; both sectors on the same device. */
 int ed_sector_apply_op(const ed_sector* src, const ed_sector* dst, int32_t op, int32_t level,
                        int32_t vtype, const void* src_vec, void* dst_vec, void* stream);
+/* Accumulating form for the mixed nonSU2 seeds (ED_GF_NONSU2.f90:571-595,
+ * 739-763): dst(j) += (coef_re + i coef_im) * sg * src(m); dst is NOT zeroed.
+ * vtype must be 1 (complex) when coef_im != 0. */
+int ed_sector_apply_op_acc(const ed_sector* src, const ed_sector* dst, int32_t op, int32_t level,
+                           double coef_re, double coef_im, int32_t vtype, const void* src_vec,
+                           void* dst_vec, void* stream);
 /* sp_lanc_tridiag from a device start vector (not modified). */
 int ed_sector_lanc_tridiag_dev(ed_sector* s, int32_t vtype, const void* v0_dev, int32_t nitermax,
                                double threshold, double* alfa, double* beta, int32_t* nlanc);

@@ -66,3 +66,73 @@ def build_gf_normal_oracle(cfg, states, gopt):
                     Gm[ispin, ispin, iorb, iorb] += (peso[None] / ((1j * wm)[:, None] - isign * de[None])).sum(1)
                     Gr[ispin, ispin, iorb, iorb] += (peso[None] / ((wr + 1j * gopt.eps)[:, None] - isign * de[None])).sum(1)
     return Gm, Gr, rec
+
+
+def seed_combo(orc, hmap_i, jsec, op, terms, vec):
+    """sum_t coef_t op_{level_t}|vec> (ED_GF_NONSU2.f90 vvinit loops)."""
+    v = None
+    for level, coef in terms:
+        hmap_j, w = seed(orc, hmap_i, jsec, op, level, vec)
+        v = coef * w if v is None else v + coef * w
+    return hmap_j, v
+
+
+def build_gf_oracle(cfg, states, gopt):
+    """build_gf_normal / build_gf_nonsu2 (normal bath) from oracle pieces;
+    nonSU2 poles from the oracle's tql2 like add_to_lanczos_gf_nonsu2
+    (ED_GF_NONSU2.f90:936)."""
+    from oracle.oracle import tql2
+
+    orc = Oracle(cfg)
+    Ns, No, Nsp = cfg.Ns, cfg.Norb, cfg.Nspin
+    wm = matsubara(gopt.beta, gopt.Lmats)
+    wr = realaxis(gopt.wini, gopt.wfin, gopt.Lreal)
+    Gm = np.zeros((Nsp, Nsp, No, No, gopt.Lmats), dtype=np.complex128)
+    Gr = np.zeros((Nsp, Nsp, No, No, gopt.Lreal), dtype=np.complex128)
+    secs = setup_pointers(cfg)
+    zeta = float(len(states.energies))
+    site = lambda o, s: o + s * Ns
+
+    def channel(idx, specs):
+        for e_i, isec, vec in zip(states.energies, states.sectors, states.vectors):
+            sec = secs[isec - 1]
+            hmap_i = orc.build_sector(sec.q1, sec.q2)
+            for op, isign, ispin, terms, weight in specs:
+                jsec = cdg_sector(cfg, sec, ispin) if op == 1 else c_sector(cfg, sec, ispin)
+                if jsec is None:
+                    continue
+                hmap_j, v = seed_combo(orc, hmap_i, jsec, op, terms, vec.astype(np.complex128))
+                norm2 = float(np.vdot(v, v).real)
+                if norm2 == 0.0:
+                    continue
+                v = v / np.sqrt(norm2)
+                csr = orc.build_csr(hmap_j)
+                nlanc = min(len(hmap_j), gopt.lanc_nGFiter)
+                a, b, n = lanc_tridiag(csr, v, nlanc, gopt.threshold)
+                if cfg.ed_mode == "nonsu2":
+                    E, Z, ierr = tql2(a[:nlanc], np.concatenate([[0.0], b[1:nlanc]]))
+                    z2 = Z[0, :] ** 2
+                else:
+                    E, z2 = tridiag_poles(a, b, nlanc)
+                de = E - e_i
+                peso = weight * norm2 / zeta * z2
+                Gm[idx] += (peso[None] / ((1j * wm)[:, None] - isign * de[None])).sum(1)
+                Gr[idx] += (peso[None] / ((wr + 1j * gopt.eps)[:, None] - isign * de[None])).sum(1)
+
+    for ispin in range(Nsp):
+        for iorb in range(No):
+            i = site(iorb, ispin)
+            channel((ispin, ispin, iorb, iorb), [(1, 1, ispin, [(i, 1)], 1.0), (0, -1, ispin, [(i, 1)], 1.0)])
+    if cfg.ed_mode == "nonsu2":
+        pairs = [(s1, s2, o) for s1 in range(Nsp) for s2 in range(Nsp) for o in range(No) if s1 != s2]
+        for ispin, jspin, iorb in pairs:
+            i, j = site(iorb, ispin), site(iorb, jspin)
+            channel((ispin, jspin, iorb, iorb), [
+                (1, 1, ispin, [(i, 1), (j, 1)], 1.0), (0, -1, ispin, [(i, 1), (j, 1)], 1.0),
+                (1, 1, ispin, [(i, 1), (j, 1j)], 1j), (0, -1, ispin, [(i, 1), (j, -1j)], 1j)])
+        for ispin, jspin, iorb in pairs:
+            for G in (Gm, Gr):
+                G[ispin, jspin, iorb, iorb] = 0.5 * (G[ispin, jspin, iorb, iorb]
+                                                     - (1 + 1j) * G[ispin, ispin, iorb, iorb]
+                                                     - (1 + 1j) * G[jspin, jspin, iorb, iorb])
+    return Gm, Gr

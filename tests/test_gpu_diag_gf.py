@@ -59,3 +59,25 @@ def test_gf_normal_matches_oracle():
         key = (r["ispin"], r["iorb"], r["isector"])
         w[key] = w.get(key, 0.0) + r["norm2"]
     assert all(abs(v - 1.0) < 1e-12 for v in w.values())
+
+
+@pytest.mark.parametrize("cfg_kw", [
+    dict(Norb=1, Nbath=3, Nspin=2, ed_mode="nonsu2", bath="random", seed=2),   # configs[4] family
+    dict(Norb=1, Nbath=4, Nspin=2, ed_mode="nonsu2"),
+])
+def test_gf_nonsu2_matches_oracle(cfg_kw):
+    """build_gf_nonsu2: diagonal and spin-off-diagonal components (mixed seeds
+    (c+_i + c+_j), (c+_i + i c+_j), recombination) vs the oracle pipeline."""
+    from edgpu.gf import GFOptions, build_gf
+    from oracle_gf import build_gf_oracle
+
+    cfg = make_config(**cfg_kw)
+    _, sl = ed_diag(cfg, DiagOptions(lanc_method="lanczos"))
+    gopt = GFOptions(Lmats=300, Lreal=300)
+    Gm, Gr = build_gf(cfg, sl, gopt)
+    Gm0, Gr0 = build_gf_oracle(cfg, sl, gopt)
+    scale = np.max(np.abs(Gm0))
+    assert np.max(np.abs(Gm - Gm0)) / scale < 1e-10
+    assert np.max(np.abs(Gr - Gr0)) / np.max(np.abs(Gr0)) < 1e-5
+    # spin-off-diagonal components are present (ed_vsf_ratio != 0 mixes spins)
+    assert np.max(np.abs(Gm0[0, 1, 0, 0])) > 1e-6 * scale
