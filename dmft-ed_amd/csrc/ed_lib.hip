@@ -18,6 +18,7 @@
 
 #include "ed_kernels.hpp"
 #include "ed_persist.hpp"
+#include "ed_trlan.hpp"
 #include "ed_tables.hpp"
 
 using namespace edg;
@@ -748,6 +749,260 @@ static double lowest_ritz(const std::vector<double>& a, const std::vector<double
   return d[0];
 }
 
+// ------------------------------------------ thick-restart Lanczos (ARPACK)
+// Cyclic Jacobi for a small real symmetric matrix (host): A (n x n, column-
+// major) -> ascending eigenvalues w, eigenvectors Z (column-major).
+static void jacobi_eigh(int n, std::vector<double> A, std::vector<double>& w, std::vector<double>& Z) {
+  Z.assign((size_t)n * n, 0.0);
+  for (int i = 0; i < n; i++) Z[i + (size_t)n * i] = 1.0;
+  auto a = [&](int i, int j) -> double& { return A[i + (size_t)n * j]; };
+  for (int sweep = 0; sweep < 100; sweep++) {
+    double off = 0.0, tot = 0.0;
+    for (int j = 0; j < n; j++)
+      for (int i = 0; i < n; i++) {
+        tot += a(i, j) * a(i, j);
+        if (i != j) off += a(i, j) * a(i, j);
+      }
+    if (off <= 1e-30 * tot || off == 0.0) break;
+    for (int p = 0; p < n - 1; p++)
+      for (int q = p + 1; q < n; q++) {
+        const double apq = a(p, q);
+        if (apq == 0.0) continue;
+        const double theta = (a(q, q) - a(p, p)) / (2.0 * apq);
+        const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+        const double c = 1.0 / sqrt(t * t + 1.0), sn = t * c;
+        for (int k = 0; k < n; k++) {  // A <- A J
+          const double akp = a(k, p), akq = a(k, q);
+          a(k, p) = c * akp - sn * akq;
+          a(k, q) = sn * akp + c * akq;
+        }
+        for (int k = 0; k < n; k++) {  // A <- J^T A
+          const double apk = a(p, k), aqk = a(q, k);
+          a(p, k) = c * apk - sn * aqk;
+          a(q, k) = sn * apk + c * aqk;
+        }
+        for (int k = 0; k < n; k++) {
+          const double zkp = Z[k + (size_t)n * p], zkq = Z[k + (size_t)n * q];
+          Z[k + (size_t)n * p] = c * zkp - sn * zkq;
+          Z[k + (size_t)n * q] = sn * zkp + c * zkq;
+        }
+      }
+  }
+  std::vector<int> idx(n);
+  for (int i = 0; i < n; i++) idx[i] = i;
+  std::sort(idx.begin(), idx.end(), [&](int x, int y) { return a(x, x) < a(y, y); });
+  std::vector<double> Zs((size_t)n * n);
+  w.assign(n, 0.0);
+  for (int k = 0; k < n; k++) {
+    w[k] = a(idx[k], idx[k]);
+    for (int i = 0; i < n; i++) Zs[i + (size_t)n * k] = Z[i + (size_t)n * idx[k]];
+  }
+  Z.swap(Zs);
+}
+
+__global__ void k_hash_vec(double* v, int64_t n, uint64_t seed) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    uint64_t z = (uint64_t)(i + 1 + seed * 0x632BE59BD9B4E019ull) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z = z ^ (z >> 31);
+    v[i] = (double)(z >> 11) * (1.0 / 9007199254740992.0) * 2.0 - 1.0;
+  }
+}
+
+// Thick-restart Lanczos state.  All O(dim) work and the CGS2 coefficients
+// stay on the device; one expansion sweep (j0 .. m-1) is captured once per
+// start column into a hipGraph (j0 = 0 and j0 = nkeep), so a restart cycle is
+// one graph launch + one host sync for the m x m projected problem.
+template <bool VC>
+struct Trlan {
+  using V = val_t<VC>;
+  ed_sector* s = nullptr;
+  int path = 0;
+  hipStream_t st = nullptr;
+  int64_t dim = 0;
+  int G = 1, m = 0;
+  V *Vb = nullptr, *Xb = nullptr, *w = nullptr;
+  double2 *h = nullptr, *coef = nullptr, *part = nullptr;
+  double *Y = nullptr, *npart = nullptr, *alpha = nullptr, *beta = nullptr;
+  std::vector<void*> mine;
+  std::vector<std::pair<int, hipGraphExec_t>> graphs;
+  int nhv = 0;
+  ~Trlan() {
+    for (auto& g : graphs) (void)hipGraphExecDestroy(g.second);
+    for (void* p : mine) (void)hipFree(p);
+  }
+  int alloc(void** p, size_t n) {
+    HIPCK(hipMalloc(p, n));
+    mine.push_back(*p);
+    return ED_OK;
+  }
+  V* col(V* b, int c) { return b + (int64_t)c * dim; }
+  // x -= V[:, :ncol] V[:, :ncol]^H x, twice; coef = summed coefficients;
+  // with jn >= 0: alpha[jn], beta[jn] = ||x|| afterwards
+  int orth(int ncol, V* x, int jn) {
+    if (ncol == 0) {
+      hipLaunchKernelGGL(k_vaxpy<VC>, dim3(G), dim3(kBlock), 0, st, Vb, 0, h, x, dim, npart);
+    }
+    const dim3 gp(G, (ncol + kVCols - 1) / kVCols);
+    for (int pass = 0; pass < 2 && ncol > 0; pass++) {
+      hipLaunchKernelGGL(k_vdot_part<VC>, gp, dim3(kBlock), 0, st, Vb, ncol, x, dim, part);
+      hipLaunchKernelGGL(k_vdot_fin<VC>, dim3(ncol), dim3(kBlock), 0, st, part, G, h, coef, pass);
+      hipLaunchKernelGGL(k_vaxpy<VC>, dim3(G), dim3(kBlock), 0, st, Vb, ncol, h, x, dim,
+                         pass == 1 ? npart : nullptr);
+    }
+    hipLaunchKernelGGL(k_trl_coef, dim3(1), dim3(kBlock), 0, st, npart, G, coef, jn >= 0 ? jn : m,
+                       jn >= 0 ? alpha : nullptr, beta);  // beta[m]: scratch slot
+    return ED_OK;
+  }
+  // Lanczos step j: w = H V_j, CGS2, alpha_j, beta_j; V_{j+1} = w / beta_j
+  int step(int j) {
+    nhv++;
+    EpiStore<VC> e{w};
+    CK(launch_hxv<VC>(s, path, col(Vb, j), e, st));
+    CK(orth(j + 1, w, j));
+    if (j + 1 < m)
+      hipLaunchKernelGGL(k_scale_into<VC>, dim3(grid_for(dim)), dim3(kBlock), 0, st, w, col(Vb, j + 1),
+                         beta + j, dim);
+    return ED_OK;
+  }
+  int sweep(int j0) {
+    const int n = m - j0;
+    hipGraphExec_t ge = nullptr;
+    for (auto& g : graphs)
+      if (g.first == j0) ge = g.second;
+    if (!ge && n > 2) {
+      hipGraph_t g;
+      HIPCK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+      int rc = ED_OK;
+      for (int j = j0; j < m && rc == ED_OK; j++) rc = step(j);
+      hipError_t e2 = hipStreamEndCapture(st, &g);
+      if (rc != ED_OK) return rc;
+      HIPCK(e2);
+      HIPCK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+      (void)hipGraphDestroy(g);
+      graphs.emplace_back(j0, ge);
+      nhv -= n;  // capture does not run anything
+    }
+    if (ge) {
+      HIPCK(hipGraphLaunch(ge, st));
+      nhv += n;
+    } else {
+      for (int j = j0; j < m; j++) CK(step(j));
+    }
+    HIPCK(hipGetLastError());
+    return ED_OK;
+  }
+};
+
+template <bool VC>
+static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, const void* v0,
+                     double* evals, void* evecs, int32_t* nconv, int32_t* nhv) {
+  using V = val_t<VC>;
+  Trlan<VC> T;
+  T.s = s;
+  T.path = resolve_path(s, -1);
+  T.st = s->stream;
+  T.dim = s->dim;
+  T.G = (int)std::min<int64_t>(grid_for(s->dim), 512);
+  const int64_t dim = s->dim;
+  const int m = (int)std::min<int64_t>(ncv, dim);
+  T.m = m;
+  if (nev < 1 || nev >= m) return fail(ED_ERR_ARG, "need 1 <= nev < min(ncv, dim)");
+  const size_t vs = sizeof(V);
+  CK(T.alloc((void**)&T.Vb, (size_t)m * dim * vs));
+  CK(T.alloc((void**)&T.Xb, (size_t)m * dim * vs));
+  CK(T.alloc((void**)&T.w, dim * vs));
+  CK(T.alloc((void**)&T.h, 64 * sizeof(double2)));
+  CK(T.alloc((void**)&T.coef, 64 * sizeof(double2)));
+  CK(T.alloc((void**)&T.part, (size_t)64 * T.G * sizeof(double2)));
+  CK(T.alloc((void**)&T.npart, (size_t)T.G * sizeof(double)));
+  CK(T.alloc((void**)&T.alpha, 72 * sizeof(double)));
+  CK(T.alloc((void**)&T.beta, 72 * sizeof(double)));
+  CK(T.alloc((void**)&T.Y, (size_t)m * m * sizeof(double)));
+  hipStream_t st = T.st;
+  const int g = grid_for(dim);
+  const int64_t nd = dim * (VC ? 2 : 1);
+  // V_0 = v0 / |v0|
+  if (v0) HIPCK(hipMemcpyAsync(T.w, v0, dim * vs, hipMemcpyHostToDevice, st));
+  else hipLaunchKernelGGL(k_default_start, dim3(grid_for(nd)), dim3(kBlock), 0, st, (double*)T.w, nd);
+  CK(T.orth(0, T.w, -1));  // ncol 0: only the norm -> beta[m]
+  double b0 = 0.0;
+  HIPCK(hipMemcpyAsync(&b0, T.beta + m, sizeof(double), hipMemcpyDeviceToHost, st));
+  HIPCK(hipStreamSynchronize(st));
+  if (!(b0 > 0.0)) return fail(ED_ERR_ARG, "zero start vector");
+  hipLaunchKernelGGL(k_scale_into<VC>, dim3(g), dim3(kBlock), 0, st, T.w, T.Vb, T.beta + m, dim);
+
+  std::vector<double> Tm((size_t)m * m, 0.0), theta, Z, al(m), be(m);
+  auto tm = [&](int i, int j) -> double& { return Tm[i + (size_t)m * j]; };
+  int jstart = 0, conv = 0;
+  uint64_t seed = 1;
+  for (int it = 0; it < maxit; it++) {
+    int j0 = jstart;
+    for (;;) {  // expansion j0..m-1, restarted past an invariant subspace
+      CK(T.sweep(j0));
+      HIPCK(hipMemcpyAsync(al.data(), T.alpha, m * sizeof(double), hipMemcpyDeviceToHost, st));
+      HIPCK(hipMemcpyAsync(be.data(), T.beta, m * sizeof(double), hipMemcpyDeviceToHost, st));
+      HIPCK(hipStreamSynchronize(st));
+      int jb = -1;
+      for (int j = j0; j < m; j++) {
+        tm(j, j) = al[j];
+        if (j + 1 < m) tm(j, j + 1) = tm(j + 1, j) = be[j];
+        const double scale = fabs(al[j]) + (j > 0 ? fabs(tm(j - 1, j)) : 0.0) + 1e-300;
+        if (j + 1 < m && be[j] < 1e-13 * scale) {
+          jb = j;
+          break;
+        }
+      }
+      if (jb < 0) break;
+      // invariant subspace at jb: continue from a random direction orthogonal to V
+      tm(jb, jb + 1) = tm(jb + 1, jb) = 0.0;
+      hipLaunchKernelGGL(k_hash_vec, dim3(grid_for(nd)), dim3(kBlock), 0, st, (double*)T.w, nd, seed++);
+      CK(T.orth(jb + 1, T.w, -1));
+      hipLaunchKernelGGL(k_scale_into<VC>, dim3(g), dim3(kBlock), 0, st, T.w, T.col(T.Vb, jb + 1),
+                         T.beta + m, dim);
+      HIPCK(hipGetLastError());
+      j0 = jb + 1;
+      if (j0 >= m) break;
+    }
+    const double beta = be[m - 1];
+    jacobi_eigh(m, Tm, theta, Z);
+    // ARPACK-style test: |beta_m * Z(m-1,i)| <= tol * max(eps^(2/3), |theta_i|)
+    const double eps23 = 3.6e-11;
+    conv = 0;
+    for (int i = 0; i < nev; i++)
+      if (fabs(beta * Z[(m - 1) + (size_t)m * i]) <= tol * std::max(eps23, fabs(theta[i]))) conv++;
+    if (conv == nev || it == maxit - 1 || m == dim) break;
+    // thick restart: keep nkeep Ritz vectors + the residual direction
+    const int nkeep = std::max(nev, std::min(m - 2, nev + (m - nev) / 2));
+    HIPCK(hipMemcpyAsync(T.Y, Z.data(), (size_t)m * m * sizeof(double), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_rotate<VC>, dim3(std::min(g, 2048)), dim3(kBlock), (size_t)m * nkeep * sizeof(double),
+                       st, T.Vb, m, T.Y, m, nkeep, T.Xb, dim);
+    HIPCK(hipMemcpyAsync(T.Vb, T.Xb, (size_t)nkeep * dim * vs, hipMemcpyDeviceToDevice, st));
+    hipLaunchKernelGGL(k_scale_into<VC>, dim3(g), dim3(kBlock), 0, st, T.w, T.col(T.Vb, nkeep),
+                       T.beta + (m - 1), dim);
+    HIPCK(hipGetLastError());
+    std::fill(Tm.begin(), Tm.end(), 0.0);
+    for (int i = 0; i < nkeep; i++) {
+      tm(i, i) = theta[i];
+      tm(i, nkeep) = tm(nkeep, i) = beta * Z[(m - 1) + (size_t)m * i];
+    }
+    jstart = nkeep;
+  }
+  for (int i = 0; i < nev; i++) evals[i] = theta[i];
+  if (evecs) {
+    HIPCK(hipMemcpyAsync(T.Y, Z.data(), (size_t)m * m * sizeof(double), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_rotate<VC>, dim3(std::min(g, 2048)), dim3(kBlock), (size_t)m * nev * sizeof(double),
+                       st, T.Vb, m, T.Y, m, nev, T.Xb, dim);
+    HIPCK(hipGetLastError());
+    HIPCK(hipMemcpyAsync(evecs, T.Xb, (size_t)nev * dim * vs, hipMemcpyDeviceToHost, st));
+  }
+  HIPCK(hipStreamSynchronize(st));
+  if (nconv) *nconv = conv;
+  if (nhv) *nhv = T.nhv;
+  return ED_OK;
+}
+
 // ---------------------------------------------------------------- C-ABI
 extern "C" {
 
@@ -1252,6 +1507,17 @@ int ed_sector_lanc_eigh(ed_sector* s, int32_t vtype, const void* v0, int32_t nit
     HIPCK(hipStreamSynchronize(s->stream));
   }
   return ED_OK;
+}
+
+int ed_sector_eigh(ed_sector* s, int32_t vtype, int32_t nev, int32_t ncv, int32_t maxit,
+                              double tol, const void* v0, double* evals, void* evecs, int32_t* nconv,
+                              int32_t* nhv) {
+  if (!s || !evals || maxit < 1) return fail(ED_ERR_ARG, "bad args");
+  if (vtype == 0 && s->hc) return fail(ED_ERR_ARG, "complex H needs vtype=1");
+  if (ncv > 64) return fail(ED_ERR_ARG, "ncv > 64 not supported");
+  HIPCK(hipSetDevice(s->device));
+  return vtype ? trlan_run<true>(s, nev, ncv, maxit, tol, v0, evals, evecs, nconv, nhv)
+               : trlan_run<false>(s, nev, ncv, maxit, tol, v0, evals, evecs, nconv, nhv);
 }
 
 // ------------------------------------------------- reference-style globals

@@ -1,0 +1,156 @@
+// ed_trlan.hpp — kernels of the device thick-restart Lanczos (ARPACK path).
+//
+// The reference's default spectrum solver is ARPACK through SciFortran's
+// sp_eigh (ED_DIAG.f90:145-167: Neigen=min(dim,6), ncv=Nblock=23,
+// which="SR", tol=lanc_tolerance).  Here the Krylov basis V (dim x ncv,
+// column-major, column c at V + c*dim) stays in HBM and every O(dim) step is
+// a kernel; only the ncv x ncv projected matrix goes to the host.
+//   k_vdot_part   partial h_c = <V_c, w> for a block of columns (CGS2 pass)
+//   k_vdot_fin    sum of the per-block partials -> h (device)
+//   k_vaxpy       w -= sum_c V_c h_c
+//   k_rotate      X_k = sum_c V_c Y(c,k)      (restart / Ritz vectors)
+//   k_scale_into  V_{j+1} = w / beta
+// All loops are grid-strided over rows with coalesced column accesses.
+#pragma once
+#include "ed_kernels.hpp"
+
+namespace edg {
+
+constexpr int kVCols = 8;  // columns handled per pass of k_vdot_part
+
+// conj(a) * b
+__device__ __forceinline__ double2 cdotc(double2 a, double2 b) {
+  return make_double2(a.x * b.x + a.y * b.y, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ double2 cdotc(double a, double b) { return make_double2(a * b, 0.0); }
+
+// part[c * G + blockIdx.x] (re, im) = partial <V_c, w>; blockIdx.y picks the
+// column chunk [8y, 8y+8) ∩ [0, ncol).
+template <bool VC>
+__global__ void __launch_bounds__(kBlock) k_vdot_part(const val_t<VC>* __restrict__ V, int ncol,
+                                                      const val_t<VC>* __restrict__ w, int64_t dim,
+                                                      double2* __restrict__ part) {
+  const int c0 = blockIdx.y * kVCols;
+  double2 acc[kVCols];
+#pragma unroll
+  for (int c = 0; c < kVCols; c++) acc[c] = make_double2(0.0, 0.0);
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < dim; i += (int64_t)gridDim.x * kBlock) {
+    const auto wi = w[i];
+#pragma unroll
+    for (int c = 0; c < kVCols; c++)
+      if (c0 + c < ncol) {
+        const double2 t = cdotc(V[(int64_t)(c0 + c) * dim + i], wi);
+        acc[c].x += t.x;
+        acc[c].y += t.y;
+      }
+  }
+#pragma unroll
+  for (int c = 0; c < kVCols; c++) {
+    if (c0 + c >= ncol) break;  // uniform
+    double re = block_sum(acc[c].x);
+    double im = block_sum(acc[c].y);
+    if (threadIdx.x == 0) part[(int64_t)(c0 + c) * gridDim.x + blockIdx.x] = make_double2(re, im);
+  }
+}
+
+// h[c] = sum_b part[c*G + b] (imaginary part dropped for real vectors); one
+// block per column.  coef[c] = h[c] (add == 0) or coef[c] += h[c] (add == 1).
+template <bool VC>
+__global__ void __launch_bounds__(kBlock) k_vdot_fin(const double2* __restrict__ part, int G,
+                                                     double2* __restrict__ h, double2* __restrict__ coef,
+                                                     int add) {
+  const int c = blockIdx.x;
+  double re = 0.0, im = 0.0;
+  for (int b = threadIdx.x; b < G; b += kBlock) {
+    re += part[(int64_t)c * G + b].x;
+    im += part[(int64_t)c * G + b].y;
+  }
+  re = block_sum(re);
+  im = VC ? block_sum(im) : 0.0;
+  if (threadIdx.x == 0) {
+    h[c] = make_double2(re, im);
+    if (add) coef[c] = make_double2(coef[c].x + re, coef[c].y + im);
+    else coef[c] = make_double2(re, im);
+  }
+}
+
+// w -= sum_{c<ncol} V_c h_c; with npart != nullptr also the block partials of |w|^2
+template <bool VC>
+__global__ void __launch_bounds__(kBlock) k_vaxpy(const val_t<VC>* __restrict__ V, int ncol,
+                                                  const double2* __restrict__ h, val_t<VC>* __restrict__ w,
+                                                  int64_t dim, double* __restrict__ npart) {
+  __shared__ double2 hs[64];
+  for (int c = threadIdx.x; c < ncol; c += kBlock) hs[c] = h[c];
+  __syncthreads();
+  double n2 = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < dim; i += (int64_t)gridDim.x * kBlock) {
+    auto x = w[i];
+    for (int c = 0; c < ncol; c++) {
+      const auto v = V[(int64_t)c * dim + i];
+      if constexpr (VC) {
+        x.x -= v.x * hs[c].x - v.y * hs[c].y;
+        x.y -= v.x * hs[c].y + v.y * hs[c].x;
+      } else {
+        x -= v * hs[c].x;  // real vectors: coefficients are real
+      }
+    }
+    w[i] = x;
+    n2 += redot(x, x);
+  }
+  if (npart) {
+    n2 = block_sum(n2);
+    if (threadIdx.x == 0) npart[blockIdx.x] = n2;
+  }
+}
+
+// beta[j] = ||w|| from the partials; alpha[j] = Re coef[j]
+__global__ void __launch_bounds__(kBlock) k_trl_coef(const double* __restrict__ npart, int G,
+                                                     const double2* __restrict__ coef, int j,
+                                                     double* __restrict__ alpha, double* __restrict__ beta) {
+  double t = 0.0;
+  for (int b = threadIdx.x; b < G; b += kBlock) t += npart[b];
+  t = block_sum(t);
+  if (threadIdx.x == 0) {
+    beta[j] = sqrt(t);
+    if (alpha) alpha[j] = coef[j].x;
+  }
+}
+
+// X_k = sum_{c<ncol} V_c Y[c + k*ldy] for k < nout (Y real, column-major).
+// Outputs in register chunks of kVCols so V is streamed ceil(nout/8) times.
+template <bool VC>
+__global__ void __launch_bounds__(kBlock) k_rotate(const val_t<VC>* __restrict__ V, int ncol,
+                                                   const double* __restrict__ Y, int ldy, int nout,
+                                                   val_t<VC>* __restrict__ X, int64_t dim) {
+  extern __shared__ double ys[];  // ncol * nout (<= 64 * 64)
+  for (int t = threadIdx.x; t < ncol * nout; t += kBlock) ys[t] = Y[(t % ncol) + (int64_t)(t / ncol) * ldy];
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < dim; i += (int64_t)gridDim.x * kBlock) {
+    for (int k0 = 0; k0 < nout; k0 += kVCols) {
+      val_t<VC> acc[kVCols];
+#pragma unroll
+      for (int k = 0; k < kVCols; k++) acc[k] = vzero<val_t<VC>>();
+      for (int c = 0; c < ncol; c++) {
+        const auto v = V[(int64_t)c * dim + i];
+#pragma unroll
+        for (int k = 0; k < kVCols; k++)
+          if (k0 + k < nout) acc[k] = add(acc[k], scl(ys[c + (k0 + k) * ncol], v));
+      }
+#pragma unroll
+      for (int k = 0; k < kVCols; k++)
+        if (k0 + k < nout) X[(int64_t)(k0 + k) * dim + i] = acc[k];
+    }
+  }
+}
+
+// y = x * (1/nrm) with nrm read from device (0 -> zeros)
+template <bool VC>
+__global__ void __launch_bounds__(kBlock) k_scale_into(const val_t<VC>* __restrict__ x,
+                                                       val_t<VC>* __restrict__ y, const double* nrm,
+                                                       int64_t dim) {
+  const double inv = nrm[0] > 0.0 ? 1.0 / nrm[0] : 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < dim; i += (int64_t)gridDim.x * kBlock)
+    y[i] = scl(inv, x[i]);
+}
+
+}  // namespace edg

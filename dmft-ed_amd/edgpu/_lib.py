@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(_PKG_ROOT, "libedgpu.so")
@@ -31,6 +32,7 @@ SIGNATURES = {
     "ed_sector_lanc_tridiag": ([_P, _i32, _P, _i32, _f64, _P, _P, _P], ctypes.c_int),
     "ed_sector_lanc_eigh": ([_P, _i32, _P, _i32, _f64, _i32, _P, _P, _P], ctypes.c_int),
     "ed_sector_lanc_run": ([_P, _i32, _P, _i32, _P, _P, _P, _P], ctypes.c_int),
+    "ed_sector_eigh": ([_P, _i32, _i32, _i32, _i32, _f64, _P, _P, _P, _P, _P], ctypes.c_int),
     "ed_sector_sell_view": ([_P, _P], ctypes.c_int),
     "ed_sector_apply_op": ([_P, _P, _i32, _i32, _i32, _P, _P, _P], ctypes.c_int),
     "ed_sector_apply_op_acc": ([_P, _P, _i32, _i32, _f64, _f64, _i32, _P, _P, _P], ctypes.c_int),
@@ -71,6 +73,14 @@ def load():
             raise EDGPUError(
                 f"HIP library {LIB_PATH} not built: run __graft_entry__.build() "
                 "(there is deliberately no CPU fallback)")
+        # torch ships its own libamdhip64 beside the /opt/rocm one this library
+        # links; when ours takes the device first, torch's later initialisation
+        # can find no free hardware queue ("No HIP GPUs are available").  Let
+        # torch initialise first; the Fortran/C users never load torch.
+        import torch
+
+        if torch.cuda.is_available():
+            torch.cuda.init()
         lib = ctypes.CDLL(LIB_PATH)
         for name, (args, res) in SIGNATURES.items():
             fn = getattr(lib, name)

@@ -6,9 +6,9 @@ For every symmetry sector (reference isector order):
     H dumped from the device sector (sp_dump_matrix) and diagonalised with
     LAPACK on the host, as the reference does on its master rank (:187-212);
   * lanc_method="lanczos": device-resident plain Lanczos (sp_lanc_eigh, :173-180);
-  * lanc_method="arpack" : implicitly restarted Lanczos (ARPACK via scipy)
-    on the host with every H·v on the GPU (sp_eigh, :145-167; SURVEY §7
-    step 6: the ARPACK path stays on the host with a device H·v).
+  * lanc_method="arpack" : sp_eigh (:145-167) replaced by a device
+    thick-restart Lanczos (ed_sector_eigh): Krylov basis in HBM, CGS2
+    reorthogonalisation kernels, only the ncv x ncv projected matrix on host.
 The T=0 state list follows :217-236 (gs_threshold window, 10*gs_threshold
 reset).  Sectors can be restricted (the farm hands each rank its subset);
 `state_list` replays the list logic in isector order over gathered
@@ -111,28 +111,15 @@ def solve_sector(cfg: EDConfig, sec: SectorId, opt: DiagOptions, device: int = 0
                                      v0=_start_vector(dim, not real), vector=opt.keep_vectors)
             vecs = vec[:, None] if vec is not None else None
             return SectorResult(sec.isector, q, dim, np.array([e0]), 1, vecs, "lanczos")
-        import scipy.sparse.linalg as sla
-
-        dt = np.float64 if real else np.complex128
-        if real:
-            import torch
-
-            xd = torch.empty(dim, dtype=torch.float64, device=f"cuda:{device}")
-            yd = torch.empty_like(xd)
-
-            def mv(x):
-                xd.copy_(torch.from_numpy(np.ascontiguousarray(x, dtype=np.float64).ravel()))
-                S.hxv_dev(xd, yd)
-                return yd.cpu().numpy()
-        else:
-            def mv(x):
-                return S.hxv(np.asarray(x, dtype=np.complex128).ravel())
-        op = sla.LinearOperator((dim, dim), matvec=mv, dtype=dt)
-        w, v = sla.eigsh(op, k=neigen, which="SA", ncv=max(nblock, neigen + 1),
-                         maxiter=max(nitermax, 10) * dim, tol=opt.lanc_tolerance,
-                         v0=_start_vector(dim, not real).astype(dt))
+        if neigen >= dim:
+            raise ValueError("arpack path needs Neigen < dim")
+        ncv = min(max(nblock, neigen + 1), 64, dim)   # device basis limit (ed_gpu.h)
+        w, v, _, _ = S.eigh(neigen=neigen, ncv=ncv, maxit=max(nitermax, 10),
+                            tol=opt.lanc_tolerance, v0=_start_vector(dim, not real),
+                            vectors=opt.keep_vectors)
         order = np.argsort(w)
-        w, v = w[order], v[:, order]
+        w = w[order]
+        v = v[:, order] if v is not None else None
         return SectorResult(sec.isector, q, dim, w, neigen, v if opt.keep_vectors else None, "arpack")
 
 

@@ -169,6 +169,23 @@ class Sector:
               "lanc_run")
         return a, b, float(ms.value)
 
+    def eigh(self, neigen: int = 6, ncv: int = 23, maxit: int = 512, tol: float = 1e-12,
+             v0: Optional[np.ndarray] = None, vectors: bool = True, real: Optional[bool] = None):
+        """sp_eigh (ARPACK, which="SR") replacement: thick-restart Lanczos with
+        the Krylov basis in HBM.  Returns (eigenvalues, vectors (dim, neigen) or
+        None, nconv, number of H·v products)."""
+        vt, buf = self._vec_arg(v0, real)
+        ev = np.zeros(neigen)
+        out = None
+        if vectors:
+            out = np.zeros((neigen, self.dim), dtype=np.complex128 if vt else np.float64)
+        nconv = ctypes.c_int32()
+        nhv = ctypes.c_int32()
+        check(_lib.load().ed_sector_eigh(self._h, vt, neigen, ncv, maxit, tol, buf, _ptr(ev),
+                                         None if out is None else _ptr(out), ctypes.byref(nconv),
+                                         ctypes.byref(nhv)), "ed_sector_eigh")
+        return ev, (out.T if out is not None else None), int(nconv.value), int(nhv.value)
+
     def _vec_arg(self, v0, real):
         use_real = self.real if real is None else real
         vt = 0 if use_real else 1

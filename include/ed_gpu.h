@@ -166,6 +166,15 @@ int ed_sector_lanc_tridiag(ed_sector* s, int32_t vtype, const void* v0, int32_t 
 int ed_sector_lanc_eigh(ed_sector* s, int32_t vtype, const void* v0, int32_t nitermax,
                         double threshold, int32_t ncheck, double* egs, void* vect,
                         int32_t* nlanc);
+/* Lowest `nev` eigenpairs by thick-restart Lanczos with full (CGS2)
+ * reorthogonalisation, Krylov basis of `ncv` vectors resident in HBM: the
+ * device replacement of SciFortran's ARPACK sp_eigh (ED_DIAG.f90:145-167,
+ * which="SR", Nblock=ncv, Nitermax=maxit restarts, tol as ARPACK:
+ * |r_i| <= tol*max(eps^(2/3),|theta_i|)).  v0: host start vector or NULL.
+ * evals[nev] ascending; evecs (host, dim x nev column-major, vtype) or NULL.
+ * nconv: converged pairs; nhv: H·v products used.  ncv <= 64. */
+int ed_sector_eigh(ed_sector* s, int32_t vtype, int32_t nev, int32_t ncv, int32_t maxit, double tol,
+                   const void* v0, double* evals, void* evecs, int32_t* nconv, int32_t* nhv);
 /* Fixed-length Lanczos on device pointers for benchmarking: runs exactly
  * `niter` iterations (no convergence test) from device vector v0 and writes
  * alfa/beta (host).  Returns the elapsed device time in ms in *ms (or NULL). */
