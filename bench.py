@@ -87,6 +87,71 @@ def cpu_baseline(budget_s=10.0):
                       f"c2 (4,4) sector, random bath) in {dt:.1f}s on 1 core"}
 
 
+def _timed(dist, fn):
+    """Barrier-bracketed wall time of fn(), max over ranks."""
+    import torch.distributed as tdist
+
+    def barrier():
+        if dist:
+            tdist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    r = fn()
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt, r
+
+
+def bench_farm(dist, world, dev):
+    """configs[3]: all 169 (Nup,Ndw) sectors of Norb=2 Nbath=5 (Nlevels=24) through
+    ed_diag's default path (dense <= 256, device thick-restart Lanczos for the 6
+    lowest otherwise), sectors farmed over the ranks (LPT), one all_gather of
+    eigenvalues.  Strong scaling: the same job on 1/2/4/8 GPUs."""
+    from edgpu.diag import DiagOptions
+    from edgpu.farm import farm_diag
+    from edgpu.params import make_config
+
+    cfg = make_config(Norb=2, Nbath=5, bath="random", seed=20251015)
+    opt = DiagOptions()
+    farm_diag(cfg, opt, device=dev)        # warm-up (code objects, allocator)
+    dt, res = _timed(dist, lambda: farm_diag(cfg, opt, device=dev))
+    nloc = len(res.local)
+    return {"wall_s": round(dt, 4), "sectors": len(res.eigenvalues), "n_gpus": world,
+            "E0": round(float(res.states.emin), 10), "gs_states": res.states.size,
+            "rank0_sectors": nloc, "scaling": "strong",
+            "workload": "configs[3]: Norb=2 Nbath=5 random bath, all sectors, lanc_method=arpack "
+                        "(Neigen=6, ncv=23) on device"}
+
+
+def bench_nonsu2(dist, world, dev):
+    """configs[4]: nonSU2 Norb=1 Nbath=6 (Nlevels=14): complex ground state over
+    all sectors + the Green's function (diagonal + spin-mixed seeds, 200-step
+    Lanczos each, Lmats=Lreal=5000), seeds farmed over the ranks."""
+    from edgpu.diag import DiagOptions
+    from edgpu.farm import farm_diag
+    from edgpu.gf import GFOptions, _job_list, build_gf
+    from edgpu.params import make_config
+
+    cfg = make_config(Norb=1, Nbath=6, Nspin=2, ed_mode="nonsu2", bath="random", seed=20251015)
+    opt = DiagOptions()
+    gopt = GFOptions()
+    res = farm_diag(cfg, opt, device=dev)
+    build_gf(cfg, res.states, gopt, device=dev, owners=res.owners)   # warm-up
+    t_diag, res = _timed(dist, lambda: farm_diag(cfg, opt, device=dev))
+    t_gf, (Gm, _) = _timed(dist, lambda: build_gf(cfg, res.states, gopt, device=dev, owners=res.owners))
+    return {"diag_s": round(t_diag, 4), "gf_s": round(t_gf, 4), "n_gpus": world,
+            "gf_seeds": len(_job_list(cfg, res.states)[0]), "E0": round(float(res.states.emin), 10),
+            "G_iw0_00": [round(float(Gm[0, 0, 0, 0, 0].real), 10), round(float(Gm[0, 0, 0, 0, 0].imag), 10)],
+            "workload": "configs[4]: nonSU2 Norb=1 Nbath=6 random bath, default (arpack) GS over all sectors "
+                        "+ build_gf (diag + mixed seeds, nGFiter=200, L=5000)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -153,6 +218,9 @@ def main():
     direct_ips = args.niter / (min(dms) * 1e-3)
     Sd.close()
 
+    farm = bench_farm(dist, world, dev)
+    nonsu2 = bench_nonsu2(dist, world, dev)
+
     out = None
     if rank == 0:
         # SpMV GB/s on the headline sector (L2-resident; launch-latency bound)
@@ -192,6 +260,8 @@ def main():
             "direct_note": "configs[2]: same sector, matrix-free H·v (Kronecker form, tables in LDS), one GPU",
             "spmv_gbs_c2": round(gbs2, 1),
             "spmv_ms_c2": round(ms2, 5),
+            "farm_c4": farm,
+            "nonsu2_c5": nonsu2,
             "roofline": roof,
             "cpu_baseline": cpu,
         }

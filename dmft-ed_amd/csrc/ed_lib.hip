@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <mutex>
 #include <string>
+#include <map>
 #include <vector>
 
 #include "ed_kernels.hpp"
@@ -101,6 +102,12 @@ struct ed_sector {
   std::vector<void*> allocs;
   // persistent one-workgroup Lanczos (small sectors)
   void* d_prun = nullptr;   // PersistRun<HC> in device memory
+  // register-resident stored matrix for the persistent kernel (MODE 2)
+  int preg_E = 0;           // 0 not built, -1 ineligible, else ELL row width W
+  int preg_rpt = 0;         // rows per thread (template value)
+  uint32_t* d_pk = nullptr;
+  void* d_dict = nullptr;
+  int ndict = 0;
   // graph cache for Lanczos iterations
   hipGraphExec_t gexec = nullptr;
   int g_path = -2, g_vc = -1, g_chunk = 0;
@@ -535,9 +542,73 @@ static int lanc_iters(ed_sector* s, int path, bool basis, int n, hipStream_t st)
 // ---------------------------------------------- persistent small-sector path
 static constexpr int64_t kLdsBudget = 150 * 1024;
 
-// Returns the persistent mode (0 stored, 1 Kronecker) or -1 when the sector
-// does not fit one workgroup's LDS / register budget.
-static int persist_mode(const ed_sector* s, int vc, int path) {
+// MODE 2 packing (ELL in registers): row i = t + r*kPRegBlock of thread t
+// keeps W words {col:17 | dictionary byte offset:14}, W = the smallest of
+// 8/12/14/16 >= the longest row, padded with entry (col 0, dict[0] = 0.0).
+// The dictionary holds the distinct values by bit pattern: exact.
+static int build_preg(ed_sector* s) {
+  if (s->preg_E) return s->preg_E;
+  s->preg_E = -1;
+  const int64_t dim = s->dim, ns = s->nslice, slots = s->padded;
+  if (!(s->flags & ED_STORED) || dim > 10 * (int64_t)kPRegBlock) return -1;
+  const int hw = s->hc ? 2 : 1;
+  std::vector<uint16_t> cnt(dim);
+  std::vector<int64_t> sptr(ns + 1);
+  std::vector<int32_t> sc(slots);
+  std::vector<double> sv(slots * hw);
+  HIPCK(hipStreamSynchronize(s->stream));  // SELL arrays come from kernels on s->stream
+  HIPCK(hipMemcpy(cnt.data(), s->d_cnt, dim * 2, hipMemcpyDeviceToHost));
+  HIPCK(hipMemcpy(sptr.data(), s->d_sptr, (ns + 1) * 8, hipMemcpyDeviceToHost));
+  HIPCK(hipMemcpy(sc.data(), s->d_cols, slots * 4, hipMemcpyDeviceToHost));
+  HIPCK(hipMemcpy(sv.data(), s->d_vals, slots * 8 * hw, hipMemcpyDeviceToHost));
+  int wmax = 0;
+  for (int64_t i = 0; i < dim; i++) wmax = std::max<int>(wmax, cnt[i]);
+  int W = 0;
+  for (int w : {8, 12, 14, 16})
+    if (!W && wmax <= w) W = w;
+  if (!W) return -1;
+  const int64_t rpt = (dim + kPRegBlock - 1) / kPRegBlock;
+  const int RPT = rpt <= 2 ? 2 : rpt <= 4 ? 4 : rpt <= 6 ? 6 : rpt <= 8 ? 8 : 10;
+  const uint32_t hs = s->hc ? 16 : 8;
+  std::map<std::pair<uint64_t, uint64_t>, uint32_t> idx;
+  std::vector<double> dict(hw, 0.0);
+  idx[{0, 0}] = 0;
+  std::vector<uint32_t> pk((size_t)RPT * W * kPRegBlock, 0u);
+  for (int64_t i = 0; i < dim; i++) {
+    const int t = (int)(i % kPRegBlock), r = (int)(i / kPRegBlock);
+    const int64_t base = sptr[i >> 6] + (i & 63);
+    for (int k = 0; k < cnt[i]; k++) {
+      const int64_t q = base + 64 * (int64_t)k;
+      uint64_t x0 = 0, x1 = 0;
+      memcpy(&x0, &sv[hw * q], 8);
+      if (hw == 2) memcpy(&x1, &sv[2 * q + 1], 8);
+      auto it = idx.find({x0, x1});
+      uint32_t id;
+      if (it == idx.end()) {
+        id = (uint32_t)idx.size();
+        if ((id + 1) * hs > kPkOffMask + 1) return -1;
+        idx[{x0, x1}] = id;
+        for (int c = 0; c < hw; c++) dict.push_back(sv[hw * q + c]);
+      } else {
+        id = it->second;
+      }
+      pk[((size_t)r * W + k) * kPRegBlock + t] = (uint32_t)sc[q] | ((id * hs) << kPkColBits);
+    }
+  }
+  CK(dalloc(s, (void**)&s->d_pk, pk.size() * 4));
+  CK(dalloc(s, &s->d_dict, dict.size() * 8));
+  HIPCK(hipMemcpy(s->d_pk, pk.data(), pk.size() * 4, hipMemcpyHostToDevice));
+  HIPCK(hipMemcpy(s->d_dict, dict.data(), dict.size() * 8, hipMemcpyHostToDevice));
+  s->ndict = (int)(dict.size() / hw);
+  s->preg_E = W;
+  s->preg_rpt = RPT;
+  return W;
+}
+
+// Returns the persistent mode (0 stored, 1 Kronecker, 2 stored in registers)
+// or -1 when the sector does not fit one workgroup's LDS / register budget.
+static int64_t persist_lds(const ed_sector* s, int vc, int mode);
+static int persist_mode(ed_sector* s, int vc, int path) {
   if (getenv("ED_GPU_NO_PERSIST")) return -1;
   const int64_t vs = vc ? 16 : 8;
   // rows per thread beyond which the register-resident p/w arrays spill
@@ -545,10 +616,24 @@ static int persist_mode(const ed_sector* s, int vc, int path) {
   const int64_t rpt_max = (vc || s->hc) ? 5 : 8;
   if (s->dim > rpt_max * (int64_t)kPBlock) return -1;
   int64_t lds = ((s->dim * vs + 15) & ~(int64_t)15);
-  // stored mode streams the matrix from L2 through one CU (~40-50 GB/s): the
-  // graph-captured multi-kernel recurrence is faster there (measured c2: 9.8 vs
-  // 8.9 us/step), so it is opt-in
-  if (path == 0) return (getenv("ED_GPU_PERSIST_STORED") && lds <= kLdsBudget) ? 0 : -1;
+  // stored: MODE 2 (ELL entries in registers; c2 4.6 us/step) by default.
+  // MODE 0 streams the matrix from L2 through one CU (~40-50 GB/s) and is
+  // slower than the graph-captured multi-kernel recurrence (c2: 9.8 vs 8.9
+  // us/step): opt-in only (ED_GPU_PERSIST_STORED), for coverage
+  if (path == 0) {
+    if (getenv("ED_GPU_PERSIST_STORED")) return lds <= kLdsBudget ? 0 : -1;
+    if (getenv("ED_GPU_NO_PREG")) return -1;
+    // MODE 2: dictionary + v + diagonal in LDS; RPT x W words + RPT x (p, w)
+    // in registers (512-thread blocks: 256 VGPRs per lane)
+    if (s->dim > 10 * (int64_t)kPRegBlock) return -1;
+    const int W = build_preg(s);
+    if (W < 0) return -1;
+    // entries per lane that compile without scratch (-Rpass-analysis=kernel-resource-usage)
+    const int cap = vc ? (s->hc ? 72 : 84) : 120;
+    if (s->preg_rpt * W > cap) return -1;
+    if (persist_lds(s, vc, 2) > kLdsBudget) return -1;
+    return 2;
+  }
   if (path == 2) {
     const KronHost& K = s->K;
     const int64_t hs = s->hc ? 16 : 8;
@@ -562,6 +647,10 @@ static int persist_mode(const ed_sector* s, int vc, int path) {
 static int64_t persist_lds(const ed_sector* s, int vc, int mode) {
   const int64_t vs = vc ? 16 : 8;
   int64_t lds = ((s->dim * vs + 15) & ~(int64_t)15);
+  if (mode == 2) {
+    const int64_t hs = s->hc ? 16 : 8;
+    return lds + ((s->dim * hs + 15) & ~(int64_t)15) + (((int64_t)s->ndict * hs + 15) & ~(int64_t)15);
+  }
   if (mode == 1) {
     const KronHost& K = s->K;
     const int64_t hs = s->hc ? 16 : 8;
@@ -573,17 +662,37 @@ static int64_t persist_lds(const ed_sector* s, int vc, int mode) {
   return lds;
 }
 
-template <bool HC, bool VC, int MODE, int RPT>
+template <bool HC, bool VC, int MODE, int RPT, int E = 1>
 static int persist_launch_t(ed_sector* s, int64_t lds, hipStream_t st) {
-  auto fn = k_lanc_persist<HC, VC, MODE, RPT>;
+  constexpr int NT = MODE == 2 ? kPRegBlock : kPBlock;
+  auto fn = k_lanc_persist<HC, VC, MODE, RPT, E, NT>;
   HIPCK(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(fn, dim3(1), dim3(kPBlock), (size_t)lds, st, (const PersistRun<HC>*)s->d_prun);
+  hipLaunchKernelGGL(fn, dim3(1), dim3(NT), (size_t)lds, st, (const PersistRun<HC>*)s->d_prun);
   HIPCK(hipGetLastError());
   return ED_OK;
 }
 
+template <bool HC, bool VC, int W>
+static int persist_launch_e(ed_sector* s, int64_t lds, hipStream_t st) {
+  switch (s->preg_rpt) {
+    case 2: return persist_launch_t<HC, VC, 2, 2, W>(s, lds, st);
+    case 4: return persist_launch_t<HC, VC, 2, 4, W>(s, lds, st);
+    case 6: return persist_launch_t<HC, VC, 2, 6, W>(s, lds, st);
+    case 8: return persist_launch_t<HC, VC, 2, 8, W>(s, lds, st);
+    default: return persist_launch_t<HC, VC, 2, 10, W>(s, lds, st);
+  }
+}
+
 template <bool HC, bool VC, int MODE>
 static int persist_launch_m(ed_sector* s, int64_t lds, hipStream_t st) {
+  if constexpr (MODE == 2) {
+    switch (s->preg_E) {
+      case 8: return persist_launch_e<HC, VC, 8>(s, lds, st);
+      case 12: return persist_launch_e<HC, VC, 12>(s, lds, st);
+      case 14: return persist_launch_e<HC, VC, 14>(s, lds, st);
+      default: return persist_launch_e<HC, VC, 16>(s, lds, st);
+    }
+  } else {
   const int64_t rpt = (s->dim + kPBlock - 1) / kPBlock;  // rows per thread, exact
   switch (rpt) {
     case 1: return persist_launch_t<HC, VC, MODE, 1>(s, lds, st);
@@ -596,6 +705,7 @@ static int persist_launch_m(ed_sector* s, int64_t lds, hipStream_t st) {
     case 9: case 10: return persist_launch_t<HC, VC, MODE, 10>(s, lds, st);
     case 11: case 12: return persist_launch_t<HC, VC, MODE, 12>(s, lds, st);
     default: return persist_launch_t<HC, VC, MODE, 16>(s, lds, st);
+  }
   }
 }
 
@@ -621,6 +731,9 @@ static int persist_iters(ed_sector* s, int mode, bool basis, int niter, int firs
     r.basis = basis ? w.basis : nullptr;
     r.niter = niter;
     r.first = first;
+    r.pk = s->d_pk;
+    r.dict = (const HT*)s->d_dict;
+    r.ndict = s->ndict;
   };
   const int64_t lds = persist_lds(s, VC, mode);
   if (s->hc) {
@@ -631,7 +744,9 @@ static int persist_iters(ed_sector* s, int mode, bool basis, int niter, int firs
       if (mode == 1) r.K = kron_args<true>(s);
       HIPCK(hipMemcpyAsync(s->d_prun, &r, sizeof(r), hipMemcpyHostToDevice, st));
       HIPCK(hipStreamSynchronize(st));  // r is a stack temporary
-      return mode == 0 ? persist_launch_m<true, true, 0>(s, lds, st) : persist_launch_m<true, true, 1>(s, lds, st);
+      return mode == 0 ? persist_launch_m<true, true, 0>(s, lds, st)
+             : mode == 1 ? persist_launch_m<true, true, 1>(s, lds, st)
+                         : persist_launch_m<true, true, 2>(s, lds, st);
     }
   }
   PersistRun<false> r;
@@ -639,7 +754,9 @@ static int persist_iters(ed_sector* s, int mode, bool basis, int niter, int firs
   if (mode == 1) r.K = kron_args<false>(s);
   HIPCK(hipMemcpyAsync(s->d_prun, &r, sizeof(r), hipMemcpyHostToDevice, st));
   HIPCK(hipStreamSynchronize(st));  // r is a stack temporary
-  return mode == 0 ? persist_launch_m<false, VC, 0>(s, lds, st) : persist_launch_m<false, VC, 1>(s, lds, st);
+  return mode == 0 ? persist_launch_m<false, VC, 0>(s, lds, st)
+         : mode == 1 ? persist_launch_m<false, VC, 1>(s, lds, st)
+                     : persist_launch_m<false, VC, 2>(s, lds, st);
 }
 
 static int persist_set_thresh(ed_sector* s, double thresh, hipStream_t st) {
@@ -1507,6 +1624,15 @@ int ed_sector_lanc_eigh(ed_sector* s, int32_t vtype, const void* v0, int32_t nit
     HIPCK(hipStreamSynchronize(s->stream));
   }
   return ED_OK;
+}
+
+int ed_sector_lanc_mode(ed_sector* s, int32_t vtype, int32_t path) {
+  if (!s) {
+    fail(ED_ERR_ARG, "null");
+    return -2;
+  }
+  if (hipSetDevice(s->device) != hipSuccess) return -2;
+  return persist_mode(s, vtype ? 1 : 0, resolve_path(s, path));
 }
 
 int ed_sector_eigh(ed_sector* s, int32_t vtype, int32_t nev, int32_t ncv, int32_t maxit,

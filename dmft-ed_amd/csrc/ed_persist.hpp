@@ -10,8 +10,14 @@
 //     by the H·v; p = v_{k-1} and w live in registers of the thread that owns
 //     the row (row i = tid + r*1024, r < RPT);
 //   * H is the stored SELL-64 matrix streamed from L2 (MODE 0, same element
-//     order as k_spmv -> same H·v bits) or the Kronecker tables copied into
-//     LDS (MODE 1, normal mode without Jx/Jp);
+//     order as k_spmv -> same H·v bits), the Kronecker tables copied into
+//     LDS (MODE 1, normal mode without Jx/Jp), or the stored matrix held in
+//     REGISTERS (MODE 2, ELL layout): row i = tid + r*NT keeps its W
+//     off-diagonal entries as 32-bit words {col:17 | value byte offset:14}
+//     into a dictionary of the distinct values (hoppings/exchange: a few
+//     dozen), padded with the dictionary's 0.0; diagonal, dictionary and v in
+//     LDS.  No matrix byte leaves the CU after the first iteration and the
+//     entry loop has no branch, so every gather of a row is in flight at once;
 //   * alpha and beta are block reductions (wave shuffles + 16-entry LDS),
 //     three barriers per iteration, no global synchronisation.
 // Independent runs (GF seeds, sector replicas) use one workgroup each
@@ -23,6 +29,7 @@ namespace edg {
 
 constexpr int kPBlock = 1024;
 constexpr int kPChunk = 8;
+constexpr int kPRegBlock = 512;  // MODE 2 block: 256-VGPR lanes hold the packed matrix
 
 template <bool HC>
 struct PersistRun {
@@ -41,10 +48,15 @@ struct PersistRun {
   double* alpha;     // [niter_total]
   double* beta;      // [niter_total+1]
   void* basis;       // optional Krylov basis (column k = v_k), or null
+  // register-resident stored matrix (MODE 2)
+  const uint32_t* pk;   // [RPT*W][kPRegBlock] packed entries
+  const H* dict;        // [ndict] distinct values, dict[0] = 0
+  int ndict;
   int niter;         // iterations in this launch
   int first;         // 1: R holds the unnormalised start vector
 };
 
+template <int NT = kPBlock>
 __device__ __forceinline__ double pblock_sum(double v, double* ws) {
   v = wave_sum(v);
   const int wv = threadIdx.x >> 6;
@@ -52,19 +64,22 @@ __device__ __forceinline__ double pblock_sum(double v, double* ws) {
   __syncthreads();
   double t = 0.0;
 #pragma unroll
-  for (int w = 0; w < kPBlock / 64; w++) t = t + ws[w];
+  for (int w = 0; w < NT / 64; w++) t = t + ws[w];
   __syncthreads();
   return t;
 }
 
-template <bool HC, bool VC, int MODE, int RPT>
-__global__ void __launch_bounds__(kPBlock) k_lanc_persist(const PersistRun<HC>* __restrict__ runs) {
+constexpr uint32_t kPkColBits = 17, kPkColMask = (1u << kPkColBits) - 1;
+constexpr uint32_t kPkOffMask = (1u << 14) - 1;  // dictionary byte offset (<= 16 KiB)
+
+template <bool HC, bool VC, int MODE, int RPT, int E = 1, int NT = kPBlock>
+__global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC>* __restrict__ runs) {
   using V = val_t<VC>;
   using H = val_t<HC>;
   const PersistRun<HC>& a = runs[blockIdx.x];  // uniform: scalar loads, no VGPR copy
   extern __shared__ __align__(16) unsigned char smem[];
-  __shared__ double ws[kPBlock / 64];
-  V* vl = (V*)smem;
+  __shared__ double ws[NT / 64];
+  V* vl = (V*)smem;  // MODE 2 moves it behind the dictionary
   const int64_t dim = a.dim;
   const int tid = threadIdx.x;
   V* Rg = (V*)a.R;
@@ -98,13 +113,30 @@ __global__ void __launch_bounds__(kPBlock) k_lanc_persist(const PersistRun<HC>* 
     uint8_t* s_impu = (uint8_t*)carve(K.dimup);
     uint8_t* s_impd = (uint8_t*)carve(K.dimdw);
     double* s_uimp = (double*)carve((int64_t)K.nimp * K.nimp * 8);
-    for (int64_t t = tid; t < K.dimup; t += kPBlock) { s_aup[t] = K.aup[t]; s_impu[t] = K.impu[t]; }
-    for (int64_t t = tid; t < K.dimdw; t += kPBlock) { s_adw[t] = K.adw[t]; s_impd[t] = K.impd[t]; }
-    for (int64_t t = tid; t < (int64_t)K.degup * K.dimup; t += kPBlock) { s_upv[t] = K.upv[t]; s_upc[t] = K.upc[t]; }
-    for (int64_t t = tid; t < (int64_t)K.degdw * K.dimdw; t += kPBlock) { s_dwv[t] = K.dwv[t]; s_dwc[t] = K.dwc[t]; }
-    for (int t = tid; t < K.nimp * K.nimp; t += kPBlock) s_uimp[t] = K.uimp[t];
+    for (int64_t t = tid; t < K.dimup; t += NT) { s_aup[t] = K.aup[t]; s_impu[t] = K.impu[t]; }
+    for (int64_t t = tid; t < K.dimdw; t += NT) { s_adw[t] = K.adw[t]; s_impd[t] = K.impd[t]; }
+    for (int64_t t = tid; t < (int64_t)K.degup * K.dimup; t += NT) { s_upv[t] = K.upv[t]; s_upc[t] = K.upc[t]; }
+    for (int64_t t = tid; t < (int64_t)K.degdw * K.dimdw; t += NT) { s_dwv[t] = K.dwv[t]; s_dwc[t] = K.dwc[t]; }
+    for (int t = tid; t < K.nimp * K.nimp; t += NT) s_uimp[t] = K.uimp[t];
     aup = s_aup; adw = s_adw; upv = s_upv; dwv = s_dwv; upc = s_upc; dwc = s_dwc;
     impu = s_impu; impd = s_impd; uimp = s_uimp;
+  }
+
+  // --- MODE 2: dictionary | v | diagonal in LDS, ELL entries in registers.
+  // (E is the row width W; the dictionary comes first so that its byte
+  // offsets fit 14 bits; vl moves behind it)
+  uint32_t pk[MODE == 2 ? RPT * E : 1];
+  const H* dg = nullptr;
+  const unsigned char* dct = smem;
+  if constexpr (MODE == 2) {
+    const int64_t dbytes = ((int64_t)a.ndict * sizeof(H) + 15) & ~(int64_t)15;
+    for (int t = tid; t < a.ndict; t += NT) ((H*)smem)[t] = a.dict[t];
+    vl = (V*)(smem + dbytes);
+    H* s_g = (H*)(smem + dbytes + ((dim * sizeof(V) + 15) & ~(int64_t)15));
+    for (int64_t t = tid; t < dim; t += NT) s_g[t] = a.diag[t];
+    dg = s_g;
+#pragma unroll
+    for (int k = 0; k < RPT * E; k++) pk[k] = a.pk[k * NT + tid];
   }
 
   // --- state in
@@ -116,7 +148,7 @@ __global__ void __launch_bounds__(kPBlock) k_lanc_persist(const PersistRun<HC>* 
     double nrm = 0.0;
 #pragma unroll
     for (int r = 0; r < RPT; r++) {
-      const int64_t i = tid + (int64_t)r * kPBlock;
+      const int64_t i = tid + (int64_t)r * NT;
       p[r] = vzero<V>();
       if (i < dim) {
         V x = Rg[i];
@@ -130,7 +162,7 @@ __global__ void __launch_bounds__(kPBlock) k_lanc_persist(const PersistRun<HC>* 
       }
     }
     if (a.first) {
-      double n2 = pblock_sum(nrm, ws);  // includes barrier: vl complete
+      double n2 = pblock_sum<NT>(nrm, ws);  // includes barrier: vl complete
       if (n2 == 0.0) {                  // lanczos_plain_iteration: "norm =0!!"
         if (tid == 0) { st->iter = 0; st->done = 1; st->beta = 0.0; }
         return;
@@ -138,7 +170,7 @@ __global__ void __launch_bounds__(kPBlock) k_lanc_persist(const PersistRun<HC>* 
       const double inv = 1.0 / sqrt(n2);
 #pragma unroll
       for (int r = 0; r < RPT; r++) {
-        const int64_t i = tid + (int64_t)r * kPBlock;
+        const int64_t i = tid + (int64_t)r * NT;
         if (i < dim) vl[i] = scl(inv, vl[i]);
       }
       b = 0.0;
@@ -162,12 +194,18 @@ __global__ void __launch_bounds__(kPBlock) k_lanc_persist(const PersistRun<HC>* 
 
   for (int k = 0; k < a.niter; k++) {
     const int it = it0 + k;
+    if constexpr (MODE == 2) {
+      // entries are loop-invariant: keep the compiler from hoisting their
+      // decoded addresses out of the iteration loop (2 VGPRs per entry)
+#pragma unroll
+      for (int e = 0; e < RPT * E; e++) asm volatile("" : "+v"(pk[e]));
+    }
     // ---- w = H v - b p ; alpha partial
     V w[RPT];
     double ap = 0.0;
 #pragma unroll
     for (int r = 0; r < RPT; r++) {
-      const int64_t i = tid + (int64_t)r * kPBlock;
+      const int64_t i = tid + (int64_t)r * NT;
       w[r] = vzero<V>();
       if (i < dim) {
         const V xi = vl[i];
@@ -190,6 +228,14 @@ __global__ void __launch_bounds__(kPBlock) k_lanc_persist(const PersistRun<HC>* 
             for (int kk = 0; kk < kPChunk; kk++)
               if (k0 + kk < wd) acc = add(acc, mul(h[kk], vl[c[kk]]));
           }
+        } else if constexpr (MODE == 2) {
+          acc = mul(dg[i], xi);
+#pragma unroll
+          for (int e = 0; e < E; e++) {
+            const uint32_t x = pk[r * E + e];
+            const H h = *(const H*)(dct + ((x >> kPkColBits) & kPkOffMask));
+            acc = add(acc, mul(h, vl[x & kPkColMask]));
+          }
         } else {
           const int du = (int)a.K.dimup, dd = (int)a.K.dimdw;
           const int iwr = (int)(rix[r] >> 16), iur = (int)(rix[r] & 0xffffu);
@@ -210,18 +256,18 @@ __global__ void __launch_bounds__(kPBlock) k_lanc_persist(const PersistRun<HC>* 
         if (basis) basis[(int64_t)it * dim + i] = xi;
       }
     }
-    const double alpha = pblock_sum(ap, ws);
+    const double alpha = pblock_sum<NT>(ap, ws);
     // ---- w -= alpha v ; beta
     double bp = 0.0;
 #pragma unroll
     for (int r = 0; r < RPT; r++) {
-      const int64_t i = tid + (int64_t)r * kPBlock;
+      const int64_t i = tid + (int64_t)r * NT;
       if (i < dim) {
         w[r] = sub(w[r], scl(alpha, vl[i]));
         bp += redot(w[r], w[r]);
       }
     }
-    const double bn = sqrt(pblock_sum(bp, ws));
+    const double bn = sqrt(pblock_sum<NT>(bp, ws));
     if (tid == 0) {
       alpha_out[it] = alpha;
       beta_out[it + 1] = bn;
@@ -231,7 +277,7 @@ __global__ void __launch_bounds__(kPBlock) k_lanc_persist(const PersistRun<HC>* 
     const double inv = 1.0 / bn;
 #pragma unroll
     for (int r = 0; r < RPT; r++) {
-      const int64_t i = tid + (int64_t)r * kPBlock;
+      const int64_t i = tid + (int64_t)r * NT;
       if (i < dim) {
         p[r] = vl[i];
         vl[i] = scl(inv, w[r]);
@@ -251,7 +297,7 @@ __global__ void __launch_bounds__(kPBlock) k_lanc_persist(const PersistRun<HC>* 
   // ---- state out
 #pragma unroll
   for (int r = 0; r < RPT; r++) {
-    const int64_t i = tid + (int64_t)r * kPBlock;
+    const int64_t i = tid + (int64_t)r * NT;
     if (i < dim) {
       Rg[i] = vl[i];
       Pg[i] = p[r];

@@ -155,88 +155,147 @@ class _SectorCache:
         self.d.clear()
 
 
-def _channel(cfg, states, gopt, G_m, G_r, seeds, wm, wr, device, record, tag, cache=None):
-    """One G component: for every kept state and every seed spec
-    (op, isign, spin-of-first-level, terms, weight) run one tridiagonalisation
-    and add its poles (add_to_lanczos_gf_normal / _nonsu2)."""
-    own = cache is None
-    cache = cache or _SectorCache(cfg, gopt, device)
-    secs = setup_pointers(cfg)
-    zeta = float(states.size)       # T=0: zeta_function = state_list%size (ED_DIAG.f90:411)
-    real_h = cfg.is_real()
-    for e_i, isec, vec in zip(states.energies, states.sectors, states.vectors):
-        if vec is None:
-            raise ValueError("the Green's function needs the state vectors (keep_vectors=True)")
-        sec = secs[isec - 1]
-        for op, isign, ispin, terms, weight in seeds:
-            jsec = _target(cfg, sec, op, ispin)
-            if jsec is None:
-                continue
-            cplx = (not real_h) or np.iscomplexobj(vec) or any(np.imag(c) != 0 for _, c in terms)
-            HI, HJ = cache.get(sec, False), cache.get(jsec, True)
-            seed, norm2 = _seed(HI, HJ, op, terms, vec, cplx)
-            if norm2 == 0.0:
-                continue
-            nlanc = min(HJ.dim, gopt.lanc_nGFiter)
-            a, b, n = _tridiag_dev(HJ, seed, nlanc, not cplx, gopt.threshold)
-            # the reference diagonalises all nlanc entries (unset ones stay 0)
-            E, z2 = tridiag_poles(a, b, nlanc)
-            if record is not None:
-                record.append(dict(channel=tag, isector=isec, op=op, norm2=norm2, alfa=a, beta=b, nlanc=n))
-            add_poles(G_m, G_r, weight * norm2 / zeta, e_i, E, z2, isign, wm, wr, gopt.eps)
-    if own:
-        cache.close()
-
-
-def build_gf(cfg: EDConfig, states: StateList, gopt: Optional[GFOptions] = None, device: int = 0,
-             record: Optional[list] = None):
-    """impGmats, impGreal (Nspin, Nspin, Norb, Norb, L) for ed_mode normal
-    (diagonal components, build_gf_normal) and nonsu2 (build_gf_nonsu2,
-    ED_GF_NONSU2.f90:18-333, bath_type normal/hybrid: diagonal components plus
-    the spin-off-diagonal ones from the mixed seeds and the 0.5*(G - (1+i)G_ii -
-    (1+i)G_jj) recombination)."""
-    gopt = gopt or GFOptions()
-    if cfg.ed_mode == "superc":
-        raise NotImplementedError("superc Green's function (ED_GF_SUPERC) is outside this hot path")
+def _job_list(cfg: EDConfig, states: StateList):
+    """Every (component, kept state, seed spec) of build_gf in the serial
+    accumulation order: diagonal components (ispin, iorb), then for nonSU2 the
+    mixed seeds (ispin != jspin, iorb).  A seed spec is (op, isign, spin of the
+    first level, [(level, coef)], weight)."""
     Ns, No, Nsp = cfg.Ns, cfg.Norb, cfg.Nspin
-    wm = matsubara(gopt.beta, gopt.Lmats)
-    wr = realaxis(gopt.wini, gopt.wfin, gopt.Lreal)
-    Gm = np.zeros((Nsp, Nsp, No, No, gopt.Lmats), dtype=np.complex128)
-    Gr = np.zeros((Nsp, Nsp, No, No, gopt.Lreal), dtype=np.complex128)
     site = lambda o, s: o + s * Ns          # impIndex(iorb,ispin), 0-based bit
-    cache = _SectorCache(cfg, gopt, device)
-    try:
-        _build(cfg, states, gopt, device, record, Gm, Gr, wm, wr, site, cache)
-    finally:
-        cache.close()
-    return Gm, Gr
-
-
-def _build(cfg, states, gopt, device, record, Gm, Gr, wm, wr, site, cache):
-    No, Nsp = cfg.Norb, cfg.Nspin
+    chans = []
     for ispin in range(Nsp):
         for iorb in range(No):
             i = site(iorb, ispin)
-            seeds = [(1, +1, ispin, [(i, 1)], 1.0), (0, -1, ispin, [(i, 1)], 1.0)]
-            _channel(cfg, states, gopt, Gm[ispin, ispin, iorb, iorb], Gr[ispin, ispin, iorb, iorb],
-                     seeds, wm, wr, device, record, ("diag", ispin, iorb), cache)
+            chans.append(((ispin, ispin, iorb), ("diag", ispin, iorb),
+                          [(1, +1, ispin, [(i, 1)], 1.0), (0, -1, ispin, [(i, 1)], 1.0)]))
+    pairs = []
     if cfg.ed_mode == "nonsu2" and cfg.bath_type in ("normal", "hybrid"):
         pairs = [(s1, s2, o) for s1 in range(Nsp) for s2 in range(Nsp) for o in range(No) if s1 != s2]
         for ispin, jspin, iorb in pairs:
             i, j = site(iorb, ispin), site(iorb, jspin)
-            seeds = [
+            chans.append(((ispin, jspin, iorb), ("mix", ispin, jspin, iorb), [
                 (1, +1, ispin, [(i, 1), (j, 1)], 1.0),         # (c+_i + c+_j)|gs>      :571-595
                 (0, -1, ispin, [(i, 1), (j, 1)], 1.0),         # (c_i + c_j)|gs>        :654-678
                 (1, +1, ispin, [(i, 1), (j, 1j)], 1j),         # (c+_i + i c+_j)|gs>    :739-763, cnorm2=i*norm2
                 (0, -1, ispin, [(i, 1), (j, -1j)], 1j),        # (c_i - i c_j)|gs>      :823-847
-            ]
-            _channel(cfg, states, gopt, Gm[ispin, jspin, iorb, iorb], Gr[ispin, jspin, iorb, iorb],
-                     seeds, wm, wr, device, record, ("mix", ispin, jspin, iorb), cache)
-        for ispin, jspin, iorb in pairs:               # build_gf_nonsu2 :35-48
-            for G in (Gm, Gr):
-                G[ispin, jspin, iorb, iorb] = 0.5 * (G[ispin, jspin, iorb, iorb]
-                                                     - (1 + 1j) * G[ispin, ispin, iorb, iorb]
-                                                     - (1 + 1j) * G[jspin, jspin, iorb, iorb])
+            ]))
+    secs = setup_pointers(cfg)
+    jobs = []
+    for comp, tag, seeds in chans:
+        for k, isec in enumerate(states.sectors):
+            sec = secs[isec - 1]
+            for spec in seeds:
+                jsec = _target(cfg, sec, spec[0], spec[2])
+                if jsec is not None:
+                    jobs.append((comp, tag, k, spec, sec, jsec))
+    return jobs, pairs
+
+
+def _run_job(cfg, states, gopt, job, cache, wm, wr, G_m, G_r, record, zeta):
+    """One tridiagonalisation + pole sum (add_to_lanczos_gf_normal / _nonsu2)."""
+    comp, tag, k, (op, isign, ispin, terms, weight), sec, jsec = job
+    e_i, vec = states.energies[k], states.vectors[k]
+    if vec is None:
+        raise ValueError("the Green's function needs the state vectors (keep_vectors=True)")
+    cplx = (not cfg.is_real()) or np.iscomplexobj(vec) or any(np.imag(c) != 0 for _, c in terms)
+    HI, HJ = cache.get(sec, False), cache.get(jsec, True)
+    seed, norm2 = _seed(HI, HJ, op, terms, vec, cplx)
+    if norm2 == 0.0:
+        return
+    nlanc = min(HJ.dim, gopt.lanc_nGFiter)
+    a, b, n = _tridiag_dev(HJ, seed, nlanc, not cplx, gopt.threshold)
+    # the reference diagonalises all nlanc entries (unset ones stay 0)
+    E, z2 = tridiag_poles(a, b, nlanc)
+    if record is not None:
+        record.append(dict(channel=tag, isector=states.sectors[k], op=op, norm2=norm2, alfa=a, beta=b,
+                           nlanc=n))
+    add_poles(G_m, G_r, weight * norm2 / zeta, e_i, E, z2, isign, wm, wr, gopt.eps)
+
+
+def _dist():
+    try:
+        import torch.distributed as dist
+
+        if dist.is_available() and dist.is_initialized():
+            return dist
+    except Exception:
+        pass
+    return None
+
+
+def build_gf(cfg: EDConfig, states: StateList, gopt: Optional[GFOptions] = None, device: int = 0,
+             record: Optional[list] = None, owners: Optional[List[int]] = None, runner=None):
+    """impGmats, impGreal (Nspin, Nspin, Norb, Norb, L) for ed_mode normal
+    (diagonal components, build_gf_normal) and nonsu2 (build_gf_nonsu2,
+    ED_GF_NONSU2.f90:18-333, bath_type normal/hybrid: diagonal components plus
+    the spin-off-diagonal ones from the mixed seeds and the 0.5*(G - (1+i)G_ii -
+    (1+i)G_jj) recombination).
+
+    Seed farm: with a process group initialised, the (component, state, seed)
+    jobs are split over ranks (longest first by target dimension), each rank
+    sums its poles into its own G, and one all_reduce adds the G arrays
+    (2 x L complex numbers per component — no collective inside a job).  State
+    vectors missing on a rank (farm_diag keeps them on their owner) are
+    broadcast from `owners` first.  `runner(cfg, states, gopt, job, wm, wr,
+    G_m, G_r, zeta)` replaces the device job (the CPU tests pass the oracle's)."""
+    gopt = gopt or GFOptions()
+    if cfg.ed_mode == "superc":
+        raise NotImplementedError("superc Green's function (ED_GF_SUPERC) is outside this hot path")
+    No, Nsp = cfg.Norb, cfg.Nspin
+    wm = matsubara(gopt.beta, gopt.Lmats)
+    wr = realaxis(gopt.wini, gopt.wfin, gopt.Lreal)
+    Gm = np.zeros((Nsp, Nsp, No, No, gopt.Lmats), dtype=np.complex128)
+    Gr = np.zeros((Nsp, Nsp, No, No, gopt.Lreal), dtype=np.complex128)
+    dist = _dist()
+    rank = dist.get_rank() if dist else 0
+    world = dist.get_world_size() if dist else 1
+    if dist and owners is not None:
+        from .farm import broadcast_vector
+
+        vecs = list(states.vectors)
+        for k, isec in enumerate(states.sectors):
+            dim = setup_pointers(cfg)[isec - 1].dim
+            cplx = not cfg.is_real() or (vecs[k] is not None and np.iscomplexobj(vecs[k]))
+            flag = [cplx]
+            dist.broadcast_object_list(flag, src=owners[k])
+            vecs[k] = broadcast_vector(vecs[k], owners[k], dim, flag[0], device)
+        states = StateList(list(states.energies), list(states.sectors), vecs)
+    jobs, pairs = _job_list(cfg, states)
+    if world > 1:
+        from .farm import lpt_partition
+
+        costs = [float(min(j[5].dim, gopt.lanc_nGFiter)) * j[5].dim for j in jobs]
+        mine = set(lpt_partition(costs, world)[rank])
+    else:
+        mine = set(range(len(jobs)))
+    zeta = float(states.size)       # T=0: zeta_function = state_list%size (ED_DIAG.f90:411)
+    cache = _SectorCache(cfg, gopt, device)
+    try:
+        for n, job in enumerate(jobs):
+            if n not in mine:
+                continue
+            ispin, jspin, iorb = job[0]
+            g_m, g_r = Gm[ispin, jspin, iorb, iorb], Gr[ispin, jspin, iorb, iorb]
+            if runner is None:
+                _run_job(cfg, states, gopt, job, cache, wm, wr, g_m, g_r, record, zeta)
+            else:
+                runner(cfg, states, gopt, job, wm, wr, g_m, g_r, zeta)
+    finally:
+        cache.close()
+    if world > 1:
+        import torch
+
+        dev = torch.device("cuda", device) if dist.get_backend() == "nccl" else torch.device("cpu")
+        for G in (Gm, Gr):
+            t = torch.view_as_real(torch.from_numpy(G).to(dev))   # (re, im) pairs: plain f64 sum
+            dist.all_reduce(t)
+            G[...] = torch.view_as_complex(t).cpu().numpy()
+    for ispin, jspin, iorb in pairs:               # build_gf_nonsu2 :35-48
+        for G in (Gm, Gr):
+            G[ispin, jspin, iorb, iorb] = 0.5 * (G[ispin, jspin, iorb, iorb]
+                                                 - (1 + 1j) * G[ispin, ispin, iorb, iorb]
+                                                 - (1 + 1j) * G[jspin, jspin, iorb, iorb])
+    return Gm, Gr
 
 
 def build_gf_normal(cfg: EDConfig, states: StateList, gopt: Optional[GFOptions] = None,

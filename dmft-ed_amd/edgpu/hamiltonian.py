@@ -169,6 +169,13 @@ class Sector:
               "lanc_run")
         return a, b, float(ms.value)
 
+    def lanc_mode(self, real: Optional[bool] = None, path: int = -1) -> int:
+        """Recurrence a Lanczos run would take: persistent mode 0 (stored, L2),
+        1 (Kronecker tables in LDS), 2 (stored matrix in registers), or -1
+        (graph-captured multi-kernel)."""
+        vt, _ = self._vec_arg(None, real)
+        return int(_lib.load().ed_sector_lanc_mode(self._h, vt, path))
+
     def eigh(self, neigen: int = 6, ncv: int = 23, maxit: int = 512, tol: float = 1e-12,
              v0: Optional[np.ndarray] = None, vectors: bool = True, real: Optional[bool] = None):
         """sp_eigh (ARPACK, which="SR") replacement: thick-restart Lanczos with

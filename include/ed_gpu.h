@@ -166,6 +166,11 @@ int ed_sector_lanc_tridiag(ed_sector* s, int32_t vtype, const void* v0, int32_t 
 int ed_sector_lanc_eigh(ed_sector* s, int32_t vtype, const void* v0, int32_t nitermax,
                         double threshold, int32_t ncheck, double* egs, void* vect,
                         int32_t* nlanc);
+/* Diagnostic: the Lanczos recurrence a run with (vtype, path) would use —
+ * persistent one-workgroup mode 0 (stored, L2), 1 (Kronecker tables in LDS),
+ * 2 (stored matrix in registers), or -1 (graph-captured multi-kernel).
+ * Honours the ED_GPU_* environment switches. */
+int ed_sector_lanc_mode(ed_sector* s, int32_t vtype, int32_t path);
 /* Lowest `nev` eigenpairs by thick-restart Lanczos with full (CGS2)
  * reorthogonalisation, Krylov basis of `ncv` vectors resident in HBM: the
  * device replacement of SciFortran's ARPACK sp_eigh (ED_DIAG.f90:145-167,

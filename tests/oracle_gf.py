@@ -136,3 +136,29 @@ def build_gf_oracle(cfg, states, gopt):
                                                      - (1 + 1j) * G[ispin, ispin, iorb, iorb]
                                                      - (1 + 1j) * G[jspin, jspin, iorb, iorb])
     return Gm, Gr
+
+
+def oracle_job_runner(cfg, states, gopt, job, wm, wr, G_m, G_r, zeta):
+    """edgpu.gf.build_gf job (one seed of one kept state) from oracle pieces,
+    for the CPU (gloo) seed-farm tests."""
+    from oracle.oracle import tql2
+
+    comp, tag, k, (op, isign, ispin, terms, weight), sec, jsec = job
+    orc = Oracle(cfg)
+    hmap_i = orc.build_sector(sec.q1, sec.q2)
+    hmap_j, v = seed_combo(orc, hmap_i, jsec, op, terms, np.asarray(states.vectors[k]).astype(np.complex128))
+    norm2 = float(np.vdot(v, v).real)
+    if norm2 == 0.0:
+        return
+    v = v / np.sqrt(norm2)
+    nlanc = min(len(hmap_j), gopt.lanc_nGFiter)
+    a, b, n = lanc_tridiag(orc.build_csr(hmap_j), v, nlanc, gopt.threshold)
+    if cfg.ed_mode == "nonsu2":
+        E, Z, ierr = tql2(a[:nlanc], np.concatenate([[0.0], b[1:nlanc]]))
+        z2 = Z[0, :] ** 2
+    else:
+        E, z2 = tridiag_poles(a, b, nlanc)
+    de = E - states.energies[k]
+    peso = weight * norm2 / zeta * z2
+    G_m += (peso[None] / ((1j * wm)[:, None] - isign * de[None])).sum(1)
+    G_r += (peso[None] / ((wr + 1j * gopt.eps)[:, None] - isign * de[None])).sum(1)

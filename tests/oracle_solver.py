@@ -23,6 +23,9 @@ def solve_sector_oracle(cfg, sec, opt, device=0):
         w, v = np.linalg.eigh(A.toarray())
         return SectorResult(sec.isector, (sec.q1, sec.q2), dim, w, neigen, v[:, :neigen], "dense")
     k = 1 if opt.lanc_method == "lanczos" else neigen
-    w, v = sla.eigsh(A, k=k, which="SA", tol=1e-13)
+    # fixed start vector: ARPACK's internal random start advances across calls
+    i = np.arange(1, dim + 1, dtype=np.float64)
+    v0 = np.sin(i) + 1j * np.cos(3.0 * i) if np.iscomplexobj(A.data) else np.sin(i)
+    w, v = sla.eigsh(A, k=k, which="SA", tol=1e-13, v0=v0)
     o = np.argsort(w)
     return SectorResult(sec.isector, (sec.q1, sec.q2), dim, w[o], k, v[:, o], "eigsh")

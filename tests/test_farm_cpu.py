@@ -83,3 +83,50 @@ def test_gloo_farm_matches_serial(cfg_kw, method):
     assign = out[0][4]
     assert all(len(a) > 0 for a in assign)
     assert sorted(i for a in assign for i in a) == [s.isector for s in setup_pointers(cfg)]
+
+
+def _gf_worker(rank, world, port, q, cfg_kw):
+    import torch.distributed as dist
+    from oracle_gf import oracle_job_runner
+    from oracle_solver import solve_sector_oracle
+    from edgpu.gf import GFOptions, build_gf
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = make_config(**cfg_kw)
+    res = farm_diag(cfg, DiagOptions(lanc_method="lanczos"), solver=solve_sector_oracle)
+    Gm, Gr = build_gf(cfg, res.states, GFOptions(Lmats=64, Lreal=64), owners=res.owners,
+                      runner=oracle_job_runner)
+    q.put((rank, Gm, Gr))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("cfg_kw", [
+    dict(Norb=1, Nbath=5, bath="random", seed=5),                       # normal, 2 seeds/state
+    dict(Norb=1, Nbath=3, Nspin=2, ed_mode="nonsu2", bath="random", seed=2),  # 12 seeds/state
+])
+def test_gloo_gf_seed_farm_matches_serial(cfg_kw):
+    """GF seed farm: jobs split over 2 gloo ranks (state vectors broadcast from
+    their farm owner, G all-reduced) equal the serial oracle build."""
+    from oracle_gf import build_gf_oracle
+    from oracle_solver import solve_sector_oracle
+    from edgpu.gf import GFOptions
+
+    cfg = make_config(**cfg_kw)
+    serial = farm_diag(cfg, DiagOptions(lanc_method="lanczos"), solver=solve_sector_oracle)
+    Gm0, Gr0 = build_gf_oracle(cfg, serial.states, GFOptions(Lmats=64, Lreal=64))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gf_worker, args=(r, 2, port, q, cfg_kw)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=300) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, Gm, Gr in out:
+        assert np.max(np.abs(Gm - Gm0)) / np.max(np.abs(Gm0)) < 1e-12
+        assert np.max(np.abs(Gr - Gr0)) / np.max(np.abs(Gr0)) < 1e-12

@@ -24,17 +24,19 @@ def _e0_scipy(csr, dim):
     return float(sla.eigsh(A, k=1, which="SA", tol=1e-14)[0][0])
 
 
-@pytest.mark.parametrize("persist", [True, False], ids=["persistent", "multikernel"])
+@pytest.mark.parametrize("persist", ["default", "l2", "multi"], ids=["persistent", "persist_l2", "multikernel"])
 @pytest.mark.parametrize("name,factory,sectors", CASES, ids=[c[0] for c in CASES])
 def test_tridiag_and_ground_state(name, factory, sectors, persist, monkeypatch):
-    """Both device recurrences: the one-workgroup persistent kernel (default for
-    sectors that fit one CU's LDS) and the graph-captured two-kernel one."""
+    """Every device recurrence: the one-workgroup persistent kernel (default for
+    sectors that fit one CU: stored matrix in registers / Kronecker tables in
+    LDS), its opt-in L2-streaming stored mode, and the graph-captured
+    two-kernel one."""
     from edgpu.hamiltonian import Sector
 
-    if not persist:
+    if persist == "multi":
         monkeypatch.setenv("ED_GPU_NO_PERSIST", "1")
-    else:
-        monkeypatch.setenv("ED_GPU_PERSIST_STORED", "1")   # cover the opt-in stored mode too
+    elif persist == "l2":
+        monkeypatch.setenv("ED_GPU_PERSIST_STORED", "1")
 
     cfg = factory()
     orc = Oracle(cfg)
@@ -79,7 +81,7 @@ def test_real_lanczos_c2():
         assert abs(e1 - e0) <= 1e-10 * abs(e0)
 
 
-@pytest.mark.parametrize("path", ["stored", "kron"])
+@pytest.mark.parametrize("path", ["stored_l2", "stored_reg", "kron"])
 def test_persistent_matches_multikernel(path, monkeypatch):
     """Same start vector, same sector: the two recurrences agree step by step
     (first 40 steps to 1e-9; only the reduction order differs)."""
@@ -87,9 +89,12 @@ def test_persistent_matches_multikernel(path, monkeypatch):
     from cases import c2
 
     cfg = c2()
-    kw = dict(stored=True) if path == "stored" else dict(stored=False, direct=True)
-    monkeypatch.setenv("ED_GPU_PERSIST_STORED", "1")
+    kw = dict(stored=False, direct=True) if path == "kron" else dict(stored=True)
+    if path == "stored_l2":
+        monkeypatch.setenv("ED_GPU_PERSIST_STORED", "1")
     with Sector(cfg, 4, 4, real=True, **kw) as S:
+        want = {"stored_l2": 0, "stored_reg": 2, "kron": 1}[path]
+        assert S.lanc_mode(real=True) == want
         v0 = np.sin(np.arange(1, S.dim + 1, dtype=np.float64))
         a1, b1, n1 = S.lanc_tridiag(v0, 60)
         monkeypatch.setenv("ED_GPU_NO_PERSIST", "1")

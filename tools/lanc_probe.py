@@ -23,17 +23,19 @@ cases = [
     ("c5 nonsu2", make_config(Norb=1, Nbath=6, Nspin=2, ed_mode="nonsu2", bath="random"), (7, 0), True),
     ("c4 real", make_config(Norb=2, Nbath=5, bath="random"), (6, 6), True),
 ]
+MODES = {"stored": [("reg", {}), ("l2", {"ED_GPU_PERSIST_STORED": "1"}), ("multi", {"ED_GPU_NO_PERSIST": "1"})],
+         "direct": [("persist", {}), ("multi", {"ED_GPU_NO_PERSIST": "1"})]}
 for name, cfg, q, real in cases:
     for kind in ("stored", "direct"):
-        for persist in (True, False):
-            if persist:
-                os.environ.pop("ED_GPU_NO_PERSIST", None)
-            else:
-                os.environ["ED_GPU_NO_PERSIST"] = "1"
+        for label, env in MODES[kind]:
+            for k in ("ED_GPU_PERSIST_STORED", "ED_GPU_NO_PERSIST"):
+                os.environ.pop(k, None)
+            os.environ.update(env)
             with Sector(cfg, q[0], q[1], stored=kind == "stored", direct=kind == "direct", real=real) as S:
                 dt = torch.float64 if real else torch.complex128
                 v0 = torch.sin(torch.arange(1, S.dim + 1, dtype=torch.float64, device="cuda")).to(dt)
+                mode = S.lanc_mode(real=real)
                 S.lanc_run(a.niter, v0_dev=v0)
                 ms = min(S.lanc_run(a.niter, v0_dev=v0)[2] for _ in range(3))
-                print(f"{name:11s} dim={S.dim:7d} {kind:6s} {'persist' if persist else 'multi  '} "
+                print(f"{name:11s} dim={S.dim:7d} {kind:6s} {label:7s} mode={mode:2d} "
                       f"{1e3 * ms / a.niter:8.3f} us/iter  {a.niter / (ms * 1e-3):10.0f} it/s", flush=True)
