@@ -160,6 +160,7 @@ def main():
     ap.add_argument("--niter", type=int, default=512)
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-farm", action="store_true", help="skip the configs[3]/[4] sections")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -218,8 +219,8 @@ def main():
     direct_ips = args.niter / (min(dms) * 1e-3)
     Sd.close()
 
-    farm = bench_farm(dist, world, dev)
-    nonsu2 = bench_nonsu2(dist, world, dev)
+    farm = None if args.no_farm else bench_farm(dist, world, dev)
+    nonsu2 = None if args.no_farm else bench_nonsu2(dist, world, dev)
 
     out = None
     if rank == 0:
@@ -232,8 +233,15 @@ def main():
             dim28, nnz28, ms28 = measure_spmv(Sector, cfg28, (7, 7), 50)
             B = spmv_bytes_real(nnz28, dim28)
             ach = B / (ms28 * 1e-3) / 1e9
+            traffic, tsrc = None, None
+            tfile = os.path.join(ROOT, "profiles", "r1", "spmv_n28_traffic.json")
+            if os.path.exists(tfile):   # PMC bytes cannot be read in-process: rocprofv3 passes
+                with open(tfile) as fh:
+                    traffic = json.load(fh)["traffic_bytes_per_launch"]
+                tsrc = "profiles/r1/spmv_n28_traffic.json (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, same kernel+sector)"
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "traffic_source": tsrc,
                     "kernel": "k_spmv<real,real> (stored SELL-64 H·v)",
                     "workload": f"Nlevels=28 Norb=1 Nbath=13 (7,7) sector, dim {dim28}, nnz {nnz28}, "
                                 f"real(8), {B} algorithmic bytes/launch",

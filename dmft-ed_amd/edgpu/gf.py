@@ -63,7 +63,10 @@ def tridiag_poles(alfa: np.ndarray, beta: np.ndarray, n: int) -> Tuple[np.ndarra
 
     if n == 1:
         return np.array([alfa[0]]), np.array([1.0])
-    w, z = eigh_tridiagonal(alfa[:n], beta[1:n])
+    # implicit QL/QR (LAPACK dstev, like SciFortran's tridiagonal eigh): MRRR
+    # (stemr) can fail on the near-degenerate ghost clusters that long
+    # unreorthogonalised GF runs produce
+    w, z = eigh_tridiagonal(alfa[:n], beta[1:n], lapack_driver="stev")
     return w, z[0, :] ** 2
 
 
