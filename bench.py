@@ -37,8 +37,16 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
 def spmv_bytes_real(nnz, dim):
-    """Algorithmic bytes of one real(8) stored SpMV: 12 nnz + 8 (dim+1) + 16 dim."""
+    """Algorithmic bytes of one real(8) stored SpMV in the reference's CSR form
+    (SURVEY §8d): 12 nnz + 8 (dim+1) + 16 dim."""
     return 12 * nnz + 8 * (dim + 1) + 16 * dim
+
+
+def spmv_bytes_packed(padded, dim):
+    """Algorithmic bytes of one packed SELL-64 SpMV (k_spmv_pk): 4-B words per
+    slot, slice pointers, real(8) diagonal, read v, write Hv."""
+    nslice = (dim + 63) // 64
+    return 4 * padded + 8 * (nslice + 1) + 8 * dim + 16 * dim
 
 
 def time_kernel(fn, iters, stream):
@@ -53,9 +61,11 @@ def time_kernel(fn, iters, stream):
     return e0.elapsed_time(e1) / iters
 
 
-def measure_spmv(Sector, cfg, q, iters, warm=5):
+def measure_spmv(Sector, cfg, q, iters, warm=5, info=None):
     with Sector(cfg, q[0], q[1], stored=True, direct=False, real=True) as S:
         dim, nnz = S.dim, S.nnz
+        if info is not None:
+            info.update(packed=int(S.info.packed), padded=int(S.info.padded), npdict=int(S.info.npdict))
         x = torch.sin(torch.arange(1, dim + 1, dtype=torch.float64, device="cuda")).contiguous()
         y = torch.empty_like(x)
         st = torch.cuda.current_stream()
@@ -230,22 +240,31 @@ def main():
         roof = None
         if not args.no_roofline:
             cfg28 = make_config(Norb=1, Nbath=13, bath="random", seed=20251015)
-            dim28, nnz28, ms28 = measure_spmv(Sector, cfg28, (7, 7), 50)
-            B = spmv_bytes_real(nnz28, dim28)
+            inf28 = {}
+            dim28, nnz28, ms28 = measure_spmv(Sector, cfg28, (7, 7), 50, info=inf28)
+            Bref = spmv_bytes_real(nnz28, dim28)
+            B = spmv_bytes_packed(inf28["padded"], dim28) if inf28["packed"] else Bref
             ach = B / (ms28 * 1e-3) / 1e9
             traffic, tsrc = None, None
             tfile = os.path.join(ROOT, "profiles", "r1", "spmv_n28_traffic.json")
             if os.path.exists(tfile):   # PMC bytes cannot be read in-process: rocprofv3 passes
                 with open(tfile) as fh:
-                    traffic = json.load(fh)["traffic_bytes_per_launch"]
-                tsrc = "profiles/r1/spmv_n28_traffic.json (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, same kernel+sector)"
+                    tj = json.load(fh)
+                if bool(tj.get("packed", False)) == bool(inf28["packed"]):   # same kernel only
+                    traffic = tj["traffic_bytes_per_launch"]
+                    tsrc = ("profiles/r1/spmv_n28_traffic.json (rocprofv3 FETCH_SIZE/WRITE_SIZE "
+                            "passes, same kernel+sector)")
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "traffic_source": tsrc,
-                    "kernel": "k_spmv<real,real> (stored SELL-64 H·v)",
+                    "kernel": ("k_spmv_pk<real> (stored SELL-64, 32-bit {col|value index} words, "
+                               f"{inf28['npdict']}-value dictionary)") if inf28["packed"]
+                              else "k_spmv<real,real> (stored SELL-64 H·v)",
                     "workload": f"Nlevels=28 Norb=1 Nbath=13 (7,7) sector, dim {dim28}, nnz {nnz28}, "
                                 f"real(8), {B} algorithmic bytes/launch",
-                    "ms_per_launch": round(ms28, 4)}
+                    "ms_per_launch": round(ms28, 4),
+                    "reference_csr_bytes": Bref,
+                    "reference_csr_equivalent_gbs": round(Bref / (ms28 * 1e-3) / 1e9, 1)}
         cpu = None if args.no_cpu else cpu_baseline()
         out = {
             "metric": "Lanczos SpMV GB/s + ground-state iters/s, Ns=16 half-filled sector, 1/2/4/8 GPU",

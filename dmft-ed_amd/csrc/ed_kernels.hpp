@@ -7,6 +7,7 @@
 //   k_count        elements per row + SELL-64 slice width   ed_buildH_c pass 1
 //   k_fill         SELL-64 fill, reference row order        ed_buildH_c + sp_insert_element
 //   k_spmv         stored H·v, SELL-64                      spMatVec_cc STORED_HxV.f90:132-143
+//   k_spmv_pk      same, 32-bit {col|dictionary index} words (real H)
 //   k_direct       matrix-free H·v (gather, any ed_mode)     directMatVec_cc DIRECT_HxV.f90:21-92
 //   k_kron         matrix-free H·v, normal mode without Jx/Jp: H = D + Hup(x)1 + 1(x)Hdw
 //   k_lanc_*       device-resident plain Lanczos recurrence .repo/PLAIN_LANCZOS.f90:87-118
@@ -278,6 +279,18 @@ __global__ void __launch_bounds__(kBlock) k_fill(const EdModel* __restrict__ Mp,
       vals[q] = mk<HC>(0.0, 0.0);
     }
   }
+  // lanes past dim in the last slice: defined padding too (every slot of the
+  // SELL arrays is then a valid (col, value) pair, e.g. for the packed form)
+  const int64_t tail = ((dim + 63) & ~(int64_t)63) - dim;
+  if (blockIdx.x == 0 && threadIdx.x < tail) {
+    const int64_t i = dim + threadIdx.x, s = i >> 6;
+    const int w = (int)((sptr[s + 1] - sptr[s]) >> 6);
+    for (int k = 0; k < w; k++) {
+      const int64_t q = sptr[s] + (i & 63) + 64 * (int64_t)k;
+      cols[q] = 0;
+      vals[q] = mk<HC>(0.0, 0.0);
+    }
+  }
 }
 
 // --------------------------------------------------------------- epilogues
@@ -511,6 +524,107 @@ __global__ void __launch_bounds__(kBlock) k_spmv(const val_t<HC>* __restrict__ d
         V g[kChunk];
 #pragma unroll
         for (int k = 0; k < kChunk; k++) g[k] = x[c[k]];
+#pragma unroll
+        for (int k = 0; k < kChunk; k++)
+          if (k0 + k < w) acc = add(acc, mul(h[k], g[k]));
+      }
+      part += epi.row(i, acc, xi);
+    }
+  }
+  epi.finish(part);
+}
+
+// ------------------------------------------- stored H·v, packed (real H)
+// When a real sector's off-diagonal values take at most 256 distinct bit
+// patterns (hoppings, exchange, pair hopping: tens), each SELL slot is one
+// 32-bit word {col:24 | dictionary index:8}: 4 B per entry instead of 12,
+// the value read from a 2 KB dictionary that stays in L1.  Same slots, same
+// order, same doubles as k_spmv: bit-identical results.
+constexpr int kPackShift = 24;
+constexpr uint32_t kPackColMask = (1u << kPackShift) - 1;
+constexpr int kDictTable = 4096;  // open-addressing hash of value bit patterns
+constexpr unsigned long long kDictEmpty = ~0ull;
+
+__device__ __forceinline__ uint32_t dict_hash(unsigned long long k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  return (uint32_t)k & (kDictTable - 1);
+}
+
+// Insert every value's bit pattern; plain reads first so that the few
+// distinct keys cost one CAS each, not one per slot.
+__global__ void __launch_bounds__(kBlock) k_dict_insert(const double* __restrict__ vals, int64_t n,
+                                                        unsigned long long* table,
+                                                        unsigned int* overflow) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    const unsigned long long key = (unsigned long long)__double_as_longlong(vals[i]);
+    if (key == kDictEmpty) {
+      atomicOr(overflow, 1u);
+      continue;
+    }
+    uint32_t h = dict_hash(key);
+    bool done = false;
+    for (int probe = 0; probe < kDictTable && !done; probe++) {
+      const unsigned long long cur = ((volatile unsigned long long*)table)[h];
+      if (cur == key) {
+        done = true;
+      } else if (cur == kDictEmpty) {
+        const unsigned long long prev = atomicCAS(table + h, kDictEmpty, key);
+        if (prev == kDictEmpty || prev == key) done = true;
+        else h = (h + 1) & (kDictTable - 1);  // lost the race to another key: probe on
+      } else {
+        h = (h + 1) & (kDictTable - 1);
+      }
+    }
+    if (!done) atomicOr(overflow, 1u);
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_dict_pack(const int32_t* __restrict__ cols,
+                                                      const double* __restrict__ vals, int64_t n,
+                                                      const unsigned long long* __restrict__ table,
+                                                      const uint8_t* __restrict__ tidx,
+                                                      uint32_t* __restrict__ words) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    const unsigned long long key = (unsigned long long)__double_as_longlong(vals[i]);
+    uint32_t h = dict_hash(key);
+    while (table[h] != key) h = (h + 1) & (kDictTable - 1);  // present by construction
+    words[i] = (uint32_t)cols[i] | ((uint32_t)tidx[h] << kPackShift);
+  }
+}
+
+template <bool VC, int NT, class Epi>
+__global__ void __launch_bounds__(kBlock) k_spmv_pk(const double* __restrict__ diag,
+                                                    const int64_t* __restrict__ sptr,
+                                                    const uint32_t* __restrict__ words,
+                                                    const double* __restrict__ dict,
+                                                    const val_t<VC>* __restrict__ x, int64_t dim,
+                                                    int64_t nslice, Epi epi) {
+  using V = val_t<VC>;
+  if (epi.skip()) return;
+  epi.prepare();
+  double part = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nslice * 64;
+       i += (int64_t)gridDim.x * kBlock) {
+    if (i < dim) {
+      const int64_t s = i >> 6;
+      const int64_t s0 = sptr[s];
+      const int w = (int)((sptr[s + 1] - s0) >> 6);
+      const uint32_t* wp = words + s0 + (i & 63);
+      const V xi = x[i];
+      V acc = add(vzero<V>(), mul(ldm<NT>(diag + i), xi));
+      for (int k0 = 0; k0 < w; k0 += kChunk) {
+        uint32_t c[kChunk];
+#pragma unroll
+        for (int k = 0; k < kChunk; k++) c[k] = (k0 + k < w) ? ldm<NT>(wp + 64 * (k0 + k)) : (uint32_t)i;
+        V g[kChunk];
+        double h[kChunk];
+#pragma unroll
+        for (int k = 0; k < kChunk; k++) {
+          g[k] = x[c[k] & kPackColMask];
+          h[k] = dict[c[k] >> kPackShift];
+        }
 #pragma unroll
         for (int k = 0; k < kChunk; k++)
           if (k0 + k < w) acc = add(acc, mul(h[k], g[k]));

@@ -92,6 +92,10 @@ struct ed_sector {
   void* d_vals = nullptr;
   uint16_t* d_cnt = nullptr;
   int64_t nnz = 0, padded = 0;
+  // packed stored H (real values, <= 256 distinct): {col:24 | index:8} words
+  uint32_t* d_words = nullptr;
+  double* d_pdict = nullptr;
+  int npdict = 0;
   // matrix-free
   bool kron = false;
   KronHost K;
@@ -105,6 +109,7 @@ struct ed_sector {
   // register-resident stored matrix for the persistent kernel (MODE 2)
   int preg_E = 0;           // 0 not built, -1 ineligible, else ELL row width W
   int preg_rpt = 0;         // rows per thread (template value)
+  int kreg_W = 0, kreg_rpt = 0;  // MODE 3 (Kronecker words in registers)
   uint32_t* d_pk = nullptr;
   void* d_dict = nullptr;
   int ndict = 0;
@@ -155,6 +160,62 @@ static void sector_free(ed_sector* s) {
 }
 
 // ---------------------------------------------------------- stored build
+// Dictionary of the distinct off-diagonal values (device hash of bit
+// patterns); when there are at most 256, pack every SELL slot into one word.
+static int build_pack(ed_sector* s) {
+  const int64_t slots = s->padded;
+  if (slots == 0) return ED_OK;
+  unsigned long long* table;
+  unsigned int* ovf;
+  uint8_t* tidx;
+  HIPCK(hipMalloc((void**)&table, kDictTable * 8));
+  HIPCK(hipMalloc((void**)&ovf, 4));
+  HIPCK(hipMalloc((void**)&tidx, kDictTable));
+  auto cleanup = [&]() {
+    (void)hipFree(table);
+    (void)hipFree(ovf);
+    (void)hipFree(tidx);
+  };
+  HIPCK(hipMemsetAsync(table, 0xFF, kDictTable * 8, s->stream));
+  HIPCK(hipMemsetAsync(ovf, 0, 4, s->stream));
+  hipLaunchKernelGGL(k_dict_insert, dim3(grid_for(slots)), dim3(kBlock), 0, s->stream,
+                     (const double*)s->d_vals, slots, table, ovf);
+  HIPCK(hipGetLastError());
+  std::vector<unsigned long long> ht(kDictTable);
+  unsigned int hov = 0;
+  HIPCK(hipMemcpyAsync(ht.data(), table, kDictTable * 8, hipMemcpyDeviceToHost, s->stream));
+  HIPCK(hipMemcpyAsync(&hov, ovf, 4, hipMemcpyDeviceToHost, s->stream));
+  HIPCK(hipStreamSynchronize(s->stream));
+  std::vector<uint8_t> ti(kDictTable, 0);
+  std::vector<double> dict;
+  for (int h = 0; h < kDictTable && !hov; h++) {
+    if (ht[h] == kDictEmpty) continue;
+    if (dict.size() == 256) {
+      hov = 1;
+      break;
+    }
+    ti[h] = (uint8_t)dict.size();
+    double v;
+    memcpy(&v, &ht[h], 8);
+    dict.push_back(v);
+  }
+  if (hov) {
+    cleanup();
+    return ED_OK;  // too many distinct values: the plain SELL path serves
+  }
+  CK(dalloc(s, (void**)&s->d_pdict, 256 * 8));
+  CK(dalloc(s, (void**)&s->d_words, slots * 4));
+  HIPCK(hipMemcpyAsync(s->d_pdict, dict.data(), dict.size() * 8, hipMemcpyHostToDevice, s->stream));
+  HIPCK(hipMemcpyAsync(tidx, ti.data(), kDictTable, hipMemcpyHostToDevice, s->stream));
+  hipLaunchKernelGGL(k_dict_pack, dim3(grid_for(slots)), dim3(kBlock), 0, s->stream, s->d_cols,
+                     (const double*)s->d_vals, slots, table, tidx, s->d_words);
+  HIPCK(hipGetLastError());
+  HIPCK(hipStreamSynchronize(s->stream));
+  cleanup();
+  s->npdict = (int)dict.size();
+  return ED_OK;
+}
+
 static int build_stored(ed_sector* s) {
   const int64_t dim = s->dim, ns = s->nslice;
   uint16_t* cnt;
@@ -206,6 +267,7 @@ static int build_stored(ed_sector* s) {
   int64_t nnz = dim;
   for (int64_t i = 0; i < dim; i++) nnz += hc[i];
   s->nnz = nnz;
+  if (!s->hc && dim <= (int64_t)kPackColMask + 1 && !getenv("ED_GPU_NO_PACK")) CK(build_pack(s));
   return ED_OK;
 }
 
@@ -355,7 +417,15 @@ static int launch_hxv_t(ed_sector* s, int path, const void* x, Epi epi, hipStrea
   using V = val_t<VC>;
   const int64_t dim = s->dim, ns = s->nslice;
   const int g = grid_for(ns * 64);
-  if (path == 0) {
+  if (path == 0 && !HC && s->d_words) {
+    const int64_t mbytes = s->padded * 4 + dim * 8;
+    if (mbytes > (int64_t)192 << 20)
+      hipLaunchKernelGGL((k_spmv_pk<VC, 1, Epi>), dim3(g), dim3(kBlock), 0, st, (const double*)s->d_diag,
+                         s->d_sptr, s->d_words, s->d_pdict, (const V*)x, dim, ns, epi);
+    else
+      hipLaunchKernelGGL((k_spmv_pk<VC, 0, Epi>), dim3(g), dim3(kBlock), 0, st, (const double*)s->d_diag,
+                         s->d_sptr, s->d_words, s->d_pdict, (const V*)x, dim, ns, epi);
+  } else if (path == 0) {
     // non-temporal matrix loads once the matrix cannot stay in the 256 MB MALL
     const int64_t mbytes = s->padded * (4 + (HC ? 16 : 8)) + dim * (HC ? 16 : 8);
     if (mbytes > (int64_t)192 << 20)
@@ -608,6 +678,8 @@ static int build_preg(ed_sector* s) {
 // Returns the persistent mode (0 stored, 1 Kronecker, 2 stored in registers)
 // or -1 when the sector does not fit one workgroup's LDS / register budget.
 static int64_t persist_lds(const ed_sector* s, int vc, int mode);
+// ELL words per lane that compile without scratch (-Rpass-analysis=kernel-resource-usage)
+constexpr int preg_cap(bool hc, bool vc) { return vc ? (hc ? 72 : 84) : 120; }
 static int persist_mode(ed_sector* s, int vc, int path) {
   if (getenv("ED_GPU_NO_PERSIST")) return -1;
   const int64_t vs = vc ? 16 : 8;
@@ -628,11 +700,28 @@ static int persist_mode(ed_sector* s, int vc, int path) {
     if (s->dim > 10 * (int64_t)kPRegBlock) return -1;
     const int W = build_preg(s);
     if (W < 0) return -1;
-    // entries per lane that compile without scratch (-Rpass-analysis=kernel-resource-usage)
-    const int cap = vc ? (s->hc ? 72 : 84) : 120;
-    if (s->preg_rpt * W > cap) return -1;
+    if (s->preg_rpt * W > preg_cap(s->hc, vc)) return -1;
     if (persist_lds(s, vc, 2) > kLdsBudget) return -1;
     return 2;
+  }
+  if (path == 2 && !getenv("ED_GPU_NO_PREG") && s->dim <= 10 * (int64_t)kPRegBlock) {
+    // MODE 3: ELL words generated in-kernel from the hop tables
+    const KronHost& K = s->K;
+    const int deg = K.degup + K.degdw;
+    int W = 0;
+    for (int w : {8, 12, 14, 16})
+      if (!W && deg <= w) W = w;
+    const int64_t rpt = (s->dim + kPRegBlock - 1) / kPRegBlock;
+    const int RPT = rpt <= 2 ? 2 : rpt <= 4 ? 4 : rpt <= 6 ? 6 : rpt <= 8 ? 8 : 10;
+    const int64_t hs = s->hc ? 16 : 8;
+    const int64_t dict = ((int64_t)(K.degup * K.dimup + K.degdw * K.dimdw) + 1) * hs;
+    const int cap = preg_cap(s->hc, vc);
+    const int64_t l3 = ((dict + 15) & ~(int64_t)15) + lds + ((s->dim * hs + 15) & ~(int64_t)15);
+    if (W && RPT * W <= cap && dict <= (int64_t)kPkOffMask + 1 && l3 <= kLdsBudget) {
+      s->kreg_W = W;
+      s->kreg_rpt = RPT;
+      return 3;
+    }
   }
   if (path == 2) {
     const KronHost& K = s->K;
@@ -651,6 +740,11 @@ static int64_t persist_lds(const ed_sector* s, int vc, int mode) {
     const int64_t hs = s->hc ? 16 : 8;
     return lds + ((s->dim * hs + 15) & ~(int64_t)15) + (((int64_t)s->ndict * hs + 15) & ~(int64_t)15);
   }
+  if (mode == 3) {
+    const int64_t hs = s->hc ? 16 : 8;
+    const int64_t dict = ((int64_t)(s->K.degup * s->K.dimup + s->K.degdw * s->K.dimdw) + 1) * hs;
+    return lds + ((s->dim * hs + 15) & ~(int64_t)15) + ((dict + 15) & ~(int64_t)15);
+  }
   if (mode == 1) {
     const KronHost& K = s->K;
     const int64_t hs = s->hc ? 16 : 8;
@@ -664,33 +758,37 @@ static int64_t persist_lds(const ed_sector* s, int vc, int mode) {
 
 template <bool HC, bool VC, int MODE, int RPT, int E = 1>
 static int persist_launch_t(ed_sector* s, int64_t lds, hipStream_t st) {
-  constexpr int NT = MODE == 2 ? kPRegBlock : kPBlock;
+  if constexpr (MODE >= 2 && RPT * E > preg_cap(HC, VC)) {
+    return fail(ED_ERR_UNSUPPORTED, "register-resident ELL exceeds the spill-free budget");
+  } else {
+  constexpr int NT = MODE >= 2 ? kPRegBlock : kPBlock;
   auto fn = k_lanc_persist<HC, VC, MODE, RPT, E, NT>;
   HIPCK(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(fn, dim3(1), dim3(NT), (size_t)lds, st, (const PersistRun<HC>*)s->d_prun);
   HIPCK(hipGetLastError());
   return ED_OK;
+  }
 }
 
-template <bool HC, bool VC, int W>
+template <bool HC, bool VC, int MODE, int W>
 static int persist_launch_e(ed_sector* s, int64_t lds, hipStream_t st) {
-  switch (s->preg_rpt) {
-    case 2: return persist_launch_t<HC, VC, 2, 2, W>(s, lds, st);
-    case 4: return persist_launch_t<HC, VC, 2, 4, W>(s, lds, st);
-    case 6: return persist_launch_t<HC, VC, 2, 6, W>(s, lds, st);
-    case 8: return persist_launch_t<HC, VC, 2, 8, W>(s, lds, st);
-    default: return persist_launch_t<HC, VC, 2, 10, W>(s, lds, st);
+  switch (MODE == 2 ? s->preg_rpt : s->kreg_rpt) {
+    case 2: return persist_launch_t<HC, VC, MODE, 2, W>(s, lds, st);
+    case 4: return persist_launch_t<HC, VC, MODE, 4, W>(s, lds, st);
+    case 6: return persist_launch_t<HC, VC, MODE, 6, W>(s, lds, st);
+    case 8: return persist_launch_t<HC, VC, MODE, 8, W>(s, lds, st);
+    default: return persist_launch_t<HC, VC, MODE, 10, W>(s, lds, st);
   }
 }
 
 template <bool HC, bool VC, int MODE>
 static int persist_launch_m(ed_sector* s, int64_t lds, hipStream_t st) {
-  if constexpr (MODE == 2) {
-    switch (s->preg_E) {
-      case 8: return persist_launch_e<HC, VC, 8>(s, lds, st);
-      case 12: return persist_launch_e<HC, VC, 12>(s, lds, st);
-      case 14: return persist_launch_e<HC, VC, 14>(s, lds, st);
-      default: return persist_launch_e<HC, VC, 16>(s, lds, st);
+  if constexpr (MODE >= 2) {
+    switch (MODE == 2 ? s->preg_E : s->kreg_W) {
+      case 8: return persist_launch_e<HC, VC, MODE, 8>(s, lds, st);
+      case 12: return persist_launch_e<HC, VC, MODE, 12>(s, lds, st);
+      case 14: return persist_launch_e<HC, VC, MODE, 14>(s, lds, st);
+      default: return persist_launch_e<HC, VC, MODE, 16>(s, lds, st);
     }
   } else {
   const int64_t rpt = (s->dim + kPBlock - 1) / kPBlock;  // rows per thread, exact
@@ -741,22 +839,24 @@ static int persist_iters(ed_sector* s, int mode, bool basis, int niter, int firs
     else {
       PersistRun<true> r;
       fill(r);
-      if (mode == 1) r.K = kron_args<true>(s);
+      if (mode == 1 || mode == 3) r.K = kron_args<true>(s);
       HIPCK(hipMemcpyAsync(s->d_prun, &r, sizeof(r), hipMemcpyHostToDevice, st));
       HIPCK(hipStreamSynchronize(st));  // r is a stack temporary
       return mode == 0 ? persist_launch_m<true, true, 0>(s, lds, st)
              : mode == 1 ? persist_launch_m<true, true, 1>(s, lds, st)
-                         : persist_launch_m<true, true, 2>(s, lds, st);
+             : mode == 2 ? persist_launch_m<true, true, 2>(s, lds, st)
+                         : persist_launch_m<true, true, 3>(s, lds, st);
     }
   }
   PersistRun<false> r;
   fill(r);
-  if (mode == 1) r.K = kron_args<false>(s);
+  if (mode == 1 || mode == 3) r.K = kron_args<false>(s);
   HIPCK(hipMemcpyAsync(s->d_prun, &r, sizeof(r), hipMemcpyHostToDevice, st));
   HIPCK(hipStreamSynchronize(st));  // r is a stack temporary
   return mode == 0 ? persist_launch_m<false, VC, 0>(s, lds, st)
          : mode == 1 ? persist_launch_m<false, VC, 1>(s, lds, st)
-                     : persist_launch_m<false, VC, 2>(s, lds, st);
+         : mode == 2 ? persist_launch_m<false, VC, 2>(s, lds, st)
+                     : persist_launch_m<false, VC, 3>(s, lds, st);
 }
 
 static int persist_set_thresh(ed_sector* s, double thresh, hipStream_t st) {
@@ -1230,6 +1330,8 @@ int ed_sector_get_info(const ed_sector* s, ed_sector_info* info) {
   info->dimup = s->T.dimup;
   info->dimdw = s->T.dimdw;
   info->device_bytes = s->bytes;
+  info->packed = s->d_words ? 1 : 0;
+  info->npdict = s->npdict;
   return ED_OK;
 }
 

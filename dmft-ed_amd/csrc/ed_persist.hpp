@@ -18,6 +18,8 @@
 //     dozen), padded with the dictionary's 0.0; diagonal, dictionary and v in
 //     LDS.  No matrix byte leaves the CU after the first iteration and the
 //     entry loop has no branch, so every gather of a row is in flight at once;
+//     MODE 3 is the matrix-free twin: the same words generated in-kernel
+//     from the Kronecker hop tables (dictionary = the tables' values);
 //   * alpha and beta are block reductions (wave shuffles + 16-entry LDS),
 //     three barriers per iteration, no global synchronisation.
 // Independent runs (GF seeds, sector replicas) use one workgroup each
@@ -125,7 +127,8 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC>* __res
   // --- MODE 2: dictionary | v | diagonal in LDS, ELL entries in registers.
   // (E is the row width W; the dictionary comes first so that its byte
   // offsets fit 14 bits; vl moves behind it)
-  uint32_t pk[MODE == 2 ? RPT * E : 1];
+  constexpr bool REG = MODE == 2 || MODE == 3;
+  uint32_t pk[REG ? RPT * E : 1];
   const H* dg = nullptr;
   const unsigned char* dct = smem;
   if constexpr (MODE == 2) {
@@ -137,6 +140,47 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC>* __res
     dg = s_g;
 #pragma unroll
     for (int k = 0; k < RPT * E; k++) pk[k] = a.pk[k * NT + tid];
+  }
+  if constexpr (MODE == 3) {
+    // matrix-free: the ELL words are generated here from the Kronecker hop
+    // tables (no matrix in HBM); the dictionary is the tables' value arrays
+    // [upv | dwv | 0], so entry order and values are those of k_kron
+    const KronArgs<HC>& K = a.K;
+    const int du = (int)K.dimup, dd = (int)K.dimdw;
+    const int nup = K.degup * du, ndw = K.degdw * dd;
+    H* sd = (H*)smem;
+    for (int t = tid; t < nup; t += NT) sd[t] = K.upv[t];
+    for (int t = tid; t < ndw; t += NT) sd[nup + t] = K.dwv[t];
+    if (tid == 0) sd[nup + ndw] = mk<HC>(0.0, 0.0);
+    const int64_t dbytes = ((int64_t)(nup + ndw + 1) * sizeof(H) + 15) & ~(int64_t)15;
+    vl = (V*)(smem + dbytes);
+    H* s_g = (H*)(smem + dbytes + ((dim * sizeof(V) + 15) & ~(int64_t)15));
+    for (int64_t t = tid; t < dim; t += NT) {
+      const int iw = (int)(t / du), iu = (int)(t - (int64_t)iw * du);
+      s_g[t] = add(add(K.aup[iu], K.adw[iw]), mk<HC>(K.uimp[K.impu[iu] * K.nimp + K.impd[iw]], 0.0));
+    }
+    dg = s_g;
+    const uint32_t hs = sizeof(H);
+    const uint32_t zero = (uint32_t)((nup + ndw) * hs) << kPkColBits;
+#pragma unroll
+    for (int r = 0; r < RPT; r++) {
+      const int64_t i = tid + (int64_t)r * NT;
+      const int iw = (int)(i / du), iu = (int)(i - (int64_t)iw * du);
+#pragma unroll
+      for (int e = 0; e < E; e++) {
+        uint32_t wd = zero;
+        if (i < dim) {
+          if (e < K.degup) {
+            const int q = e * du + iu;
+            wd = (uint32_t)(iw * du + K.upc[q]) | (((uint32_t)q * hs) << kPkColBits);
+          } else if (e < K.degup + K.degdw) {
+            const int q = (e - K.degup) * dd + iw;
+            wd = (uint32_t)(K.dwc[q] * du + iu) | (((uint32_t)(nup + q) * hs) << kPkColBits);
+          }
+        }
+        pk[r * E + e] = wd;
+      }
+    }
   }
 
   // --- state in
@@ -194,7 +238,7 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC>* __res
 
   for (int k = 0; k < a.niter; k++) {
     const int it = it0 + k;
-    if constexpr (MODE == 2) {
+    if constexpr (REG) {
       // entries are loop-invariant: keep the compiler from hoisting their
       // decoded addresses out of the iteration loop (2 VGPRs per entry)
 #pragma unroll
@@ -228,7 +272,7 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC>* __res
             for (int kk = 0; kk < kPChunk; kk++)
               if (k0 + kk < wd) acc = add(acc, mul(h[kk], vl[c[kk]]));
           }
-        } else if constexpr (MODE == 2) {
+        } else if constexpr (REG) {
           acc = mul(dg[i], xi);
 #pragma unroll
           for (int e = 0; e < E; e++) {

@@ -56,7 +56,8 @@ SIGNATURES = {
 class SectorInfo(ctypes.Structure):
     _fields_ = [("dim", _i64), ("nnz", _i64), ("padded", _i64), ("ns", _i32), ("mode", _i32),
                 ("q1", _i32), ("q2", _i32), ("flags", _i32), ("kron", _i32),
-                ("dimup", _i64), ("dimdw", _i64), ("device_bytes", _i64)]
+                ("dimup", _i64), ("dimdw", _i64), ("device_bytes", _i64),
+                ("packed", _i32), ("npdict", _i32)]
 
 
 class EDGPUError(RuntimeError):

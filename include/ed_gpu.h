@@ -111,6 +111,8 @@ typedef struct ed_sector_info {
   int32_t kron;     /* 1 if the direct path uses the (DimUp x DimDw) form */
   int64_t dimup, dimdw;   /* factor dimensions (normal mode), else 0    */
   int64_t device_bytes;   /* device memory held by the sector           */
+  int32_t packed;   /* 1 if stored H·v reads 32-bit {col|value index} words */
+  int32_t npdict;   /* distinct off-diagonal values (packed dictionary)  */
 } ed_sector_info;
 
 typedef struct ed_sector ed_sector; /* opaque */

@@ -24,7 +24,8 @@ def _e0_scipy(csr, dim):
     return float(sla.eigsh(A, k=1, which="SA", tol=1e-14)[0][0])
 
 
-@pytest.mark.parametrize("persist", ["default", "l2", "multi"], ids=["persistent", "persist_l2", "multikernel"])
+@pytest.mark.parametrize("persist", ["default", "l2", "lds", "multi"],
+                         ids=["persistent", "persist_l2", "persist_lds", "multikernel"])
 @pytest.mark.parametrize("name,factory,sectors", CASES, ids=[c[0] for c in CASES])
 def test_tridiag_and_ground_state(name, factory, sectors, persist, monkeypatch):
     """Every device recurrence: the one-workgroup persistent kernel (default for
@@ -37,6 +38,8 @@ def test_tridiag_and_ground_state(name, factory, sectors, persist, monkeypatch):
         monkeypatch.setenv("ED_GPU_NO_PERSIST", "1")
     elif persist == "l2":
         monkeypatch.setenv("ED_GPU_PERSIST_STORED", "1")
+    elif persist == "lds":
+        monkeypatch.setenv("ED_GPU_NO_PREG", "1")        # Kronecker tables in LDS (MODE 1)
 
     cfg = factory()
     orc = Oracle(cfg)
@@ -81,7 +84,7 @@ def test_real_lanczos_c2():
         assert abs(e1 - e0) <= 1e-10 * abs(e0)
 
 
-@pytest.mark.parametrize("path", ["stored_l2", "stored_reg", "kron"])
+@pytest.mark.parametrize("path", ["stored_l2", "stored_reg", "kron_lds", "kron_reg"])
 def test_persistent_matches_multikernel(path, monkeypatch):
     """Same start vector, same sector: the two recurrences agree step by step
     (first 40 steps to 1e-9; only the reduction order differs)."""
@@ -89,11 +92,13 @@ def test_persistent_matches_multikernel(path, monkeypatch):
     from cases import c2
 
     cfg = c2()
-    kw = dict(stored=False, direct=True) if path == "kron" else dict(stored=True)
+    kw = dict(stored=False, direct=True) if path.startswith("kron") else dict(stored=True)
     if path == "stored_l2":
         monkeypatch.setenv("ED_GPU_PERSIST_STORED", "1")
+    if path == "kron_lds":
+        monkeypatch.setenv("ED_GPU_NO_PREG", "1")
     with Sector(cfg, 4, 4, real=True, **kw) as S:
-        want = {"stored_l2": 0, "stored_reg": 2, "kron": 1}[path]
+        want = {"stored_l2": 0, "stored_reg": 2, "kron_lds": 1, "kron_reg": 3}[path]
         assert S.lanc_mode(real=True) == want
         v0 = np.sin(np.arange(1, S.dim + 1, dtype=np.float64))
         a1, b1, n1 = S.lanc_tridiag(v0, 60)

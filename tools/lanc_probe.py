@@ -24,11 +24,11 @@ cases = [
     ("c4 real", make_config(Norb=2, Nbath=5, bath="random"), (6, 6), True),
 ]
 MODES = {"stored": [("reg", {}), ("l2", {"ED_GPU_PERSIST_STORED": "1"}), ("multi", {"ED_GPU_NO_PERSIST": "1"})],
-         "direct": [("persist", {}), ("multi", {"ED_GPU_NO_PERSIST": "1"})]}
+         "direct": [("reg", {}), ("lds", {"ED_GPU_NO_PREG": "1"}), ("multi", {"ED_GPU_NO_PERSIST": "1"})]}
 for name, cfg, q, real in cases:
     for kind in ("stored", "direct"):
         for label, env in MODES[kind]:
-            for k in ("ED_GPU_PERSIST_STORED", "ED_GPU_NO_PERSIST"):
+            for k in ("ED_GPU_PERSIST_STORED", "ED_GPU_NO_PERSIST", "ED_GPU_NO_PREG"):
                 os.environ.pop(k, None)
             os.environ.update(env)
             with Sector(cfg, q[0], q[1], stored=kind == "stored", direct=kind == "direct", real=real) as S:

@@ -24,16 +24,17 @@ SECTORS = {
 ap = argparse.ArgumentParser()
 ap.add_argument("--sector", default="n28")
 ap.add_argument("--path", type=int, default=0)
-ap.add_argument("--complex", action="store_true")
+ap.add_argument("--complex", action="store_true", help="complex(8) H values (and vectors)")
+ap.add_argument("--cvec", action="store_true", help="real H, complex vectors")
 ap.add_argument("--iters", type=int, default=20)
 a = ap.parse_args()
 kw, q = SECTORS[a.sector]
 cfg = make_config(bath="random", seed=20251015, **kw)
 real = not a.complex
 with Sector(cfg, q[0], q[1], stored=(a.path == 0), direct=(a.path != 0), real=real) as S:
-    dt = torch.float64 if real else torch.complex128
+    dt = torch.float64 if (real and not a.cvec) else torch.complex128
     i = torch.arange(1, S.dim + 1, dtype=torch.float64, device="cuda")
-    x = torch.sin(i) if real else torch.complex(torch.sin(i), torch.cos(3 * i))
+    x = torch.sin(i) if dt == torch.float64 else torch.complex(torch.sin(i), torch.cos(3 * i))
     x = x.to(dt).contiguous()
     y = torch.empty_like(x)
     st = torch.cuda.current_stream()
@@ -47,4 +48,4 @@ with Sector(cfg, q[0], q[1], stored=(a.path == 0), direct=(a.path != 0), real=re
     e1.synchronize()
     ms = e0.elapsed_time(e1) / a.iters
     print(f"sector={a.sector} dim={S.dim} nnz={S.nnz} padded={S.info.padded} path={a.path} "
-          f"real={real} ms/launch={ms:.5f}")
+          f"real={real} cvec={a.cvec} packed={S.info.packed} ndict={S.info.npdict} ms/launch={ms:.5f}")
