@@ -242,8 +242,12 @@ def main():
             cfg28 = make_config(Norb=1, Nbath=13, bath="random", seed=20251015)
             inf28 = {}
             dim28, nnz28, ms28 = measure_spmv(Sector, cfg28, (7, 7), 50, info=inf28)
-            Bref = spmv_bytes_real(nnz28, dim28)
-            B = spmv_bytes_packed(inf28["padded"], dim28) if inf28["packed"] else Bref
+            # achieved: SURVEY §8(d)'s algorithmic bytes for this unit (real(8) CSR
+            # stored SpMV).  The packed form moves fewer bytes, so this may exceed
+            # the physical rate; `traffic` is the PMC-measured HBM
+            # side and own_format_bytes the packed kernel's own algorithmic bytes.
+            B = spmv_bytes_real(nnz28, dim28)
+            Bown = spmv_bytes_packed(inf28["padded"], dim28) if inf28["packed"] else B
             ach = B / (ms28 * 1e-3) / 1e9
             traffic, tsrc = None, None
             tfile = os.path.join(ROOT, "profiles", "r1", "spmv_n28_traffic.json")
@@ -257,14 +261,16 @@ def main():
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
                     "traffic_source": tsrc,
+                    "achieved_basis": "SURVEY §8(d) real(8) stored SpMV bytes 12*nnz+8*(dim+1)+16*dim",
                     "kernel": ("k_spmv_pk<real> (stored SELL-64, 32-bit {col|value index} words, "
                                f"{inf28['npdict']}-value dictionary)") if inf28["packed"]
                               else "k_spmv<real,real> (stored SELL-64 H·v)",
                     "workload": f"Nlevels=28 Norb=1 Nbath=13 (7,7) sector, dim {dim28}, nnz {nnz28}, "
                                 f"real(8), {B} algorithmic bytes/launch",
                     "ms_per_launch": round(ms28, 4),
-                    "reference_csr_bytes": Bref,
-                    "reference_csr_equivalent_gbs": round(Bref / (ms28 * 1e-3) / 1e9, 1)}
+                    "own_format_bytes": Bown,
+                    "own_format_gbs": round(Bown / (ms28 * 1e-3) / 1e9, 1),
+                    "physical_gbs": round(traffic / (ms28 * 1e-3) / 1e9, 1) if traffic else None}
         cpu = None if args.no_cpu else cpu_baseline()
         out = {
             "metric": "Lanczos SpMV GB/s + ground-state iters/s, Ns=16 half-filled sector, 1/2/4/8 GPU",

@@ -496,14 +496,15 @@ __global__ void __launch_bounds__(kBlock) k_spmv(const val_t<HC>* __restrict__ d
                                                  const int32_t* __restrict__ cols,
                                                  const val_t<HC>* __restrict__ vals,
                                                  const val_t<VC>* __restrict__ x, int64_t dim,
-                                                 int64_t nslice, Epi epi) {
+                                                 int64_t nslice, Epi epi, int xcd) {
   using V = val_t<VC>;
   using H = val_t<HC>;
   if (epi.skip()) return;
   epi.prepare();
   double part = 0.0;
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nslice * 64;
-       i += (int64_t)gridDim.x * kBlock) {
+  int64_t b = blockIdx.x;
+  if (xcd) b = (b & 7) * (gridDim.x >> 3) + (b >> 3);  // one row range per XCD (see k_spmv_pk)
+  for (int64_t i = b * kBlock + threadIdx.x; i < nslice * 64; i += (int64_t)gridDim.x * kBlock) {
     if (i < dim) {
       const int64_t s = i >> 6;
       const int64_t s0 = sptr[s];
@@ -600,13 +601,21 @@ __global__ void __launch_bounds__(kBlock) k_spmv_pk(const double* __restrict__ d
                                                     const uint32_t* __restrict__ words,
                                                     const double* __restrict__ dict,
                                                     const val_t<VC>* __restrict__ x, int64_t dim,
-                                                    int64_t nslice, Epi epi) {
+                                                    int64_t nslice, Epi epi, int xcd) {
   using V = val_t<VC>;
   if (epi.skip()) return;
   epi.prepare();
   double part = 0.0;
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nslice * 64;
-       i += (int64_t)gridDim.x * kBlock) {
+  // xcd: blocks are dealt round-robin to the 8 XCDs; remap so that each XCD
+  // sweeps one contiguous range of rows (its L2 then serves the v gathers
+  // shared by neighbouring rows)
+  int64_t b = blockIdx.x;
+  if (xcd) b = (b & 7) * (gridDim.x >> 3) + (b >> 3);
+  // dictionary in LDS: its lookups leave the vector-memory pipe to the gathers
+  __shared__ double sdict[256];
+  sdict[threadIdx.x] = dict[threadIdx.x];  // kBlock == 256 == dictionary capacity
+  __syncthreads();
+  for (int64_t i = b * kBlock + threadIdx.x; i < nslice * 64; i += (int64_t)gridDim.x * kBlock) {
     if (i < dim) {
       const int64_t s = i >> 6;
       const int64_t s0 = sptr[s];
@@ -623,7 +632,7 @@ __global__ void __launch_bounds__(kBlock) k_spmv_pk(const double* __restrict__ d
 #pragma unroll
         for (int k = 0; k < kChunk; k++) {
           g[k] = x[c[k] & kPackColMask];
-          h[k] = dict[c[k] >> kPackShift];
+          h[k] = sdict[c[k] >> kPackShift];
         }
 #pragma unroll
         for (int k = 0; k < kChunk; k++)
