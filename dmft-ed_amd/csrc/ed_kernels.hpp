@@ -43,6 +43,16 @@ __device__ __forceinline__ double2 mul(double h, double2 x) { return make_double
 __device__ __forceinline__ double2 mul(double2 h, double2 x) {
   return make_double2(h.x * x.x - h.y * x.y, h.x * x.y + h.y * x.x);
 }
+// acc + h*x with fused multiply-adds (persistent register paths only: the
+// stored/direct H·v kernels keep separate mul/add for bit-parity with the
+// oracle's spMatVec_cc)
+__device__ __forceinline__ double fmac(double acc, double h, double x) { return __fma_rn(h, x, acc); }
+__device__ __forceinline__ double2 fmac(double2 acc, double h, double2 x) {
+  return make_double2(__fma_rn(h, x.x, acc.x), __fma_rn(h, x.y, acc.y));
+}
+__device__ __forceinline__ double2 fmac(double2 acc, double2 h, double2 x) {
+  return make_double2(__fma_rn(-h.y, x.y, __fma_rn(h.x, x.x, acc.x)), __fma_rn(h.y, x.x, __fma_rn(h.x, x.y, acc.y)));
+}
 __device__ __forceinline__ double add(double a, double b) { return a + b; }
 __device__ __forceinline__ double2 add(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ double sub(double a, double b) { return a - b; }

@@ -1829,6 +1829,14 @@ int ed_gpu_lanc_eigh(int32_t nitermax, double threshold, int32_t ncheck, double*
   return ed_sector_lanc_eigh(g_cur, 1, nullptr, nitermax, threshold, ncheck, egs, vect, nlanc);
 }
 
+int ed_gpu_eigh(int32_t neigen, int32_t nblock, int32_t nitermax, double tol, const double* v0,
+                double* evals, double* evecs, int32_t* nconv) {
+  if (!g_cur) return fail(ED_ERR_STATE, "no current sector");
+  const int64_t dim = g_cur->dim;
+  const int ncv = (int)std::min<int64_t>(std::min(std::max(nblock, neigen + 1), 64), dim);
+  return ed_sector_eigh(g_cur, 1, neigen, ncv, nitermax, tol, v0, evals, evecs, nconv, nullptr);
+}
+
 int ed_gpu_lanc_tridiag(const double* v0, int32_t nitermax, double threshold, double* alfa,
                         double* beta, int32_t* nlanc) {
   if (!g_cur) return fail(ED_ERR_STATE, "no current sector");

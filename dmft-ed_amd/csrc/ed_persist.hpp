@@ -278,7 +278,7 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC>* __res
           for (int e = 0; e < E; e++) {
             const uint32_t x = pk[r * E + e];
             const H h = *(const H*)(dct + ((x >> kPkColBits) & kPkOffMask));
-            acc = add(acc, mul(h, vl[x & kPkColMask]));
+            acc = fmac(acc, h, vl[x & kPkColMask]);
           }
         } else {
           const int du = (int)a.K.dimup, dd = (int)a.K.dimdw;

@@ -32,11 +32,11 @@ program ed_gpu_driver
   type(ed_params_t)        :: p
   integer                  :: Norb, Nbath, nup, ndw, Nspin, i, Nh, nlanc_h
   integer(c_int64_t)       :: dim8
-  integer(c_int32_t)       :: flags, nlanc, vecdim, ng
+  integer(c_int32_t)       :: flags, nlanc, vecdim, ng, nconv
   character(len=32)        :: arg
   real(8)                  :: Uloc(3), de, hw, e0_host, e0_dev, resid
-  real(8), allocatable     :: e(:,:,:), v(:,:,:), alfa(:), beta(:), a_h(:), b_h(:)
-  complex(8), allocatable  :: impHloc(:,:,:,:), vect(:), hv(:), vin(:)
+  real(8), allocatable     :: e(:,:,:), v(:,:,:), alfa(:), beta(:), a_h(:), b_h(:), eval6(:)
+  complex(8), allocatable  :: impHloc(:,:,:,:), vect(:), hv(:), vin(:), evec6(:,:)
   logical                  :: direct
 
   call get_command_argument(1, arg) ; read(arg,*) Norb
@@ -109,6 +109,14 @@ program ed_gpu_driver
   allocate(alfa(50), beta(50))
   call ed_gpu_check(ed_gpu_lanc_tridiag(vect, 50_c_int32_t, 1d-13, alfa, beta, ng), "sp_lanc_tridiag")
   write(*,"(A,F20.12,A,I0)") "ALFA1=", alfa(1), " NTRI=", ng
+
+  ! --- sp_eigh (ED_DIAG.f90:145-167): Neigen=6, Nblock=23, tol=1e-12 on the device
+  allocate(eval6(6), evec6(vecdim, 6))
+  call ed_gpu_check(ed_gpu_eigh(6_c_int32_t, 23_c_int32_t, 512_c_int32_t, 1d-12, vin, eval6, evec6, nconv), &
+       "sp_eigh")
+  call spHtimesV_cc(vecdim, evec6(:,1), hv)
+  write(*,"(A,F20.12,A,F20.12,A,I0,A,ES10.3)") "EIG1=", eval6(1), " EIG6=", eval6(6), " NCONV=", nconv, &
+       " EIGRES=", sqrt(sum(abs(hv - eval6(1)*evec6(:,1))**2))
 
   call ed_gpu_check(ed_gpu_delete_sector(), "delete_Hv_sector")
   call ed_gpu_check(ed_gpu_finalize(), "finalize")

@@ -79,6 +79,17 @@ module ED_GPU_HXV
        real(c_double), intent(out) :: alfa(*), beta(*)
        integer(c_int32_t), intent(out) :: nlanc
      end function ed_gpu_lanc_tridiag
+     ! sp_eigh (ARPACK, ED_DIAG.f90:145-167) on the device
+     integer(c_int) function ed_gpu_eigh(neigen, nblock, nitermax, tol, v0, evals, evecs, nconv) &
+          bind(C, name="ed_gpu_eigh")
+       import :: c_int, c_int32_t, c_double, c_double_complex
+       integer(c_int32_t), value :: neigen, nblock, nitermax
+       real(c_double), value :: tol
+       complex(c_double_complex), intent(in) :: v0(*)
+       real(c_double), intent(out) :: evals(*)
+       complex(c_double_complex), intent(out) :: evecs(*)
+       integer(c_int32_t), intent(out) :: nconv
+     end function ed_gpu_eigh
      integer(c_int) function ed_gpu_delete_sector() bind(C, name="ed_gpu_delete_sector")
        import :: c_int
      end function ed_gpu_delete_sector
@@ -95,7 +106,7 @@ module ED_GPU_HXV
   end interface
 
   public :: ed_gpu_init, ed_gpu_set_device, ed_gpu_build_sector, ed_gpu_vecdim, ed_gpu_hxv
-  public :: ed_gpu_lanc_eigh, ed_gpu_lanc_tridiag, ed_gpu_delete_sector, ed_gpu_finalize
+  public :: ed_gpu_lanc_eigh, ed_gpu_lanc_tridiag, ed_gpu_eigh, ed_gpu_delete_sector, ed_gpu_finalize
   public :: gpuMatVec_cc
   public :: ed_gpu_check
   public :: ed_gpu_pack_params

@@ -32,6 +32,7 @@
  *                                (row-of-arrays order of sp_insert_element :249-320)
  *   ed_gpu_lanc_eigh          <- sp_lanc_eigh (SciFortran; spec .repo/PLAIN_LANCZOS.f90:286-385)
  *   ed_gpu_lanc_tridiag       <- sp_lanc_tridiag (SciFortran; spec .repo/PLAIN_LANCZOS.f90:154-180)
+ *   ed_gpu_eigh               <- sp_eigh (ARPACK; called at ED_DIAG.f90:145-167)
  */
 #ifndef ED_GPU_H
 #define ED_GPU_H
@@ -216,6 +217,13 @@ int ed_gpu_hxv(const int32_t* nloc, const double* v, double* hv);
 int ed_gpu_dump_csr(int64_t* rowptr, int32_t* cols, double* vals);
 int ed_gpu_lanc_eigh(int32_t nitermax, double threshold, int32_t ncheck, double* egs,
                      double* vect, int32_t* nlanc);
+/* sp_eigh(spHtimesV_cc, eig_values, eig_basis, Nblock, Nitermax, tol)
+ * (ED_DIAG.f90:145-167, ARPACK which="SR"): device thick-restart Lanczos on
+ * the current sector, complex(8) vectors.  v0 (dim, complex) or NULL;
+ * evals[neigen] ascending; evecs complex(8) (dim x neigen, column-major) or
+ * NULL; nconv converged pairs. */
+int ed_gpu_eigh(int32_t neigen, int32_t nblock, int32_t nitermax, double tol, const double* v0,
+                double* evals, double* evecs, int32_t* nconv);
 int ed_gpu_lanc_tridiag(const double* v0, int32_t nitermax, double threshold,
                         double* alfa, double* beta, int32_t* nlanc);
 int ed_gpu_delete_sector(void);

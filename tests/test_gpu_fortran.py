@@ -33,6 +33,11 @@ def test_fortran_driver_c2(mode):
     assert abs(float(v["E0_DEV"]) - float(v["E0_HOST"])) < 1e-9
     assert float(v["RESID"]) < 1e-5
     assert abs(float(v["ALFA1"]) - float(v["E0_DEV"])) < 1e-9   # <gs|H|gs> = E0
+    # sp_eigh replacement: 6 lowest, converged, ground state equals the Lanczos one
+    assert int(v["NCONV"]) == 6
+    assert abs(float(v["EIG1"]) - float(v["E0_DEV"])) < 1e-9
+    assert float(v["EIG6"]) >= float(v["EIG1"])
+    assert float(v["EIGRES"]) < 1e-8
 
 
 def test_fortran_driver_error_is_loud():
