@@ -119,9 +119,19 @@ struct ed_sector {
   bool g_basis = false;
 };
 
+// All device memory and copies of a sector are ordered on its private stream
+// (stream-ordered allocator, async copies + a stream sync): no call here
+// synchronises the device or the null stream, so sectors can be built,
+// solved (graph capture included) and freed from several host threads at
+// once (farm workers).
+static int dcopy(const ed_sector* s, void* dst, const void* src, size_t n, hipMemcpyKind k) {
+  HIPCK(hipMemcpyAsync(dst, src, n, k, s->stream));
+  HIPCK(hipStreamSynchronize(s->stream));
+  return ED_OK;
+}
 static int dalloc(ed_sector* s, void** p, size_t n) {
   if (n == 0) n = 16;
-  hipError_t e = hipMalloc(p, n);
+  hipError_t e = hipMallocAsync(p, n, s->stream);
   if (e != hipSuccess) {
     *p = nullptr;
     return fail(e == hipErrorOutOfMemory ? ED_ERR_OOM : ED_ERR_HIP,
@@ -135,7 +145,7 @@ static void dfree(ed_sector* s, void** p, size_t n) {
   if (!*p) return;
   auto it = std::find(s->allocs.begin(), s->allocs.end(), *p);
   if (it != s->allocs.end()) s->allocs.erase(it);
-  (void)hipFree(*p);
+  (void)hipFreeAsync(*p, s->stream);
   s->bytes -= (int64_t)n;
   *p = nullptr;
 }
@@ -146,16 +156,18 @@ static int dalloc_t(ed_sector* s, T** p, size_t count) {
 template <class T>
 static int upload(ed_sector* s, T** p, const std::vector<T>& h) {
   CK(dalloc_t(s, p, h.size()));
-  HIPCK(hipMemcpy(*p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
-  return ED_OK;
+  return dcopy(s, *p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice);
 }
 
 static void sector_free(ed_sector* s) {
   if (!s) return;
   (void)hipSetDevice(s->device);
   if (s->gexec) (void)hipGraphExecDestroy(s->gexec);
-  for (void* p : s->allocs) (void)hipFree(p);
-  if (s->stream) (void)hipStreamDestroy(s->stream);
+  if (s->stream) {
+    for (void* p : s->allocs) (void)hipFreeAsync(p, s->stream);
+    (void)hipStreamSynchronize(s->stream);
+    (void)hipStreamDestroy(s->stream);
+  }
   delete s;
 }
 
@@ -168,13 +180,13 @@ static int build_pack(ed_sector* s) {
   unsigned long long* table;
   unsigned int* ovf;
   uint8_t* tidx;
-  HIPCK(hipMalloc((void**)&table, kDictTable * 8));
-  HIPCK(hipMalloc((void**)&ovf, 4));
-  HIPCK(hipMalloc((void**)&tidx, kDictTable));
+  HIPCK(hipMallocAsync((void**)&table, kDictTable * 8, s->stream));
+  HIPCK(hipMallocAsync((void**)&ovf, 4, s->stream));
+  HIPCK(hipMallocAsync((void**)&tidx, kDictTable, s->stream));
   auto cleanup = [&]() {
-    (void)hipFree(table);
-    (void)hipFree(ovf);
-    (void)hipFree(tidx);
+    (void)hipFreeAsync(table, s->stream);
+    (void)hipFreeAsync(ovf, s->stream);
+    (void)hipFreeAsync(tidx, s->stream);
   };
   HIPCK(hipMemsetAsync(table, 0xFF, kDictTable * 8, s->stream));
   HIPCK(hipMemsetAsync(ovf, 0, 4, s->stream));
@@ -225,10 +237,10 @@ static int build_stored(ed_sector* s) {
   CK(dalloc_t(s, &cnt, dim));
   s->d_cnt = cnt;
   // width/bsum/total are scratch, freed right after the build
-  HIPCK(hipMalloc((void**)&width, ns * sizeof(int32_t)));
+  HIPCK(hipMallocAsync((void**)&width, ns * sizeof(int32_t), s->stream));
   int64_t nb = (ns + 1023) / 1024;
-  HIPCK(hipMalloc((void**)&bsum, std::max<int64_t>(nb, 1) * sizeof(int64_t)));
-  HIPCK(hipMalloc((void**)&total, sizeof(int64_t)));
+  HIPCK(hipMallocAsync((void**)&bsum, std::max<int64_t>(nb, 1) * sizeof(int64_t), s->stream));
+  HIPCK(hipMallocAsync((void**)&total, sizeof(int64_t), s->stream));
   CK(dalloc_t(s, &s->d_sptr, ns + 1));
   hipLaunchKernelGGL(k_count, dim3(grid_for(ns * 64)), dim3(kBlock), 0, s->stream, s->Md, s->d_map,
                      dim, ns, cnt, width);
@@ -242,9 +254,9 @@ static int build_stored(ed_sector* s) {
   int64_t slots = 0;
   HIPCK(hipMemcpyAsync(&slots, total, sizeof(int64_t), hipMemcpyDeviceToHost, s->stream));
   HIPCK(hipStreamSynchronize(s->stream));
-  (void)hipFree(width);
-  (void)hipFree(bsum);
-  (void)hipFree(total);
+  (void)hipFreeAsync(width, s->stream);
+  (void)hipFreeAsync(bsum, s->stream);
+  (void)hipFreeAsync(total, s->stream);
   s->padded = slots;
   const size_t hv = s->hc ? 16 : 8;
   CK(dalloc(s, &s->d_diag, dim * hv));
@@ -369,9 +381,9 @@ static int build_kron(ed_sector* s) {
     uint8_t* di;
     CK(upload(s, &dc, cols));
     CK(dalloc(s, &dv, vals.size() * 8));
-    HIPCK(hipMemcpy(dv, vals.data(), vals.size() * 8, hipMemcpyHostToDevice));
+    CK(dcopy(s, dv, vals.data(), vals.size() * 8, hipMemcpyHostToDevice));
     CK(dalloc(s, &da, a.size() * 8));
-    HIPCK(hipMemcpy(da, a.data(), a.size() * 8, hipMemcpyHostToDevice));
+    CK(dcopy(s, da, a.data(), a.size() * 8, hipMemcpyHostToDevice));
     CK(upload(s, &di, imp));
     if (sp == 0) {
       K.degup = deg; K.upc = dc; K.upv = dv; K.aup = da; K.impu = di;
@@ -647,10 +659,10 @@ static int build_preg(ed_sector* s) {
   std::vector<int32_t> sc(slots);
   std::vector<double> sv(slots * hw);
   HIPCK(hipStreamSynchronize(s->stream));  // SELL arrays come from kernels on s->stream
-  HIPCK(hipMemcpy(cnt.data(), s->d_cnt, dim * 2, hipMemcpyDeviceToHost));
-  HIPCK(hipMemcpy(sptr.data(), s->d_sptr, (ns + 1) * 8, hipMemcpyDeviceToHost));
-  HIPCK(hipMemcpy(sc.data(), s->d_cols, slots * 4, hipMemcpyDeviceToHost));
-  HIPCK(hipMemcpy(sv.data(), s->d_vals, slots * 8 * hw, hipMemcpyDeviceToHost));
+  CK(dcopy(s, cnt.data(), s->d_cnt, dim * 2, hipMemcpyDeviceToHost));
+  CK(dcopy(s, sptr.data(), s->d_sptr, (ns + 1) * 8, hipMemcpyDeviceToHost));
+  CK(dcopy(s, sc.data(), s->d_cols, slots * 4, hipMemcpyDeviceToHost));
+  CK(dcopy(s, sv.data(), s->d_vals, slots * 8 * hw, hipMemcpyDeviceToHost));
   int wmax = 0;
   for (int64_t i = 0; i < dim; i++) wmax = std::max<int>(wmax, cnt[i]);
   int W = 0;
@@ -687,8 +699,8 @@ static int build_preg(ed_sector* s) {
   }
   CK(dalloc(s, (void**)&s->d_pk, pk.size() * 4));
   CK(dalloc(s, &s->d_dict, dict.size() * 8));
-  HIPCK(hipMemcpy(s->d_pk, pk.data(), pk.size() * 4, hipMemcpyHostToDevice));
-  HIPCK(hipMemcpy(s->d_dict, dict.data(), dict.size() * 8, hipMemcpyHostToDevice));
+  CK(dcopy(s, s->d_pk, pk.data(), pk.size() * 4, hipMemcpyHostToDevice));
+  CK(dcopy(s, s->d_dict, dict.data(), dict.size() * 8, hipMemcpyHostToDevice));
   s->ndict = (int)(dict.size() / hw);
   s->preg_E = W;
   s->preg_rpt = RPT;
@@ -699,7 +711,7 @@ static int build_preg(ed_sector* s) {
 // or -1 when the sector does not fit one workgroup's LDS / register budget.
 static int64_t persist_lds(const ed_sector* s, int vc, int mode);
 // ELL words per lane that compile without scratch (-Rpass-analysis=kernel-resource-usage)
-constexpr int preg_cap(bool hc, bool vc) { return vc ? (hc ? 72 : 84) : 120; }
+constexpr int preg_cap(bool hc, bool vc) { return vc ? (hc ? 60 : 72) : 112; }
 static int persist_mode(ed_sector* s, int vc, int path) {
   if (getenv("ED_GPU_NO_PERSIST")) return -1;
   const int64_t vs = vc ? 16 : 8;
@@ -1067,10 +1079,10 @@ struct Trlan {
   int nhv = 0;
   ~Trlan() {
     for (auto& g : graphs) (void)hipGraphExecDestroy(g.second);
-    for (void* p : mine) (void)hipFree(p);
+    for (void* p : mine) (void)hipFreeAsync(p, st);
   }
   int alloc(void** p, size_t n) {
-    HIPCK(hipMalloc(p, n));
+    HIPCK(hipMallocAsync(p, n, st));
     mine.push_back(*p);
     return ED_OK;
   }
@@ -1294,7 +1306,7 @@ int ed_sector_create(const ed_params* p, int32_t q1, int32_t q2, int32_t flags, 
     return fail(ED_ERR_HIP, "hipStreamCreate");
   }
   TRY(dalloc_t(s, &s->Md, 1));
-  if (hipMemcpy(s->Md, &s->Mh, sizeof(EdModel), hipMemcpyHostToDevice) != hipSuccess) {
+  if (dcopy(s, s->Md, &s->Mh, sizeof(EdModel), hipMemcpyHostToDevice) != ED_OK) {
     sector_free(s);
     return fail(ED_ERR_HIP, "model upload");
   }
@@ -1396,7 +1408,7 @@ int ed_sector_hxv(ed_sector* s, int32_t nloc, const double* v, double* hv) {
 int ed_sector_map(const ed_sector* s, uint32_t* map_host) {
   if (!s || !map_host) return fail(ED_ERR_ARG, "null");
   HIPCK(hipSetDevice(s->device));
-  HIPCK(hipMemcpy(map_host, s->d_map, s->dim * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  CK(dcopy(s, map_host, s->d_map, s->dim * sizeof(uint32_t), hipMemcpyDeviceToHost));
   return ED_OK;
 }
 
@@ -1410,11 +1422,11 @@ int ed_sector_dump_csr(const ed_sector* s, int64_t* rowptr, int32_t* cols, doubl
   std::vector<int64_t> sptr(ns + 1);
   std::vector<int32_t> sc(slots);
   std::vector<double> sv(slots * hw), dg(dim * hw);
-  HIPCK(hipMemcpy(cnt.data(), s->d_cnt, dim * 2, hipMemcpyDeviceToHost));
-  HIPCK(hipMemcpy(sptr.data(), s->d_sptr, (ns + 1) * 8, hipMemcpyDeviceToHost));
-  HIPCK(hipMemcpy(sc.data(), s->d_cols, slots * 4, hipMemcpyDeviceToHost));
-  HIPCK(hipMemcpy(sv.data(), s->d_vals, slots * 8 * hw, hipMemcpyDeviceToHost));
-  HIPCK(hipMemcpy(dg.data(), s->d_diag, dim * 8 * hw, hipMemcpyDeviceToHost));
+  CK(dcopy(s, cnt.data(), s->d_cnt, dim * 2, hipMemcpyDeviceToHost));
+  CK(dcopy(s, sptr.data(), s->d_sptr, (ns + 1) * 8, hipMemcpyDeviceToHost));
+  CK(dcopy(s, sc.data(), s->d_cols, slots * 4, hipMemcpyDeviceToHost));
+  CK(dcopy(s, sv.data(), s->d_vals, slots * 8 * hw, hipMemcpyDeviceToHost));
+  CK(dcopy(s, dg.data(), s->d_diag, dim * 8 * hw, hipMemcpyDeviceToHost));
   int64_t q = 0;
   rowptr[0] = 0;
   for (int64_t i = 0; i < dim; i++) {
@@ -1518,8 +1530,8 @@ int ed_sector_lanc_run(ed_sector* s, int32_t vtype, const void* v0_dev, int32_t 
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   CK(rc);
-  if (alfa) HIPCK(hipMemcpy(alfa, s->ws.alpha, niter * sizeof(double), hipMemcpyDeviceToHost));
-  if (beta) HIPCK(hipMemcpy(beta, s->ws.beta, niter * sizeof(double), hipMemcpyDeviceToHost));
+  if (alfa) CK(dcopy(s, alfa, s->ws.alpha, niter * sizeof(double), hipMemcpyDeviceToHost));
+  if (beta) CK(dcopy(s, beta, s->ws.beta, niter * sizeof(double), hipMemcpyDeviceToHost));
   return ED_OK;
 }
 
@@ -1688,7 +1700,7 @@ int ed_sector_lanc_eigh(ed_sector* s, int32_t vtype, const void* v0, int32_t nit
   }
   if (nl == 0) {
     LancState hs;
-    HIPCK(hipMemcpy(&hs, s->ws.st, sizeof(hs), hipMemcpyDeviceToHost));
+    CK(dcopy(s, &hs, s->ws.st, sizeof(hs), hipMemcpyDeviceToHost));
     char msg[256];
     snprintf(msg, sizeof msg,
              "Lanczos made no step: iter=%d done=%d beta0=%g b[1]=%g a[0]=%g path=%d pm=%d keep=%d",

@@ -41,6 +41,9 @@ class DiagOptions:
     gs_threshold: float = 1e-9
     mpi_size: int = 1
     keep_vectors: bool = True
+    # sectors solved concurrently on one GPU (host threads, one HIP stream per
+    # sector; ctypes releases the GIL): small sectors are launch-latency bound
+    workers: int = 8
 
 
 @dataclass
@@ -141,17 +144,33 @@ def state_list(results: Iterable[SectorResult], opt: DiagOptions) -> StateList:
     return sl
 
 
+def solve_many(cfg: EDConfig, secs: List[SectorId], opt: DiagOptions, device: int = 0,
+               solver=None, cost=None) -> List[SectorResult]:
+    """Solve a list of sectors on one GPU with `opt.workers` host threads,
+    largest first; results in the order of `secs` (each sector's result does
+    not depend on the schedule)."""
+    solver = solver or solve_sector
+    if opt.workers <= 1 or len(secs) <= 1:
+        return [solver(cfg, sec, opt, device) for sec in secs]
+    from concurrent.futures import ThreadPoolExecutor
+
+    order = sorted(range(len(secs)), key=lambda i: -(cost(secs[i]) if cost else secs[i].dim))
+    out: List[Optional[SectorResult]] = [None] * len(secs)
+    with ThreadPoolExecutor(max_workers=opt.workers) as ex:
+        futs = {i: ex.submit(solver, cfg, secs[i], opt, device) for i in order}
+        for i, f in futs.items():
+            out[i] = f.result()
+    return out
+
+
 def ed_diag(cfg: EDConfig, opt: Optional[DiagOptions] = None,
             sectors: Optional[Iterable[int]] = None, device: int = 0):
     """Diagonalise all (or the given) sectors; returns (results, state_list)."""
     opt = opt or DiagOptions()
     secs = setup_pointers(cfg)
     pick = set(sectors) if sectors is not None else None
-    results: List[SectorResult] = []
-    for sec in secs:
-        if pick is not None and sec.isector not in pick:
-            continue
-        results.append(solve_sector(cfg, sec, opt, device))
+    todo = [sec for sec in secs if pick is None or sec.isector in pick]
+    results = solve_many(cfg, todo, opt, device)
     return results, state_list(results, opt)
 
 

@@ -79,7 +79,7 @@ def farm_diag(cfg: EDConfig, opt: Optional[DiagOptions] = None, *, device: int =
               solver: Optional[Callable[[EDConfig, SectorId, DiagOptions, int], SectorResult]] = None
               ) -> FarmResult:
     """ed_diag over all ranks of the default process group (or serially)."""
-    from .diag import solve_sector
+    from .diag import solve_many, solve_sector
 
     opt = opt or DiagOptions()
     solver = solver or solve_sector
@@ -90,8 +90,8 @@ def farm_diag(cfg: EDConfig, opt: Optional[DiagOptions] = None, *, device: int =
     parts = lpt_partition([sector_cost(cfg, s, opt) for s in secs], world)
     assignment = [[secs[i].isector for i in p] for p in parts]
     local: Dict[int, SectorResult] = {}
-    for i in parts[rank]:
-        r = solver(cfg, secs[i], opt, device)
+    mine = [secs[i] for i in parts[rank]]
+    for r in solve_many(cfg, mine, opt, device, solver=solver, cost=lambda s: sector_cost(cfg, s, opt)):
         local[r.isector] = r
     # gather eigenvalues (tiny) from every rank
     mine = {k: (v.q, v.dim, v.neigen, np.asarray(v.eigenvalues[: max(v.neigen, 1)])) for k, v in local.items()}
