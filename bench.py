@@ -181,8 +181,16 @@ def main():
         import torch.distributed as tdist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # rehearsal switches (not used by the driver): ED_BENCH_BACKEND=gloo and
+        # ED_BENCH_ONE_DEVICE=1 run N ranks on one GPU to exercise the N>1 flow
+        if os.environ.get("ED_BENCH_ONE_DEVICE"):
+            local = 0
         torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("ED_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            tdist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
