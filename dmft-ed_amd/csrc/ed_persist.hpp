@@ -58,7 +58,10 @@ struct PersistRun {
   int first;         // 1: R holds the unnormalised start vector
 };
 
-template <int NT = kPBlock>
+// TAIL=false drops the trailing barrier: the caller guarantees a barrier
+// between this read of ws and the next write to the same buffer (the
+// iteration alternates two buffers, separated by the step's barriers).
+template <int NT = kPBlock, bool TAIL = true>
 __device__ __forceinline__ double pblock_sum(double v, double* ws) {
   v = wave_sum(v);
   const int wv = threadIdx.x >> 6;
@@ -67,7 +70,7 @@ __device__ __forceinline__ double pblock_sum(double v, double* ws) {
   double t = 0.0;
 #pragma unroll
   for (int w = 0; w < NT / 64; w++) t = t + ws[w];
-  __syncthreads();
+  if constexpr (TAIL) __syncthreads();
   return t;
 }
 
@@ -81,6 +84,7 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC>* __res
   const PersistRun<HC>& a = runs[blockIdx.x];  // uniform: scalar loads, no VGPR copy
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ double ws[NT / 64];
+  __shared__ double ws2[NT / 64];  // beta's buffer: alpha/beta alternate, one barrier each
   V* vl = (V*)smem;  // MODE 2 moves it behind the dictionary
   const int64_t dim = a.dim;
   const int tid = threadIdx.x;
@@ -300,7 +304,9 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC>* __res
         if (basis) basis[(int64_t)it * dim + i] = xi;
       }
     }
-    const double alpha = pblock_sum<NT>(ap, ws);
+    // alpha reads ws, beta ws2; the barrier inside the beta reduction and the
+    // end-of-step barrier separate each read from the next write of its buffer
+    const double alpha = pblock_sum<NT, false>(ap, ws);
     // ---- w -= alpha v ; beta
     double bp = 0.0;
 #pragma unroll
@@ -311,7 +317,7 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC>* __res
         bp += redot(w[r], w[r]);
       }
     }
-    const double bn = sqrt(pblock_sum<NT>(bp, ws));
+    const double bn = sqrt(pblock_sum<NT, false>(bp, ws2));
     if (tid == 0) {
       alpha_out[it] = alpha;
       beta_out[it + 1] = bn;
