@@ -748,6 +748,52 @@ __global__ void __launch_bounds__(kBlock) k_kron(KronArgs<HC> K, const val_t<VC>
   epi.finish(part);
 }
 
+// ------------------------------------ within-sector split
+// H = D + Hup(x)1 + 1(x)Hdw on the DimDw x DimUp view.  A rank owning down
+// rows [w0, w0+nw) applies the diagonal and the up-spin hops locally
+// (k_kron_rows on its nw x DimUp block); the down-spin hops act along the
+// other index and run on the transposed block (k_kron_cols on nu x DimDw
+// columns it receives by an all-to-all).  Term order per element: diagonal,
+// up hops | down hops — the two partial sums are added by the caller.
+template <bool HC, bool VC>
+__global__ void __launch_bounds__(kBlock) k_kron_rows(KronArgs<HC> K, int64_t w0, int64_t nw,
+                                                      const val_t<VC>* __restrict__ x,
+                                                      val_t<VC>* __restrict__ y) {
+  using V = val_t<VC>;
+  const int64_t du = K.dimup;
+  for (int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x; q < nw * du;
+       q += (int64_t)gridDim.x * kBlock) {
+    const int64_t r = q / du, iu = q - r * du, iw = w0 + r;
+    auto d = add(add(K.aup[iu], K.adw[iw]), mk<HC>(K.uimp[K.impu[iu] * K.nimp + K.impd[iw]], 0.0));
+    V acc = mul(d, x[q]);
+    const V* xrow = x + r * du;
+    for (int k = 0; k < K.degup; k++) {
+      const int64_t t = (int64_t)k * du + iu;
+      acc = add(acc, mul(K.upv[t], xrow[K.upc[t]]));
+    }
+    y[q] = acc;
+  }
+}
+
+template <bool HC, bool VC>
+__global__ void __launch_bounds__(kBlock) k_kron_cols(KronArgs<HC> K, int64_t nu,
+                                                      const val_t<VC>* __restrict__ xt,
+                                                      val_t<VC>* __restrict__ yt, int accumulate) {
+  using V = val_t<VC>;
+  const int64_t dd = K.dimdw;
+  for (int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x; q < nu * dd;
+       q += (int64_t)gridDim.x * kBlock) {
+    const int64_t c = q / dd, iw = q - c * dd;
+    V acc = accumulate ? yt[q] : vzero<V>();
+    const V* xcol = xt + c * dd;
+    for (int k = 0; k < K.degdw; k++) {
+      const int64_t t = (int64_t)k * dd + iw;
+      acc = add(acc, mul(K.dwv[t], xcol[K.dwc[t]]));
+    }
+    yt[q] = acc;
+  }
+}
+
 // ------------------------------------------------ GF seeds: c / c^+ |state>
 // One thread per source row; every target row is hit at most once (the
 // operator is injective on the Fock basis), so plain stores suffice.

@@ -1252,6 +1252,37 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
   return ED_OK;
 }
 
+template <bool HC, bool VC>
+static int kron_split_launch(ed_sector* s, int part, int64_t o, int64_t n, const void* x, void* y, int acc,
+                             hipStream_t st) {
+  using V = val_t<VC>;
+  const int64_t cnt = n * (part == 0 ? s->K.dimup : s->K.dimdw);
+  if (cnt == 0) return ED_OK;
+  if (part == 0)
+    hipLaunchKernelGGL((k_kron_rows<HC, VC>), dim3(grid_for(cnt)), dim3(kBlock), 0, st, kron_args<HC>(s), o, n,
+                       (const V*)x, (V*)y);
+  else
+    hipLaunchKernelGGL((k_kron_cols<HC, VC>), dim3(grid_for(cnt)), dim3(kBlock), 0, st, kron_args<HC>(s), n,
+                       (const V*)x, (V*)y, acc);
+  HIPCK(hipGetLastError());
+  return ED_OK;
+}
+
+static int kron_split(ed_sector* s, int part, int32_t vtype, int64_t o, int64_t n, const void* x, void* y,
+                      int acc, void* stream) {
+  if (!s || !x || !y) return fail(ED_ERR_ARG, "null");
+  if (!s->kron) return fail(ED_ERR_UNSUPPORTED, "sector has no Kronecker form (normal mode without Jx/Jp, ED_DIRECT)");
+  const int64_t lim = part == 0 ? s->K.dimdw : s->K.dimup;
+  if (o < 0 || n < 0 || o + n > lim) return fail(ED_ERR_ARG, "row/column range outside the factor dimension");
+  if (vtype != 0 && vtype != 1) return fail(ED_ERR_ARG, "vtype must be 0 (real) or 1 (complex)");
+  if (vtype == 0 && s->hc) return fail(ED_ERR_ARG, "complex H needs vtype=1");
+  HIPCK(hipSetDevice(s->device));
+  hipStream_t st = (hipStream_t)stream;
+  if (s->hc) return kron_split_launch<true, true>(s, part, o, n, x, y, acc, st);
+  return vtype ? kron_split_launch<false, true>(s, part, o, n, x, y, acc, st)
+               : kron_split_launch<false, false>(s, part, o, n, x, y, acc, st);
+}
+
 // ---------------------------------------------------------------- C-ABI
 extern "C" {
 
@@ -1383,6 +1414,16 @@ int ed_sector_hxv_dev_path(ed_sector* s, int32_t path, int32_t vtype, const void
     return launch_hxv<false>(s, pth, v, e, st);
   }
   return fail(ED_ERR_ARG, "vtype must be 0 (real) or 1 (complex)");
+}
+
+int ed_sector_kron_rows(ed_sector* s, int32_t vtype, int64_t w0, int64_t nw, const void* x, void* y,
+                        void* stream) {
+  return kron_split(s, 0, vtype, w0, nw, x, y, 0, stream);
+}
+
+int ed_sector_kron_cols(ed_sector* s, int32_t vtype, int64_t u0, int64_t nu, const void* xt, void* yt,
+                        int32_t accumulate, void* stream) {
+  return kron_split(s, 1, vtype, u0, nu, xt, yt, accumulate, stream);
 }
 
 int ed_sector_hxv_dev(ed_sector* s, int32_t vtype, const void* v, void* hv, void* stream) {

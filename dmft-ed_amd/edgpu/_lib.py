@@ -34,6 +34,8 @@ SIGNATURES = {
     "ed_sector_lanc_run": ([_P, _i32, _P, _i32, _P, _P, _P, _P], ctypes.c_int),
     "ed_sector_lanc_mode": ([_P, _i32, _i32], ctypes.c_int),
     "ed_gpu_eigh": ([_i32, _i32, _i32, _f64, _P, _P, _P, _P], ctypes.c_int),
+    "ed_sector_kron_rows": ([_P, _i32, _i64, _i64, _P, _P, _P], ctypes.c_int),
+    "ed_sector_kron_cols": ([_P, _i32, _i64, _i64, _P, _P, _i32, _P], ctypes.c_int),
     "ed_sector_eigh": ([_P, _i32, _i32, _i32, _i32, _f64, _P, _P, _P, _P, _P], ctypes.c_int),
     "ed_sector_sell_view": ([_P, _P], ctypes.c_int),
     "ed_sector_apply_op": ([_P, _P, _i32, _i32, _i32, _P, _P, _P], ctypes.c_int),

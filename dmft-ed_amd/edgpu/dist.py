@@ -1,0 +1,258 @@
+"""Within-sector multi-GPU H·v.
+
+The reference splits one sector's rows over MPI ranks and all-gathers the
+whole vector before every product (ED_HAMILTONIAN.f90:55-62,
+ED_HAMILTONIAN_STORED_HxV.f90:147-197: spMatVec_mpi_cc).  For the normal-mode
+Hamiltonian without Jx/Jp the sector factorises,
+
+    H = D + Hup (x) 1 + 1 (x) Hdw      on the DimDw x DimUp view of v,
+
+so a rank that owns down rows [w0, w0+nw) applies D and the up-spin hops to
+its own block, and the down-spin hops — which mix rows — run on the
+transposed view, where each rank owns up columns [u0, u0+nu):
+
+    y  = rows(x)                                  ed_sector_kron_rows (HIP)
+    xt = transpose(x)                             all_to_all over RCCL/xGMI
+    yt = cols(xt)                                 ed_sector_kron_cols (HIP)
+    y += transpose(yt)                            all_to_all
+
+Each H·v moves 2·(P-1)/P of the local block per rank instead of the
+reference's full-vector Allgatherv (P·x the local block), and every rank
+holds only its 1/P of v.  `dist_lanczos` runs the plain recurrence
+(.repo/PLAIN_LANCZOS.f90:87-118) on the split vector with two all-reduces of
+scalars per step.
+
+The collective backend is the default process group (nccl = RCCL on the GPU
+box; gloo in the CPU tests, where `ops` injects reference factor products).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import check
+
+
+def _dist():
+    try:
+        import torch.distributed as dist
+
+        if dist.is_available() and dist.is_initialized():
+            return dist
+    except Exception:
+        pass
+    return None
+
+
+def split(n: int, parts: int) -> Tuple[List[int], List[int]]:
+    """Contiguous near-even split: (starts, counts)."""
+    base, extra = divmod(n, parts)
+    counts = [base + (1 if p < extra else 0) for p in range(parts)]
+    starts = [int(x) for x in np.concatenate([[0], np.cumsum(counts)[:-1]])]
+    return starts, counts
+
+
+class DeviceKronOps:
+    """The two factor products on the GPU (ed_sector_kron_rows / _cols)."""
+
+    def __init__(self, S):
+        self.S = S
+        self.dimup = int(S.info.dimup)
+        self.dimdw = int(S.info.dimdw)
+
+    def _args(self, x, y):
+        import torch
+
+        st = torch.cuda.current_stream(x.device)
+        return ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(y.data_ptr()), ctypes.c_void_p(st.cuda_stream)
+
+    def rows(self, w0: int, nw: int, x):
+        import torch
+
+        y = torch.empty_like(x)
+        xp, yp, sp = self._args(x, y)
+        vt = 1 if x.is_complex() else 0
+        check(_lib.load().ed_sector_kron_rows(self.S.handle, vt, w0, nw, xp, yp, sp), "ed_sector_kron_rows")
+        return y
+
+    def cols(self, u0: int, nu: int, xt):
+        import torch
+
+        yt = torch.empty_like(xt)
+        xp, yp, sp = self._args(xt, yt)
+        vt = 1 if xt.is_complex() else 0
+        check(_lib.load().ed_sector_kron_cols(self.S.handle, vt, u0, nu, xp, yp, 0, sp), "ed_sector_kron_cols")
+        return yt
+
+
+class DistKronSector:
+    """One sector split by down rows over the ranks of the default process
+    group (or serial).  Vectors are 1-D torch tensors holding this rank's
+    nw x DimUp block (row-major = the reference's row order)."""
+
+    def __init__(self, cfg=None, q1: int = 0, q2: int = 0, *, device: int = 0, real: Optional[bool] = None,
+                 ops=None):
+        import torch
+
+        dist = _dist()
+        self.rank = dist.get_rank() if dist else 0
+        self.world = dist.get_world_size() if dist else 1
+        self._S = None
+        if ops is None:
+            from .hamiltonian import Sector
+
+            real = cfg.is_real() if real is None else real
+            self._S = Sector(cfg, q1, q2, stored=False, direct=True, real=real, device=device)
+            if not self._S.info.kron:
+                self._S.close()
+                raise ValueError("within-sector split needs the Kronecker form (normal mode, no Jx/Jp)")
+            ops = DeviceKronOps(self._S)
+            self.dtype = torch.float64 if real else torch.complex128
+            self.device = torch.device("cuda", device)
+        else:
+            self.dtype = getattr(ops, "dtype", torch.complex128)
+            self.device = getattr(ops, "device", torch.device("cpu"))
+        self.ops = ops
+        self.du, self.dd = ops.dimup, ops.dimdw
+        self.w0, self.nw = split(self.dd, self.world)
+        self.u0, self.nu = split(self.du, self.world)
+        self.comm_cpu = dist is not None and dist.get_backend() != "nccl"
+
+    # ------------------------------------------------------------- layout
+    @property
+    def local_rows(self) -> Tuple[int, int]:
+        return self.w0[self.rank], self.nw[self.rank]
+
+    @property
+    def local_dim(self) -> int:
+        return self.nw[self.rank] * self.du
+
+    def scatter(self, v_full):
+        """This rank's block of a full vector (tests, start vectors)."""
+        w0, nw = self.local_rows
+        return v_full[w0 * self.du:(w0 + nw) * self.du].contiguous()
+
+    def gather(self, v_loc):
+        """Full vector on every rank (tests only: the point is not to need it)."""
+        import torch
+
+        dist = _dist()
+        if dist is None:
+            return v_loc
+        m = max(self.nw) * self.du           # equal-size all_gather (gloo needs it): pad
+        pad = torch.zeros(m, dtype=v_loc.dtype, device=v_loc.device)
+        pad[:v_loc.numel()] = v_loc
+        parts = [torch.empty(m, dtype=v_loc.dtype, device=v_loc.device) for _ in self.nw]
+        if self.comm_cpu:
+            cpu = [p.cpu() for p in parts]
+            dist.all_gather(cpu, pad.cpu())
+            parts = [p.to(v_loc.device) for p in cpu]
+        else:
+            dist.all_gather(parts, pad)
+        parts = [p[:n * self.du] for p, n in zip(parts, self.nw)]
+        return torch.cat(parts)
+
+    # ------------------------------------------------------ communication
+    def _a2a(self, send, in_splits, out_splits):
+        import torch
+
+        dist = _dist()
+        if dist is None:
+            return send
+        recv = torch.empty(sum(out_splits), dtype=send.dtype, device=send.device)
+        if self.comm_cpu:
+            r = recv.cpu()
+            dist.all_to_all_single(r, send.cpu(), output_split_sizes=out_splits, input_split_sizes=in_splits)
+            return r.to(send.device)
+        dist.all_to_all_single(recv, send, output_split_sizes=out_splits, input_split_sizes=in_splits)
+        return recv
+
+    def to_cols(self, x):
+        """Row block (nw_r x du) -> column block of the transposed view (nu_r x dd)."""
+        import torch
+
+        r, P = self.rank, self.world
+        X = x.view(self.nw[r], self.du)
+        send = torch.cat([X[:, self.u0[q]:self.u0[q] + self.nu[q]].reshape(-1) for q in range(P)])
+        recv = self._a2a(send, [self.nw[r] * self.nu[q] for q in range(P)],
+                         [self.nw[q] * self.nu[r] for q in range(P)])
+        xt = torch.empty(self.nu[r], self.dd, dtype=x.dtype, device=x.device)
+        off = 0
+        for q in range(P):
+            n = self.nw[q] * self.nu[r]
+            xt[:, self.w0[q]:self.w0[q] + self.nw[q]] = recv[off:off + n].view(self.nw[q], self.nu[r]).T
+            off += n
+        return xt.reshape(-1)
+
+    def to_rows(self, yt):
+        """Column block (nu_r x dd) of the transposed view -> row block (nw_r x du)."""
+        import torch
+
+        r, P = self.rank, self.world
+        Yt = yt.view(self.nu[r], self.dd)
+        send = torch.cat([Yt[:, self.w0[q]:self.w0[q] + self.nw[q]].T.reshape(-1) for q in range(P)])
+        recv = self._a2a(send, [self.nu[r] * self.nw[q] for q in range(P)],
+                         [self.nu[q] * self.nw[r] for q in range(P)])
+        Y = torch.empty(self.nw[r], self.du, dtype=yt.dtype, device=yt.device)
+        off = 0
+        for q in range(P):
+            n = self.nu[q] * self.nw[r]
+            Y[:, self.u0[q]:self.u0[q] + self.nu[q]] = recv[off:off + n].view(self.nw[r], self.nu[q])
+            off += n
+        return Y.reshape(-1)
+
+    # ----------------------------------------------------------------- H·v
+    def hxv(self, x):
+        """H·v on the split vector (spMatVec_mpi_cc semantics)."""
+        r = self.rank
+        y = self.ops.rows(self.w0[r], self.nw[r], x)
+        yt = self.ops.cols(self.u0[r], self.nu[r], self.to_cols(x))
+        return y + self.to_rows(yt)
+
+    def close(self):
+        if self._S is not None:
+            self._S.close()
+            self._S = None
+
+
+def _allreduce_sum(t):
+    dist = _dist()
+    if dist is None:
+        return t
+    if dist.get_backend() != "nccl":
+        c = t.cpu()
+        dist.all_reduce(c)
+        return c.to(t.device)
+    dist.all_reduce(t)
+    return t
+
+
+def dist_lanczos(ds: DistKronSector, v0_loc, nitermax: int, threshold: float = 1e-13):
+    """sp_lanc_tridiag on the split vector: (alfa, beta, nlanc); beta[0] = 0,
+    beta[k+1] couples k, k+1 (.repo/PLAIN_LANCZOS.f90:87-118, 154-180)."""
+    import torch
+
+    v = v0_loc.clone()
+    nrm = _allreduce_sum(torch.sum(torch.abs(v) ** 2).reshape(1).to(torch.float64))
+    v = v / torch.sqrt(nrm).to(v.dtype)
+    vo = torch.zeros_like(v)
+    b = 0.0
+    alfa = np.zeros(nitermax)
+    beta = np.zeros(nitermax + 1)
+    n = 0
+    for it in range(nitermax):
+        w = ds.hxv(v) - b * vo
+        a = float(_allreduce_sum(torch.sum(torch.conj(v) * w).real.reshape(1).to(torch.float64)).item())
+        w = w - a * v
+        b = float(torch.sqrt(_allreduce_sum(torch.sum(torch.abs(w) ** 2).reshape(1).to(torch.float64))).item())
+        alfa[it] = a
+        beta[it + 1] = b
+        n = it + 1
+        if abs(b) < threshold:
+            break
+        vo = v
+        v = w / b
+    return alfa, beta, n

@@ -1,0 +1,88 @@
+"""Within-sector split (edgpu.dist) on CPU: the all-to-all transposes and the
+split Lanczos on 1/2/3 gloo ranks against the oracle's full-sector CSR."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from edgpu.params import make_config
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _cfg():
+    return make_config(Norb=1, Nbath=7, bath="random", seed=5)    # c2 family, (4,4): 70 x 70
+
+
+def test_factors_reproduce_sector():
+    from oracle_kron import oracle_factors
+
+    H, D, Hup, Hdw, du, dd = oracle_factors(_cfg(), 4, 4)
+    x = np.sin(np.arange(1, du * dd + 1)) + 1j * np.cos(3 * np.arange(1, du * dd + 1))
+    X = x.reshape(dd, du)
+    y = (D * X + (Hup @ X.T).T + Hdw @ X).reshape(-1)
+    assert np.max(np.abs(y - H @ x)) < 1e-12
+
+
+def test_split_serial_equals_full():
+    from oracle_kron import NumpyKronOps, oracle_factors
+    from edgpu.dist import DistKronSector
+
+    H, D, Hup, Hdw, du, dd = oracle_factors(_cfg(), 4, 4)
+    ds = DistKronSector(ops=NumpyKronOps(D, Hup, Hdw, du, dd))
+    x = torch.from_numpy(np.sin(np.arange(1, du * dd + 1)) + 1j * np.cos(3 * np.arange(1, du * dd + 1)))
+    y = ds.hxv(x)
+    assert np.max(np.abs(y.numpy() - H @ x.numpy())) < 1e-12
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    from oracle_kron import NumpyKronOps, oracle_factors
+    from edgpu.dist import DistKronSector, dist_lanczos
+    from oracle.oracle import lanc_tridiag, Oracle
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = _cfg()
+    H, D, Hup, Hdw, du, dd = oracle_factors(cfg, 4, 4)
+    ds = DistKronSector(ops=NumpyKronOps(D, Hup, Hdw, du, dd))
+    n = du * dd
+    i = np.arange(1, n + 1, dtype=np.float64)
+    x = torch.from_numpy(np.sin(i) + 1j * np.cos(3 * i))
+    y = ds.gather(ds.hxv(ds.scatter(x)))
+    err = float(np.max(np.abs(y.numpy() - H @ x.numpy())))
+    a, b, nl = dist_lanczos(ds, ds.scatter(x), 40)
+    orc = Oracle(cfg)
+    hmap = orc.build_sector(4, 4)
+    ar, br, nr = lanc_tridiag(orc.build_csr(hmap), x.numpy(), 40)
+    q.put((rank, err, float(np.max(np.abs(a[:30] - ar[:30]))), float(np.max(np.abs(b[:30] - br[:30]))), nl, nr,
+           ds.local_dim))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_split_matches_full(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert sum(o[6] for o in out) == 4900          # the blocks tile the sector
+    for rank, err, da, db, nl, nr, _ in out:
+        assert err < 1e-12
+        assert nl == nr == 40
+        assert da < 1e-10 and db < 1e-10
