@@ -162,6 +162,28 @@ def bench_nonsu2(dist, world, dev):
                         "+ build_gf (diag + mixed seeds, nGFiter=200, L=5000)"}
 
 
+def bench_split(dist, world, dev, iters=10):
+    """one Nlevels=28 (7,7) sector split by down rows over all
+    ranks; H·v = local Kronecker rows + all-to-all transpose + columns +
+    all-to-all back (edgpu.dist).  Strong scaling of a single H·v."""
+    from edgpu.dist import DistKronSector
+    from edgpu.params import make_config
+
+    cfg = make_config(Norb=1, Nbath=13, bath="random", seed=20251015)
+    ds = DistKronSector(cfg, 7, 7, device=dev, real=True)
+    w0, nw = ds.local_rows
+    i = torch.arange(w0 * ds.du + 1, (w0 + nw) * ds.du + 1, dtype=torch.float64, device="cuda")
+    x = torch.sin(i)
+    for _ in range(2):
+        ds.hxv(x)
+    dt, _ = _timed(dist, lambda: [ds.hxv(x) for _ in range(iters)])
+    ds.close()
+    return {"ms_per_hxv": round(dt / iters * 1e3, 4), "n_gpus": world, "scaling": "strong",
+            "dim": ds.du * ds.dd, "local_rows": nw,
+            "workload": "Nlevels=28 Norb=1 Nbath=13 (7,7) sector split by down rows; Kronecker rows/cols "
+                        "kernels + 2 all_to_all exchanges per H·v (RCCL; strip layout, no transposes)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -237,6 +259,7 @@ def main():
     direct_ips = args.niter / (min(dms) * 1e-3)
     Sd.close()
 
+    split = None if args.no_farm else bench_split(dist, world, dev)
     farm = None if args.no_farm else bench_farm(dist, world, dev)
     nonsu2 = None if args.no_farm else bench_nonsu2(dist, world, dev)
 
@@ -302,6 +325,7 @@ def main():
             "spmv_gbs_c2": round(gbs2, 1),
             "spmv_ms_c2": round(ms2, 5),
             "farm_c4": farm,
+            "split_n28": split,
             "nonsu2_c5": nonsu2,
             "roofline": roof,
             "cpu_baseline": cpu,

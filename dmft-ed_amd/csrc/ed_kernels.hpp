@@ -752,8 +752,8 @@ __global__ void __launch_bounds__(kBlock) k_kron(KronArgs<HC> K, const val_t<VC>
 // H = D + Hup(x)1 + 1(x)Hdw on the DimDw x DimUp view.  A rank owning down
 // rows [w0, w0+nw) applies the diagonal and the up-spin hops locally
 // (k_kron_rows on its nw x DimUp block); the down-spin hops act along the
-// other index and run on the transposed block (k_kron_cols on nu x DimDw
-// columns it receives by an all-to-all).  Term order per element: diagonal,
+// other index and run on the DimDw x nu column strip it receives by an
+// all-to-all (k_kron_cols).  Term order per element: diagonal,
 // up hops | down hops — the two partial sums are added by the caller.
 template <bool HC, bool VC>
 __global__ void __launch_bounds__(kBlock) k_kron_rows(KronArgs<HC> K, int64_t w0, int64_t nw,
@@ -775,22 +775,25 @@ __global__ void __launch_bounds__(kBlock) k_kron_rows(KronArgs<HC> K, int64_t w0
   }
 }
 
+// z, yz: DimDw x nu row-major (down row iw, up column c fastest): exactly
+// the concatenation of the row blocks an all-to-all delivers, so neither
+// side of the exchange needs a transpose and the gathers z[iw'][c] are
+// coalesced over c.
 template <bool HC, bool VC>
 __global__ void __launch_bounds__(kBlock) k_kron_cols(KronArgs<HC> K, int64_t nu,
-                                                      const val_t<VC>* __restrict__ xt,
-                                                      val_t<VC>* __restrict__ yt, int accumulate) {
+                                                      const val_t<VC>* __restrict__ z,
+                                                      val_t<VC>* __restrict__ yz, int accumulate) {
   using V = val_t<VC>;
   const int64_t dd = K.dimdw;
   for (int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x; q < nu * dd;
        q += (int64_t)gridDim.x * kBlock) {
-    const int64_t c = q / dd, iw = q - c * dd;
-    V acc = accumulate ? yt[q] : vzero<V>();
-    const V* xcol = xt + c * dd;
+    const int64_t iw = q / nu, c = q - iw * nu;
+    V acc = accumulate ? yz[q] : vzero<V>();
     for (int k = 0; k < K.degdw; k++) {
       const int64_t t = (int64_t)k * dd + iw;
-      acc = add(acc, mul(K.dwv[t], xcol[K.dwc[t]]));
+      acc = add(acc, mul(K.dwv[t], z[(int64_t)K.dwc[t] * nu + c]));
     }
-    yt[q] = acc;
+    yz[q] = acc;
   }
 }
 

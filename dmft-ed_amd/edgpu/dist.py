@@ -12,9 +12,13 @@ its own block, and the down-spin hops — which mix rows — run on the
 transposed view, where each rank owns up columns [u0, u0+nu):
 
     y  = rows(x)                                  ed_sector_kron_rows (HIP)
-    xt = transpose(x)                             all_to_all over RCCL/xGMI
-    yt = cols(xt)                                 ed_sector_kron_cols (HIP)
-    y += transpose(yt)                            all_to_all
+    z  = strip(x)                                 all_to_all over RCCL/xGMI
+    yz = cols(z)                                  ed_sector_kron_cols (HIP)
+    y += unstrip(yz)                              all_to_all
+
+The strip is the DimDw x nu block of the rank's up columns, row-major: the
+row blocks an all-to-all delivers are already in that order, so neither
+exchange needs a transpose (only a column slice/scatter of the local block).
 
 Each H·v moves 2·(P-1)/P of the local block per rank instead of the
 reference's full-vector Allgatherv (P·x the local block), and every rank
@@ -171,35 +175,33 @@ class DistKronSector:
         return recv
 
     def to_cols(self, x):
-        """Row block (nw_r x du) -> column block of the transposed view (nu_r x dd)."""
+        """Row block (nw_r x du) -> the DimDw x nu_r strip of this rank's up
+        columns.  Block q of the send buffer is X[:, cols of q]; what arrives
+        from ranks 0..P-1 (down rows in rank order) is the strip row-major."""
         import torch
 
         r, P = self.rank, self.world
+        if P == 1:
+            return x
         X = x.view(self.nw[r], self.du)
         send = torch.cat([X[:, self.u0[q]:self.u0[q] + self.nu[q]].reshape(-1) for q in range(P)])
-        recv = self._a2a(send, [self.nw[r] * self.nu[q] for q in range(P)],
+        return self._a2a(send, [self.nw[r] * self.nu[q] for q in range(P)],
                          [self.nw[q] * self.nu[r] for q in range(P)])
-        xt = torch.empty(self.nu[r], self.dd, dtype=x.dtype, device=x.device)
-        off = 0
-        for q in range(P):
-            n = self.nw[q] * self.nu[r]
-            xt[:, self.w0[q]:self.w0[q] + self.nw[q]] = recv[off:off + n].view(self.nw[q], self.nu[r]).T
-            off += n
-        return xt.reshape(-1)
 
-    def to_rows(self, yt):
-        """Column block (nu_r x dd) of the transposed view -> row block (nw_r x du)."""
+    def to_rows(self, yz):
+        """DimDw x nu_r strip -> this rank's row block: the strip's row block q
+        goes to rank q as is; the blocks received are scattered into columns."""
         import torch
 
         r, P = self.rank, self.world
-        Yt = yt.view(self.nu[r], self.dd)
-        send = torch.cat([Yt[:, self.w0[q]:self.w0[q] + self.nw[q]].T.reshape(-1) for q in range(P)])
-        recv = self._a2a(send, [self.nu[r] * self.nw[q] for q in range(P)],
-                         [self.nu[q] * self.nw[r] for q in range(P)])
-        Y = torch.empty(self.nw[r], self.du, dtype=yt.dtype, device=yt.device)
+        if P == 1:
+            return yz
+        recv = self._a2a(yz, [self.nw[q] * self.nu[r] for q in range(P)],
+                         [self.nw[r] * self.nu[q] for q in range(P)])
+        Y = torch.empty(self.nw[r], self.du, dtype=yz.dtype, device=yz.device)
         off = 0
         for q in range(P):
-            n = self.nu[q] * self.nw[r]
+            n = self.nw[r] * self.nu[q]
             Y[:, self.u0[q]:self.u0[q] + self.nu[q]] = recv[off:off + n].view(self.nw[r], self.nu[q])
             off += n
         return Y.reshape(-1)

@@ -195,14 +195,15 @@ int ed_sector_lanc_run(ed_sector* s, int32_t vtype, const void* v0_dev, int32_t 
  * H = D + Hup(x)1 + 1(x)Hdw on the DimDw x DimUp view of v.
  *   kron_rows: y[r][:] = D[w0+r][:] .* x[r][:] + Hup x[r][:]      (r < nw)
  *              x, y: the nw x DimUp row block of down rows [w0, w0+nw)
- *   kron_cols: yt[c][:] (+)= Hdw xt[c][:]                          (c < nu)
- *              xt, yt: an nu x DimDw block of the transposed view (up
- *              columns [u0, u0+nu)); accumulate = 1 adds into yt
- * H v = rows(x) + transpose(cols(transpose(x))): two all-to-alls per H·v
- * (edgpu.dist).  Device pointers, async on `stream`. */
+ *   kron_cols: yz[:][c] (+)= Hdw z[:][c]                           (c < nu)
+ *              z, yz: the DimDw x nu strip of up columns [u0, u0+nu),
+ *              row-major (c fastest); accumulate = 1 adds into yz
+ * H v = rows(x) + cols(strip(x)) regathered: two all-to-alls per H·v, whose
+ * row blocks are already the strip layout (edgpu.dist).  Device pointers,
+ * async on `stream`. */
 int ed_sector_kron_rows(ed_sector* s, int32_t vtype, int64_t w0, int64_t nw, const void* x, void* y,
                         void* stream);
-int ed_sector_kron_cols(ed_sector* s, int32_t vtype, int64_t u0, int64_t nu, const void* xt, void* yt,
+int ed_sector_kron_cols(ed_sector* s, int32_t vtype, int64_t u0, int64_t nu, const void* z, void* yz,
                         int32_t accumulate, void* stream);
 
 /* Green's-function seed (ED_GF_NORMAL.f90:159-174 / :216-229):

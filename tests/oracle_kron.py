@@ -42,7 +42,6 @@ class NumpyKronOps:
         Y = self.D[w0:w0 + nw] * X + (self.Hup @ X.T).T
         return torch.from_numpy(np.ascontiguousarray(Y).reshape(-1))
 
-    def cols(self, u0, nu, xt):
-        XT = xt.numpy().reshape(nu, self.dimdw)
-        YT = (self.Hdw @ XT.T).T
-        return torch.from_numpy(np.ascontiguousarray(YT).reshape(-1))
+    def cols(self, u0, nu, z):
+        Z = z.numpy().reshape(self.dimdw, nu)
+        return torch.from_numpy(np.ascontiguousarray(self.Hdw @ Z).reshape(-1))
