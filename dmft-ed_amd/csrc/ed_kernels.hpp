@@ -59,6 +59,8 @@ __device__ __forceinline__ double sub(double a, double b) { return a - b; }
 __device__ __forceinline__ double2 sub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
 __device__ __forceinline__ double scl(double s, double a) { return s * a; }
 __device__ __forceinline__ double2 scl(double s, double2 a) { return make_double2(s * a.x, s * a.y); }
+__device__ __forceinline__ double re_of(double a) { return a; }
+__device__ __forceinline__ double re_of(double2 a) { return a.x; }
 // Re(conj(a)*b): dot_product real part
 __device__ __forceinline__ double redot(double a, double b) { return a * b; }
 __device__ __forceinline__ double redot(double2 a, double2 b) { return a.x * b.x + a.y * b.y; }

@@ -55,6 +55,7 @@ static inline int grid_once(int64_t nthreads) { return std::min(grid_for(nthread
 struct KronHost {
   int64_t dimup = 0, dimdw = 0;
   int degup = 0, degdw = 0, nimp = 0;
+  bool diag_real = true;  // spin-factor diagonals have no imaginary part
   int32_t *upc = nullptr, *dwc = nullptr;
   void *upv = nullptr, *dwv = nullptr, *aup = nullptr, *adw = nullptr;
   double* uimp = nullptr;
@@ -368,6 +369,7 @@ static int build_kron(ed_sector* s) {
     for (int64_t r = 0; r < nr; r++) {
       double re, im;
       spin_diag(M, sp, st[r], &re, &im);
+      if (im != 0.0) K.diag_real = false;
       if (s->hc) {
         a[2 * r] = re;
         a[2 * r + 1] = im;
@@ -663,6 +665,12 @@ static int build_preg(ed_sector* s) {
   CK(dcopy(s, sptr.data(), s->d_sptr, (ns + 1) * 8, hipMemcpyDeviceToHost));
   CK(dcopy(s, sc.data(), s->d_cols, slots * 4, hipMemcpyDeviceToHost));
   CK(dcopy(s, sv.data(), s->d_vals, slots * 8 * hw, hipMemcpyDeviceToHost));
+  if (hw == 2) {  // the register modes keep a real diagonal (Hermitian H)
+    std::vector<double> dg(dim * 2);
+    CK(dcopy(s, dg.data(), s->d_diag, dim * 16, hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < dim; i++)
+      if (dg[2 * i + 1] != 0.0) return -1;
+  }
   int wmax = 0;
   for (int64_t i = 0; i < dim; i++) wmax = std::max<int>(wmax, cnt[i]);
   int W = 0;
@@ -711,7 +719,7 @@ static int build_preg(ed_sector* s) {
 // or -1 when the sector does not fit one workgroup's LDS / register budget.
 static int64_t persist_lds(const ed_sector* s, int vc, int mode);
 // ELL words per lane that compile without scratch (-Rpass-analysis=kernel-resource-usage)
-constexpr int preg_cap(bool hc, bool vc) { return vc ? (hc ? 60 : 72) : 112; }
+constexpr int preg_cap(bool hc, bool vc) { return vc ? (hc ? 80 : 84) : 112; }
 static int persist_mode(ed_sector* s, int vc, int path) {
   if (getenv("ED_GPU_NO_PERSIST")) return -1;
   const int64_t vs = vc ? 16 : 8;
@@ -748,8 +756,8 @@ static int persist_mode(ed_sector* s, int vc, int path) {
     const int64_t hs = s->hc ? 16 : 8;
     const int64_t dict = ((int64_t)(K.degup * K.dimup + K.degdw * K.dimdw) + 1) * hs;
     const int cap = preg_cap(s->hc, vc);
-    const int64_t l3 = ((dict + 15) & ~(int64_t)15) + lds + ((s->dim * hs + 15) & ~(int64_t)15);
-    if (W && RPT * W <= cap && dict <= (int64_t)kPkOffMask + 1 && l3 <= kLdsBudget) {
+    const int64_t l3 = ((dict + 15) & ~(int64_t)15) + lds + ((s->dim * 8 + 15) & ~(int64_t)15);
+    if (W && RPT * W <= cap && dict <= (int64_t)kPkOffMask + 1 && l3 <= kLdsBudget && K.diag_real) {
       s->kreg_W = W;
       s->kreg_rpt = RPT;
       return 3;
@@ -770,12 +778,12 @@ static int64_t persist_lds(const ed_sector* s, int vc, int mode) {
   int64_t lds = ((s->dim * vs + 15) & ~(int64_t)15);
   if (mode == 2) {
     const int64_t hs = s->hc ? 16 : 8;
-    return lds + ((s->dim * hs + 15) & ~(int64_t)15) + (((int64_t)s->ndict * hs + 15) & ~(int64_t)15);
+    return lds + ((s->dim * 8 + 15) & ~(int64_t)15) + (((int64_t)s->ndict * hs + 15) & ~(int64_t)15);
   }
   if (mode == 3) {
     const int64_t hs = s->hc ? 16 : 8;
     const int64_t dict = ((int64_t)(s->K.degup * s->K.dimup + s->K.degdw * s->K.dimdw) + 1) * hs;
-    return lds + ((s->dim * hs + 15) & ~(int64_t)15) + ((dict + 15) & ~(int64_t)15);
+    return lds + ((s->dim * 8 + 15) & ~(int64_t)15) + ((dict + 15) & ~(int64_t)15);
   }
   if (mode == 1) {
     const KronHost& K = s->K;

@@ -133,14 +133,16 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC>* __res
   // offsets fit 14 bits; vl moves behind it)
   constexpr bool REG = MODE == 2 || MODE == 3;
   uint32_t pk[REG ? RPT * E : 1];
-  const H* dg = nullptr;
+  // diagonal of a Hermitian H is real: kept as real(8) in LDS (host checks
+  // the imaginary parts are zero before choosing a register mode)
+  const double* dg = nullptr;
   const unsigned char* dct = smem;
   if constexpr (MODE == 2) {
     const int64_t dbytes = ((int64_t)a.ndict * sizeof(H) + 15) & ~(int64_t)15;
     for (int t = tid; t < a.ndict; t += NT) ((H*)smem)[t] = a.dict[t];
     vl = (V*)(smem + dbytes);
-    H* s_g = (H*)(smem + dbytes + ((dim * sizeof(V) + 15) & ~(int64_t)15));
-    for (int64_t t = tid; t < dim; t += NT) s_g[t] = a.diag[t];
+    double* s_g = (double*)(smem + dbytes + ((dim * sizeof(V) + 15) & ~(int64_t)15));
+    for (int64_t t = tid; t < dim; t += NT) s_g[t] = re_of(a.diag[t]);
     dg = s_g;
 #pragma unroll
     for (int k = 0; k < RPT * E; k++) pk[k] = a.pk[k * NT + tid];
@@ -158,10 +160,10 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC>* __res
     if (tid == 0) sd[nup + ndw] = mk<HC>(0.0, 0.0);
     const int64_t dbytes = ((int64_t)(nup + ndw + 1) * sizeof(H) + 15) & ~(int64_t)15;
     vl = (V*)(smem + dbytes);
-    H* s_g = (H*)(smem + dbytes + ((dim * sizeof(V) + 15) & ~(int64_t)15));
+    double* s_g = (double*)(smem + dbytes + ((dim * sizeof(V) + 15) & ~(int64_t)15));
     for (int64_t t = tid; t < dim; t += NT) {
       const int iw = (int)(t / du), iu = (int)(t - (int64_t)iw * du);
-      s_g[t] = add(add(K.aup[iu], K.adw[iw]), mk<HC>(K.uimp[K.impu[iu] * K.nimp + K.impd[iw]], 0.0));
+      s_g[t] = re_of(add(add(K.aup[iu], K.adw[iw]), mk<HC>(K.uimp[K.impu[iu] * K.nimp + K.impd[iw]], 0.0)));
     }
     dg = s_g;
     const uint32_t hs = sizeof(H);
@@ -188,7 +190,11 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC>* __res
   }
 
   // --- state in
-  V p[RPT];
+  // complex vectors in register modes keep p = v_{k-1} in global memory (own
+  // rows only, read once and written once per step, L2-resident): it frees
+  // 4 VGPRs per row for the ELL words
+  constexpr bool PG = REG && VC;
+  V p[PG ? 1 : RPT];
   uint32_t rix[RPT];  // Kronecker row index packed (iw << 16) | iu  (DimUp, DimDw < 2^16)
   double b;
   int it0;
@@ -197,12 +203,16 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC>* __res
 #pragma unroll
     for (int r = 0; r < RPT; r++) {
       const int64_t i = tid + (int64_t)r * NT;
-      p[r] = vzero<V>();
+      if constexpr (!PG) p[r] = vzero<V>();
       if (i < dim) {
         V x = Rg[i];
         vl[i] = x;
-        if (a.first) nrm += redot(x, x);
-        else p[r] = Pg[i];
+        if (a.first) {
+          nrm += redot(x, x);
+          if constexpr (PG) Pg[i] = vzero<V>();
+        } else if constexpr (!PG) {
+          p[r] = Pg[i];
+        }
         if constexpr (MODE == 1) {
           const uint32_t w_ = (uint32_t)(i / a.K.dimup);
           rix[r] = (w_ << 16) | (uint32_t)(i - (int64_t)w_ * a.K.dimup);
@@ -299,7 +309,8 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC>* __res
             acc = add(acc, mul(dwv[q], vl[dwc[q] * du + iur]));
           }
         }
-        w[r] = sub(acc, scl(b, p[r]));
+        if constexpr (PG) w[r] = sub(acc, scl(b, Pg[i]));
+        else w[r] = sub(acc, scl(b, p[r]));
         ap += redot(xi, w[r]);
         if (basis) basis[(int64_t)it * dim + i] = xi;
       }
@@ -329,7 +340,8 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC>* __res
     for (int r = 0; r < RPT; r++) {
       const int64_t i = tid + (int64_t)r * NT;
       if (i < dim) {
-        p[r] = vl[i];
+        if constexpr (PG) Pg[i] = vl[i];
+        else p[r] = vl[i];
         vl[i] = scl(inv, w[r]);
       }
     }
@@ -350,7 +362,7 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC>* __res
     const int64_t i = tid + (int64_t)r * NT;
     if (i < dim) {
       Rg[i] = vl[i];
-      Pg[i] = p[r];
+      if constexpr (!PG) Pg[i] = p[r];
     }
   }
   if (tid == 0) {
