@@ -114,6 +114,12 @@ struct ed_sector {
   uint32_t* d_pk = nullptr;
   void* d_dict = nullptr;
   int ndict = 0;
+  // Kronecker register layout for the persistent kernel (MODE 4)
+  int pkr_state = 0;        // 0 not tried, -1 ineligible, 1 tables ready
+  int pkr_src = -1;         // path the tables came from (0 stored SELL, 2 hop tables)
+  int pkr_E = 0, pkr_rpt = 0, pkr_du = 0, pkr_dd = 0, pkr_degu = 0, pkr_degd = 0;
+  const int32_t *d_kupc = nullptr, *d_kdwc = nullptr;
+  const double *d_kupv = nullptr, *d_kdwv = nullptr, *d_kdiag = nullptr;
   // graph cache for Lanczos iterations
   hipGraphExec_t gexec = nullptr;
   int g_path = -2, g_vc = -1, g_chunk = 0;
@@ -499,6 +505,11 @@ static void drop_graph(ed_sector* s) {
   s->gexec = nullptr;
 }
 
+// P (= v_{k-1}) is read by every row slot of the register-mode persistent
+// kernels, padding rows included (a guarded load per row costs spills): it
+// has at least kPRegBlock * 10 rows, the padding kept zero by the kernel.
+static size_t p_rows(const ed_sector* s) { return (size_t)std::max<int64_t>(s->dim, (int64_t)kPRegBlock * 10); }
+
 static int lanc_prepare(ed_sector* s, int vc, int cap, bool want_basis, int basis_cols) {
   LancWS& w = s->ws;
   const size_t vs = vc ? 16 : 8;
@@ -508,20 +519,20 @@ static int lanc_prepare(ed_sector* s, int vc, int cap, bool want_basis, int basi
       HIPCK(hipStreamSynchronize(s->stream));
       const size_t ovs = w.vc ? 16 : 8;
       dfree(s, &w.R, s->dim * ovs);
-      dfree(s, &w.P, s->dim * ovs);
+      dfree(s, &w.P, p_rows(s) * ovs);
       dfree(s, &w.W, s->dim * ovs);
       dfree(s, &w.Y, s->dim * ovs);
       dfree(s, &w.basis, (size_t)w.basis_cols * s->dim * ovs);
       w.basis_cols = 0;
       CK(dalloc(s, &w.R, s->dim * vs));
-      CK(dalloc(s, &w.P, s->dim * vs));
+      CK(dalloc(s, &w.P, p_rows(s) * vs));
       CK(dalloc(s, &w.W, s->dim * vs));
       CK(dalloc(s, &w.Y, s->dim * vs));
       w.vc = vc;
       goto sized;
     }
     CK(dalloc(s, &w.R, s->dim * vs));
-    CK(dalloc(s, &w.P, s->dim * vs));
+    CK(dalloc(s, &w.P, p_rows(s) * vs));
     CK(dalloc(s, &w.W, s->dim * vs));
     CK(dalloc(s, &w.Y, s->dim * vs));
     CK(dalloc_t(s, &w.st, 1));
@@ -715,9 +726,134 @@ static int build_preg(ed_sector* s) {
   return W;
 }
 
+// MODE 4 (Kronecker register layout, ed_persist.hpp): per lane E up-hop
+// entries once plus RPT rows x (E down-hop entries, diagonal, r, p, w) must
+// stay below the spill-free budget (-Rpass-analysis=kernel-resource-usage:
+// E=4/RPT=10 and E=8/RPT=6 compile without scratch).
+constexpr bool pkr_fits(int E, int RPT) { return RPT * (3 * E + 8) + 3 * E <= 216; }
+static int pkr_geom(ed_sector* s, int64_t du, int64_t dd, int degu, int degd) {
+  const int deg = std::max(degu, degd);
+  const int E = deg <= 4 ? 4 : deg <= 8 ? 8 : 0;
+  if (!E || du < 1 || du > kPRegBlock || du * dd != s->dim) return -1;
+  const int64_t G = kPRegBlock / du, rpt = (dd + G - 1) / G;
+  const int RPT = rpt <= 2 ? 2 : rpt <= 4 ? 4 : rpt <= 6 ? 6 : rpt <= 8 ? 8 : rpt <= 10 ? 10 : 0;
+  if (!RPT || !pkr_fits(E, RPT)) return -1;
+  s->pkr_E = E;
+  s->pkr_rpt = RPT;
+  s->pkr_du = (int)du;
+  s->pkr_dd = (int)dd;
+  s->pkr_degu = degu;
+  s->pkr_degd = degd;
+  return 1;
+}
+
+// MODE 4 tables of a stored sector: read back from the stored SELL matrix
+// and accepted only when it has the Kronecker form H = D + Hup(x)1 + 1(x)Hdw
+// on the DimDw x DimUp view (row = iw*DimUp + iu): every entry of row
+// (iw, iu) keeps iw (up hop) or iu (down hop), the up list of iu is the same
+// (targets and value bits, in order) in every iw block and the down list of
+// iw the same for every iu.  The registers then hold exactly the stored
+// values; only the summation order (diag, up, down) differs from k_spmv.
+static int build_pkron_stored(ed_sector* s) {
+  if (s->pkr_state && s->pkr_src == 0) return s->pkr_state;
+  s->pkr_state = -1;
+  s->pkr_src = 0;
+  if (s->hc || s->Mh.mode != ED_MODE_NORMAL || !(s->flags & ED_STORED)) return -1;
+  const int64_t du = s->T.dimup, dd = s->T.dimdw, dim = s->dim, ns = s->nslice, slots = s->padded;
+  if (du < 1 || du > kPRegBlock || du * dd != dim) return -1;
+  std::vector<uint16_t> cnt(dim);
+  std::vector<int64_t> sptr(ns + 1);
+  std::vector<int32_t> sc(slots);
+  std::vector<double> sv(slots);
+  HIPCK(hipStreamSynchronize(s->stream));
+  CK(dcopy(s, cnt.data(), s->d_cnt, dim * 2, hipMemcpyDeviceToHost));
+  CK(dcopy(s, sptr.data(), s->d_sptr, (ns + 1) * 8, hipMemcpyDeviceToHost));
+  CK(dcopy(s, sc.data(), s->d_cols, slots * 4, hipMemcpyDeviceToHost));
+  CK(dcopy(s, sv.data(), s->d_vals, slots * 8, hipMemcpyDeviceToHost));
+  using Hop = std::pair<int32_t, uint64_t>;
+  std::vector<std::vector<Hop>> ul(du), dl(dd);
+  std::vector<char> useen(du, 0), dseen(dd, 0);
+  std::vector<Hop> lu, ld;
+  for (int64_t i = 0; i < dim; i++) {
+    const int64_t iw = i / du, iu = i - iw * du, base = sptr[i >> 6] + (i & 63);
+    lu.clear();
+    ld.clear();
+    for (int k = 0; k < cnt[i]; k++) {
+      const int64_t q = base + 64 * (int64_t)k;
+      const int64_t c = sc[q], cw = c / du, cu = c - cw * du;
+      uint64_t bits;
+      memcpy(&bits, &sv[q], 8);
+      if (cw == iw && cu != iu) lu.push_back({(int32_t)cu, bits});
+      else if (cu == iu && cw != iw) ld.push_back({(int32_t)cw, bits});
+      else return -1;
+    }
+    if (!useen[iu]) { ul[iu] = lu; useen[iu] = 1; } else if (ul[iu] != lu) return -1;
+    if (!dseen[iw]) { dl[iw] = ld; dseen[iw] = 1; } else if (dl[iw] != ld) return -1;
+  }
+  int degu = 0, degd = 0;
+  for (auto& l : ul) degu = std::max<int>(degu, (int)l.size());
+  for (auto& l : dl) degd = std::max<int>(degd, (int)l.size());
+  if (pkr_geom(s, du, dd, degu, degd) < 0) return -1;
+  auto table = [&](const std::vector<std::vector<Hop>>& L, int deg, int64_t n, const int32_t** dc,
+                   const double** dv) {
+    std::vector<int32_t> c((size_t)std::max(deg, 1) * n, 0);
+    std::vector<double> v((size_t)std::max(deg, 1) * n, 0.0);
+    for (int64_t r = 0; r < n; r++)
+      for (size_t e = 0; e < L[r].size(); e++) {
+        c[e * n + r] = L[r][e].first;
+        memcpy(&v[e * n + r], &L[r][e].second, 8);
+      }
+    int32_t* pc;
+    void* pv;
+    CK(upload(s, &pc, c));
+    CK(dalloc(s, &pv, v.size() * 8));
+    CK(dcopy(s, pv, v.data(), v.size() * 8, hipMemcpyHostToDevice));
+    *dc = pc;
+    *dv = (const double*)pv;
+    return ED_OK;
+  };
+  CK(table(ul, degu, du, &s->d_kupc, &s->d_kupv));
+  CK(table(dl, degd, dd, &s->d_kdwc, &s->d_kdwv));
+  s->d_kdiag = (const double*)s->d_diag;
+  s->pkr_state = 1;
+  return 1;
+}
+
+// MODE 4 tables of a matrix-free sector: the Kronecker hop tables themselves
+// (diagonal generated in-kernel from aup + adw + U, as k_kron).
+static int build_pkron_direct(ed_sector* s) {
+  if (s->pkr_state && s->pkr_src == 2) return s->pkr_state;
+  s->pkr_state = -1;
+  s->pkr_src = 2;
+  if (s->hc || !s->kron || !s->K.diag_real) return -1;
+  const KronHost& K = s->K;
+  if (pkr_geom(s, K.dimup, K.dimdw, K.degup, K.degdw) < 0) return -1;
+  s->d_kupc = K.upc;
+  s->d_kupv = (const double*)K.upv;
+  s->d_kdwc = K.dwc;
+  s->d_kdwv = (const double*)K.dwv;
+  s->d_kdiag = nullptr;
+  s->pkr_state = 1;
+  return 1;
+}
+
 // Returns the persistent mode (0 stored, 1 Kronecker, 2 stored in registers)
 // or -1 when the sector does not fit one workgroup's LDS / register budget.
 static int64_t persist_lds(const ed_sector* s, int vc, int mode);
+// Rows per thread of the 1024-thread modes (0, 1): the launch's template value
+static int persist_rpt01(int64_t dim) {
+  const int64_t rpt = (dim + kPBlock - 1) / kPBlock;
+  return rpt <= 6 ? (int)rpt : rpt <= 8 ? 8 : rpt <= 10 ? 10 : rpt <= 12 ? 12 : 16;
+}
+// LDS vector rows of a persistent launch: NT * RPT (padding rows stay zero)
+static int64_t persist_vrows(const ed_sector* s, int mode) {
+  switch (mode) {
+    case 2: return (int64_t)kPRegBlock * s->preg_rpt;
+    case 3: return (int64_t)kPRegBlock * s->kreg_rpt;
+    case 4: return (int64_t)kPRegBlock * s->pkr_rpt;
+    default: return (int64_t)kPBlock * persist_rpt01(s->dim);
+  }
+}
 // ELL words per lane that compile without scratch (-Rpass-analysis=kernel-resource-usage)
 constexpr int preg_cap(bool hc, bool vc) { return vc ? (hc ? 80 : 84) : 112; }
 static int persist_mode(ed_sector* s, int vc, int path) {
@@ -727,7 +863,13 @@ static int persist_mode(ed_sector* s, int vc, int path) {
   // (-Rpass-analysis: 0-8 B/lane scratch up to 8 real / 5 complex rows)
   const int64_t rpt_max = (vc || s->hc) ? 5 : 8;
   if (s->dim > rpt_max * (int64_t)kPBlock) return -1;
-  int64_t lds = ((s->dim * vs + 15) & ~(int64_t)15);
+  int64_t lds = ((persist_vrows(s, 0) * vs + 15) & ~(int64_t)15);
+  // MODE 4 (Kronecker register layout, real vectors): c2 2.2 us/step
+  if (vc == 0 && !getenv("ED_GPU_NO_PKRON") && !getenv("ED_GPU_NO_PREG") &&
+      ((path == 0 && !getenv("ED_GPU_PERSIST_STORED") && build_pkron_stored(s) > 0) ||
+       (path == 2 && build_pkron_direct(s) > 0)) &&
+      persist_lds(s, vc, 4) <= kLdsBudget)
+    return 4;
   // stored: MODE 2 (ELL entries in registers; c2 4.6 us/step) by default.
   // MODE 0 streams the matrix from L2 through one CU (~40-50 GB/s) and is
   // slower than the graph-captured multi-kernel recurrence (c2: 9.8 vs 8.9
@@ -756,7 +898,8 @@ static int persist_mode(ed_sector* s, int vc, int path) {
     const int64_t hs = s->hc ? 16 : 8;
     const int64_t dict = ((int64_t)(K.degup * K.dimup + K.degdw * K.dimdw) + 1) * hs;
     const int cap = preg_cap(s->hc, vc);
-    const int64_t l3 = ((dict + 15) & ~(int64_t)15) + lds + ((s->dim * 8 + 15) & ~(int64_t)15);
+    const int64_t vr = (int64_t)kPRegBlock * RPT;
+    const int64_t l3 = ((dict + 15) & ~(int64_t)15) + ((vr * vs + 15) & ~(int64_t)15) + ((vr * 8 + 15) & ~(int64_t)15);
     if (W && RPT * W <= cap && dict <= (int64_t)kPkOffMask + 1 && l3 <= kLdsBudget && K.diag_real) {
       s->kreg_W = W;
       s->kreg_rpt = RPT;
@@ -774,16 +917,17 @@ static int persist_mode(ed_sector* s, int vc, int path) {
 }
 
 static int64_t persist_lds(const ed_sector* s, int vc, int mode) {
-  const int64_t vs = vc ? 16 : 8;
-  int64_t lds = ((s->dim * vs + 15) & ~(int64_t)15);
+  const int64_t vs = vc ? 16 : 8, vr = persist_vrows(s, mode);
+  int64_t lds = ((vr * vs + 15) & ~(int64_t)15);
+  if (mode == 4) return lds;
   if (mode == 2) {
     const int64_t hs = s->hc ? 16 : 8;
-    return lds + ((s->dim * 8 + 15) & ~(int64_t)15) + (((int64_t)s->ndict * hs + 15) & ~(int64_t)15);
+    return lds + ((vr * 8 + 15) & ~(int64_t)15) + (((int64_t)s->ndict * hs + 15) & ~(int64_t)15);
   }
   if (mode == 3) {
     const int64_t hs = s->hc ? 16 : 8;
     const int64_t dict = ((int64_t)(s->K.degup * s->K.dimup + s->K.degdw * s->K.dimdw) + 1) * hs;
-    return lds + ((s->dim * 8 + 15) & ~(int64_t)15) + ((dict + 15) & ~(int64_t)15);
+    return lds + ((vr * 8 + 15) & ~(int64_t)15) + ((dict + 15) & ~(int64_t)15);
   }
   if (mode == 1) {
     const KronHost& K = s->K;
@@ -798,8 +942,10 @@ static int64_t persist_lds(const ed_sector* s, int vc, int mode) {
 
 template <bool HC, bool VC, int MODE, int RPT, int E = 1>
 static int persist_launch_t(ed_sector* s, int64_t lds, hipStream_t st) {
-  if constexpr (MODE >= 2 && RPT * E > preg_cap(HC, VC)) {
+  if constexpr ((MODE == 2 || MODE == 3) && RPT * E > preg_cap(HC, VC)) {
     return fail(ED_ERR_UNSUPPORTED, "register-resident ELL exceeds the spill-free budget");
+  } else if constexpr (MODE == 4 && (HC || VC || !pkr_fits(E, RPT))) {
+    return fail(ED_ERR_UNSUPPORTED, "Kronecker register layout: real H and vectors within the register budget");
   } else {
   constexpr int NT = MODE >= 2 ? kPRegBlock : kPBlock;
   auto fn = k_lanc_persist<HC, VC, MODE, RPT, E, NT>;
@@ -812,7 +958,7 @@ static int persist_launch_t(ed_sector* s, int64_t lds, hipStream_t st) {
 
 template <bool HC, bool VC, int MODE, int W>
 static int persist_launch_e(ed_sector* s, int64_t lds, hipStream_t st) {
-  switch (MODE == 2 ? s->preg_rpt : s->kreg_rpt) {
+  switch (MODE == 2 ? s->preg_rpt : MODE == 3 ? s->kreg_rpt : s->pkr_rpt) {
     case 2: return persist_launch_t<HC, VC, MODE, 2, W>(s, lds, st);
     case 4: return persist_launch_t<HC, VC, MODE, 4, W>(s, lds, st);
     case 6: return persist_launch_t<HC, VC, MODE, 6, W>(s, lds, st);
@@ -823,7 +969,14 @@ static int persist_launch_e(ed_sector* s, int64_t lds, hipStream_t st) {
 
 template <bool HC, bool VC, int MODE>
 static int persist_launch_m(ed_sector* s, int64_t lds, hipStream_t st) {
-  if constexpr (MODE >= 2) {
+  if constexpr (MODE == 4) {
+    if constexpr (HC || VC) {
+      return fail(ED_ERR_UNSUPPORTED, "MODE 4 needs real H and vectors");
+    } else {
+      return s->pkr_E == 4 ? persist_launch_e<HC, VC, 4, 4>(s, lds, st)
+                           : persist_launch_e<HC, VC, 4, 8>(s, lds, st);
+    }
+  } else if constexpr (MODE >= 2) {
     switch (MODE == 2 ? s->preg_E : s->kreg_W) {
       case 8: return persist_launch_e<HC, VC, MODE, 8>(s, lds, st);
       case 12: return persist_launch_e<HC, VC, MODE, 12>(s, lds, st);
@@ -831,17 +984,16 @@ static int persist_launch_m(ed_sector* s, int64_t lds, hipStream_t st) {
       default: return persist_launch_e<HC, VC, MODE, 16>(s, lds, st);
     }
   } else {
-  const int64_t rpt = (s->dim + kPBlock - 1) / kPBlock;  // rows per thread, exact
-  switch (rpt) {
+  switch (persist_rpt01(s->dim)) {
     case 1: return persist_launch_t<HC, VC, MODE, 1>(s, lds, st);
     case 2: return persist_launch_t<HC, VC, MODE, 2>(s, lds, st);
     case 3: return persist_launch_t<HC, VC, MODE, 3>(s, lds, st);
     case 4: return persist_launch_t<HC, VC, MODE, 4>(s, lds, st);
     case 5: return persist_launch_t<HC, VC, MODE, 5>(s, lds, st);
     case 6: return persist_launch_t<HC, VC, MODE, 6>(s, lds, st);
-    case 7: case 8: return persist_launch_t<HC, VC, MODE, 8>(s, lds, st);
-    case 9: case 10: return persist_launch_t<HC, VC, MODE, 10>(s, lds, st);
-    case 11: case 12: return persist_launch_t<HC, VC, MODE, 12>(s, lds, st);
+    case 8: return persist_launch_t<HC, VC, MODE, 8>(s, lds, st);
+    case 10: return persist_launch_t<HC, VC, MODE, 10>(s, lds, st);
+    case 12: return persist_launch_t<HC, VC, MODE, 12>(s, lds, st);
     default: return persist_launch_t<HC, VC, MODE, 16>(s, lds, st);
   }
   }
@@ -872,6 +1024,15 @@ static int persist_iters(ed_sector* s, int mode, bool basis, int niter, int firs
     r.pk = s->d_pk;
     r.dict = (const HT*)s->d_dict;
     r.ndict = s->ndict;
+    r.kupc = s->d_kupc;
+    r.kupv = s->d_kupv;
+    r.kdwc = s->d_kdwc;
+    r.kdwv = s->d_kdwv;
+    r.kdiag = s->d_kdiag;
+    r.kdu = s->pkr_du;
+    r.kdd = s->pkr_dd;
+    r.kdegu = s->pkr_degu;
+    r.kdegd = s->pkr_degd;
   };
   const int64_t lds = persist_lds(s, VC, mode);
   if (s->hc) {
@@ -882,6 +1043,7 @@ static int persist_iters(ed_sector* s, int mode, bool basis, int niter, int firs
       if (mode == 1 || mode == 3) r.K = kron_args<true>(s);
       HIPCK(hipMemcpyAsync(s->d_prun, &r, sizeof(r), hipMemcpyHostToDevice, st));
       HIPCK(hipStreamSynchronize(st));  // r is a stack temporary
+      if (mode == 4) return fail(ED_ERR_UNSUPPORTED, "MODE 4 needs real H");
       return mode == 0 ? persist_launch_m<true, true, 0>(s, lds, st)
              : mode == 1 ? persist_launch_m<true, true, 1>(s, lds, st)
              : mode == 2 ? persist_launch_m<true, true, 2>(s, lds, st)
@@ -890,13 +1052,14 @@ static int persist_iters(ed_sector* s, int mode, bool basis, int niter, int firs
   }
   PersistRun<false> r;
   fill(r);
-  if (mode == 1 || mode == 3) r.K = kron_args<false>(s);
+  if (mode == 1 || mode == 3 || (mode == 4 && s->kron)) r.K = kron_args<false>(s);
   HIPCK(hipMemcpyAsync(s->d_prun, &r, sizeof(r), hipMemcpyHostToDevice, st));
   HIPCK(hipStreamSynchronize(st));  // r is a stack temporary
   return mode == 0 ? persist_launch_m<false, VC, 0>(s, lds, st)
          : mode == 1 ? persist_launch_m<false, VC, 1>(s, lds, st)
          : mode == 2 ? persist_launch_m<false, VC, 2>(s, lds, st)
-                     : persist_launch_m<false, VC, 3>(s, lds, st);
+         : mode == 3 ? persist_launch_m<false, VC, 3>(s, lds, st)
+                     : persist_launch_m<false, VC, 4>(s, lds, st);
 }
 
 static int persist_set_thresh(ed_sector* s, double thresh, hipStream_t st) {

@@ -41,12 +41,12 @@ struct PersistRun {
   const int64_t* sptr;
   const int32_t* cols;
   const H* vals;
-  // Kronecker tables (MODE 1)
+  // Kronecker tables (MODE 1, 3; MODE 4 direct diagonal)
   KronArgs<HC> K;
   int64_t dim;
-  void* R;           // in: start vector (first) or saved v; out: saved v
-  void* P;           // saved p
-  LancState* st;     // beta, iter, done, thresh
+  void* R;           // in: start vector (first) or saved unnormalised r_k; out: saved r_k
+  void* P;           // saved p = v_{k-1}
+  LancState* st;     // beta (norm of R), iter, done, thresh
   double* alpha;     // [niter_total]
   double* beta;      // [niter_total+1]
   void* basis;       // optional Krylov basis (column k = v_k), or null
@@ -54,18 +54,45 @@ struct PersistRun {
   const uint32_t* pk;   // [RPT*W][kPRegBlock] packed entries
   const H* dict;        // [ndict] distinct values, dict[0] = 0
   int ndict;
+  // Kronecker register layout (MODE 4): per-spin hop lists [deg][n] (target
+  // rank, value), zero-padded beyond a row's own degree
+  const int32_t* kupc;
+  const double* kupv;
+  const int32_t* kdwc;
+  const double* kdwv;
+  const double* kdiag;  // [dim] real diagonal, or null: from K (aup + adw + U)
+  int kdu, kdd, kdegu, kdegd;
   int niter;         // iterations in this launch
   int first;         // 1: R holds the unnormalised start vector
 };
 
-// TAIL=false drops the trailing barrier: the caller guarantees a barrier
-// between this read of ws and the next write to the same buffer (the
-// iteration alternates two buffers, separated by the step's barriers).
+// Wave sum on DPP row operations (no LDS traffic, ~6 dependent VALU steps
+// instead of 6 ds_bpermute round trips); the total lands in lane 63.
+template <int CTRL, int RM>
+__device__ __forceinline__ double dpp_add(double v) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  const int l2 = __builtin_amdgcn_update_dpp(0, lo, CTRL, RM, 0xF, false);
+  const int h2 = __builtin_amdgcn_update_dpp(0, hi, CTRL, RM, 0xF, false);
+  return v + __hiloint2double(h2, l2);
+}
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+  v = dpp_add<0xB1, 0xF>(v);   // quad_perm [1,0,3,2]
+  v = dpp_add<0x4E, 0xF>(v);   // quad_perm [2,3,0,1]
+  v = dpp_add<0x141, 0xF>(v);  // row_half_mirror
+  v = dpp_add<0x140, 0xF>(v);  // row_mirror: every lane holds its row's sum
+  v = dpp_add<0x142, 0xA>(v);  // row_bcast:15 -> rows 1, 3
+  v = dpp_add<0x143, 0xC>(v);  // row_bcast:31 -> rows 2, 3
+  return v;
+}
+
+// Deterministic block sum (fixed order), valid in every thread.  Must be
+// reached by all threads with full waves (DPP).  TAIL=false drops the
+// trailing barrier: the caller guarantees a barrier between this read of ws
+// and the next write to the same buffer.
 template <int NT = kPBlock, bool TAIL = true>
 __device__ __forceinline__ double pblock_sum(double v, double* ws) {
-  v = wave_sum(v);
-  const int wv = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) ws[wv] = v;
+  v = wave_sum_dpp(v);
+  if ((threadIdx.x & 63) == 63) ws[threadIdx.x >> 6] = v;
   __syncthreads();
   double t = 0.0;
 #pragma unroll
@@ -77,6 +104,47 @@ __device__ __forceinline__ double pblock_sum(double v, double* ws) {
 constexpr uint32_t kPkColBits = 17, kPkColMask = (1u << kPkColBits) - 1;
 constexpr uint32_t kPkOffMask = (1u << 14) - 1;  // dictionary byte offset (<= 16 KiB)
 
+// Rows of one thread: slot r holds row row0 + r*stride; slots r < nvalid are
+// basis rows (< dim), the others are padding rows in [dim, NT*RPT) whose LDS
+// entries, diagonal and matrix entries are zero, so every loop over r runs
+// without a branch (no per-row EXEC save / LDS wait).
+struct PRows {
+  int row0, stride, nvalid, iu;
+};
+
+template <int MODE, int RPT, int NT>
+__device__ __forceinline__ PRows persist_rows(int tid, int64_t dim, int du, int dd) {
+  PRows q;
+  if constexpr (MODE == 4) {
+    // Kronecker layout: thread (g, iu) owns rows (iw = g + G*r, iu), so its
+    // up-hop list is the same for all of its rows
+    const int G = NT / du;
+    if (tid < G * du) {
+      const int g = tid / du;
+      q.iu = tid - g * du;
+      q.row0 = g * du + q.iu;
+      q.stride = G * du;
+      q.nvalid = dd > g ? (dd - g + G - 1) / G : 0;
+    } else {  // idle lanes: private padding rows above G*du*RPT
+      q.iu = 0;
+      q.row0 = G * du * RPT + (tid - G * du);
+      q.stride = NT - G * du;
+      q.nvalid = 0;
+    }
+  } else {
+    q.iu = 0;
+    q.row0 = tid;
+    q.stride = NT;
+    q.nvalid = dim > tid ? (int)((dim - tid + NT - 1) / NT) : 0;
+  }
+  return q;
+}
+
+// One-workgroup plain Lanczos (.repo/PLAIN_LANCZOS.f90:87-118):
+//   w = H v_k - b_k v_{k-1};  a_k = <v_k, w>;  w -= a_k v_k;  b_{k+1} = |w|
+// LDS holds r_k = b_k v_k UNNORMALISED: w is stored as soon as a_k is known
+// (all gathers of the step are behind the alpha barrier) and the next step
+// scales H r by 1/b — two barriers per step (alpha, beta), one LDS vector.
 template <bool HC, bool VC, int MODE, int RPT, int E = 1, int NT = kPBlock>
 __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC>* __restrict__ runs) {
   using V = val_t<VC>;
@@ -84,13 +152,16 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC>* __res
   const PersistRun<HC>& a = runs[blockIdx.x];  // uniform: scalar loads, no VGPR copy
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ double ws[NT / 64];
-  __shared__ double ws2[NT / 64];  // beta's buffer: alpha/beta alternate, one barrier each
-  V* vl = (V*)smem;  // MODE 2 moves it behind the dictionary
+  __shared__ double ws2[NT / 64];
+  constexpr int VROWS = NT * RPT;  // LDS vector rows incl. padding
+  V* vl = (V*)smem;                // MODE 2/3 move it behind the dictionary
   const int64_t dim = a.dim;
   const int tid = threadIdx.x;
   V* Rg = (V*)a.R;
   V* Pg = (V*)a.P;
   LancState* st = a.st;
+  PRows q = persist_rows<MODE, RPT, NT>(tid, dim, a.kdu, a.kdd);
+#define PROW(r) (q.row0 + (r) * q.stride)
 
   // --- Kronecker tables into LDS (after v)
   const H* aup = nullptr;
@@ -104,10 +175,10 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC>* __res
   const double* uimp = nullptr;
   if constexpr (MODE == 1) {
     const KronArgs<HC>& K = a.K;
-    unsigned char* q = smem + ((dim * sizeof(V) + 15) & ~(int64_t)15);
+    unsigned char* qq = smem + (((int64_t)VROWS * sizeof(V) + 15) & ~(int64_t)15);
     auto carve = [&](int64_t bytes) {
-      unsigned char* r = q;
-      q += (bytes + 15) & ~(int64_t)15;
+      unsigned char* r = qq;
+      qq += (bytes + 15) & ~(int64_t)15;
       return r;
     };
     H* s_aup = (H*)carve(K.dimup * sizeof(H));
@@ -128,7 +199,7 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC>* __res
     impu = s_impu; impd = s_impd; uimp = s_uimp;
   }
 
-  // --- MODE 2: dictionary | v | diagonal in LDS, ELL entries in registers.
+  // --- MODE 2/3: dictionary | v | diagonal in LDS, ELL entries in registers.
   // (E is the row width W; the dictionary comes first so that its byte
   // offsets fit 14 bits; vl moves behind it)
   constexpr bool REG = MODE == 2 || MODE == 3;
@@ -141,8 +212,8 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC>* __res
     const int64_t dbytes = ((int64_t)a.ndict * sizeof(H) + 15) & ~(int64_t)15;
     for (int t = tid; t < a.ndict; t += NT) ((H*)smem)[t] = a.dict[t];
     vl = (V*)(smem + dbytes);
-    double* s_g = (double*)(smem + dbytes + ((dim * sizeof(V) + 15) & ~(int64_t)15));
-    for (int64_t t = tid; t < dim; t += NT) s_g[t] = re_of(a.diag[t]);
+    double* s_g = (double*)(smem + dbytes + (((int64_t)VROWS * sizeof(V) + 15) & ~(int64_t)15));
+    for (int t = tid; t < VROWS; t += NT) s_g[t] = t < dim ? re_of(a.diag[t]) : 0.0;
     dg = s_g;
 #pragma unroll
     for (int k = 0; k < RPT * E; k++) pk[k] = a.pk[k * NT + tid];
@@ -160,77 +231,118 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC>* __res
     if (tid == 0) sd[nup + ndw] = mk<HC>(0.0, 0.0);
     const int64_t dbytes = ((int64_t)(nup + ndw + 1) * sizeof(H) + 15) & ~(int64_t)15;
     vl = (V*)(smem + dbytes);
-    double* s_g = (double*)(smem + dbytes + ((dim * sizeof(V) + 15) & ~(int64_t)15));
-    for (int64_t t = tid; t < dim; t += NT) {
-      const int iw = (int)(t / du), iu = (int)(t - (int64_t)iw * du);
-      s_g[t] = re_of(add(add(K.aup[iu], K.adw[iw]), mk<HC>(K.uimp[K.impu[iu] * K.nimp + K.impd[iw]], 0.0)));
+    double* s_g = (double*)(smem + dbytes + (((int64_t)VROWS * sizeof(V) + 15) & ~(int64_t)15));
+    for (int t = tid; t < VROWS; t += NT) {
+      const int iw = t / du, iu = t - iw * du;
+      s_g[t] = t < dim ? re_of(add(add(K.aup[iu], K.adw[iw]), mk<HC>(K.uimp[K.impu[iu] * K.nimp + K.impd[iw]], 0.0)))
+                       : 0.0;
     }
     dg = s_g;
     const uint32_t hs = sizeof(H);
     const uint32_t zero = (uint32_t)((nup + ndw) * hs) << kPkColBits;
 #pragma unroll
     for (int r = 0; r < RPT; r++) {
-      const int64_t i = tid + (int64_t)r * NT;
-      const int iw = (int)(i / du), iu = (int)(i - (int64_t)iw * du);
+      const int i = PROW(r);
+      const int iw = i / du, iu = i - iw * du;
 #pragma unroll
       for (int e = 0; e < E; e++) {
         uint32_t wd = zero;
-        if (i < dim) {
+        if (r < q.nvalid) {
           if (e < K.degup) {
-            const int q = e * du + iu;
-            wd = (uint32_t)(iw * du + K.upc[q]) | (((uint32_t)q * hs) << kPkColBits);
+            const int qq = e * du + iu;
+            wd = (uint32_t)(iw * du + K.upc[qq]) | (((uint32_t)qq * hs) << kPkColBits);
           } else if (e < K.degup + K.degdw) {
-            const int q = (e - K.degup) * dd + iw;
-            wd = (uint32_t)(K.dwc[q] * du + iu) | (((uint32_t)(nup + q) * hs) << kPkColBits);
+            const int qq = (e - K.degup) * dd + iw;
+            wd = (uint32_t)(K.dwc[qq] * du + iu) | (((uint32_t)(nup + qq) * hs) << kPkColBits);
           }
         }
         pk[r * E + e] = wd;
       }
     }
   }
+  // --- MODE 4: Kronecker register layout (real H, real vectors).  Up-hop
+  // list (target rank as a byte offset inside the V row, value) once per
+  // thread; down-hop entries (LDS byte address, value) and the diagonal per
+  // row; no dictionary, no matrix byte in LDS.
+  constexpr bool KR = MODE == 4;
+  int ucol[KR ? E : 1];
+  double uval[KR ? E : 1];
+  int dcol[KR ? RPT * E : 1];
+  double dval[KR ? RPT * E : 1];
+  double dgr[KR ? RPT : 1];
+  if constexpr (KR) {
+    const int du = a.kdu, dd = a.kdd, G = NT / du;
+    const bool act = tid < G * du;
+    const int g = act ? tid / du : 0;
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+      const bool ok = act && e < a.kdegu;
+      ucol[e] = ok ? a.kupc[e * du + q.iu] * (int)sizeof(V) : 0;
+      uval[e] = ok ? a.kupv[e * du + q.iu] : 0.0;
+    }
+#pragma unroll
+    for (int r = 0; r < RPT; r++) {
+      const bool okr = r < q.nvalid;
+      const int iw = g + G * r;
+#pragma unroll
+      for (int e = 0; e < E; e++) {
+        const bool ok = okr && e < a.kdegd;
+        dcol[r * E + e] = (ok ? a.kdwc[e * dd + iw] * du + q.iu : 0) * (int)sizeof(V);
+        dval[r * E + e] = ok ? a.kdwv[e * dd + iw] : 0.0;
+      }
+      double d = 0.0;
+      if (okr) {
+        if (a.kdiag) {
+          d = a.kdiag[PROW(r)];
+        } else {
+          const KronArgs<HC>& K = a.K;
+          d = re_of(add(add(K.aup[q.iu], K.adw[iw]), mk<HC>(K.uimp[K.impu[q.iu] * K.nimp + K.impd[iw]], 0.0)));
+        }
+      }
+      dgr[r] = d;
+    }
+  }
 
   // --- state in
   // complex vectors in register modes keep p = v_{k-1} in global memory (own
   // rows only, read once and written once per step, L2-resident): it frees
-  // 4 VGPRs per row for the ELL words
+  // 4 VGPRs per row for the ELL words.  P is allocated with >= NT*RPT rows
+  // (p_rows, ed_lib.hip) so padding slots load and store without a guard.
   constexpr bool PG = REG && VC;
+  // real vectors keep their own rows of r_k in registers; complex ones
+  // re-read them from LDS (register budget of the ELL words)
+  constexpr bool UREG = !VC && (REG || KR);
+  V u[UREG ? RPT : 1];  // own rows of r_k (the LDS vector)
   V p[PG ? 1 : RPT];
-  uint32_t rix[RPT];  // Kronecker row index packed (iw << 16) | iu  (DimUp, DimDw < 2^16)
-  double b;
+  uint32_t rix[RPT];    // Kronecker row index packed (iw << 16) | iu  (DimUp, DimDw < 2^16)
+  double b, s;          // b_k and 1/b_k (s = 1/|r_0| on the first step, b_0 = 0)
   int it0;
   {
     double nrm = 0.0;
 #pragma unroll
     for (int r = 0; r < RPT; r++) {
-      const int64_t i = tid + (int64_t)r * NT;
-      if constexpr (!PG) p[r] = vzero<V>();
-      if (i < dim) {
-        V x = Rg[i];
-        vl[i] = x;
-        if (a.first) {
-          nrm += redot(x, x);
-          if constexpr (PG) Pg[i] = vzero<V>();
-        } else if constexpr (!PG) {
-          p[r] = Pg[i];
-        }
-        if constexpr (MODE == 1) {
-          const uint32_t w_ = (uint32_t)(i / a.K.dimup);
-          rix[r] = (w_ << 16) | (uint32_t)(i - (int64_t)w_ * a.K.dimup);
-        }
+      const int i = PROW(r);
+      const bool ok = r < q.nvalid;
+      const V x = ok ? Rg[i] : vzero<V>();
+      if constexpr (UREG) u[r] = x;
+      vl[i] = x;
+      if constexpr (!PG) p[r] = (ok && !a.first) ? Pg[i] : vzero<V>();
+      if (a.first) {
+        nrm += redot(x, x);
+        if constexpr (PG) Pg[i] = vzero<V>();  // padding rows too
+      }
+      if constexpr (MODE == 1) {
+        const uint32_t w_ = (uint32_t)(i / a.K.dimup);
+        rix[r] = ok ? (w_ << 16) | (uint32_t)(i - (int64_t)w_ * a.K.dimup) : 0u;
       }
     }
     if (a.first) {
-      double n2 = pblock_sum<NT>(nrm, ws);  // includes barrier: vl complete
+      const double n2 = pblock_sum<NT>(nrm, ws);
       if (n2 == 0.0) {                  // lanczos_plain_iteration: "norm =0!!"
         if (tid == 0) { st->iter = 0; st->done = 1; st->beta = 0.0; }
         return;
       }
-      const double inv = 1.0 / sqrt(n2);
-#pragma unroll
-      for (int r = 0; r < RPT; r++) {
-        const int64_t i = tid + (int64_t)r * NT;
-        if (i < dim) vl[i] = scl(inv, vl[i]);
-      }
+      s = 1.0 / sqrt(n2);
       b = 0.0;
       it0 = 0;
       if (tid == 0) {
@@ -240,6 +352,7 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC>* __res
       }
     } else {
       b = st->beta;
+      s = 1.0 / b;
       it0 = st->iter;
     }
     __syncthreads();
@@ -258,22 +371,29 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC>* __res
 #pragma unroll
       for (int e = 0; e < RPT * E; e++) asm volatile("" : "+v"(pk[e]));
     }
-    // ---- w = H v - b p ; alpha partial
+    if constexpr (KR) {
+#pragma unroll
+      for (int e = 0; e < RPT * E; e++) asm volatile("" : "+v"(dcol[e]));
+    }
+    // opaque row base: the per-row LDS / global addresses are re-derived each
+    // step (one integer op) instead of being hoisted into 1-2 VGPRs per row
+    asm volatile("" : "+v"(q.row0));
+    // ---- w = (H r_k)/b_k - b_k p ; alpha partial
     V w[RPT];
     double ap = 0.0;
 #pragma unroll
     for (int r = 0; r < RPT; r++) {
-      const int64_t i = tid + (int64_t)r * NT;
-      w[r] = vzero<V>();
-      if (i < dim) {
-        const V xi = vl[i];
-        V acc;
-        if constexpr (MODE == 0) {
-          const int64_t s = i >> 6, s0 = a.sptr[s];
-          const int wd = (int)((a.sptr[s + 1] - s0) >> 6);
+      const int i = PROW(r);
+      const V ur = UREG ? u[r] : vl[i];
+      V acc;
+      if constexpr (MODE == 0) {
+        acc = vzero<V>();
+        if (r < q.nvalid) {
+          const int64_t sl = i >> 6, s0 = a.sptr[sl];
+          const int wd = (int)((a.sptr[sl + 1] - s0) >> 6);
           const int32_t* cp = a.cols + s0 + (i & 63);
           const H* vp = a.vals + s0 + (i & 63);
-          acc = add(vzero<V>(), mul(a.diag[i], xi));
+          acc = add(vzero<V>(), mul(a.diag[i], ur));
           for (int k0 = 0; k0 < wd; k0 += kPChunk) {
             int32_t c[kPChunk];
             H h[kPChunk];
@@ -286,68 +406,77 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC>* __res
             for (int kk = 0; kk < kPChunk; kk++)
               if (k0 + kk < wd) acc = add(acc, mul(h[kk], vl[c[kk]]));
           }
-        } else if constexpr (REG) {
-          acc = mul(dg[i], xi);
+        }
+      } else if constexpr (REG) {
+        acc = mul(dg[i], ur);
 #pragma unroll
-          for (int e = 0; e < E; e++) {
-            const uint32_t x = pk[r * E + e];
-            const H h = *(const H*)(dct + ((x >> kPkColBits) & kPkOffMask));
-            acc = fmac(acc, h, vl[x & kPkColMask]);
-          }
-        } else {
+        for (int e = 0; e < E; e++) {
+          const uint32_t x = pk[r * E + e];
+          const H h = *(const H*)(dct + ((x >> kPkColBits) & kPkOffMask));
+          acc = fmac(acc, h, vl[x & kPkColMask]);
+        }
+      } else if constexpr (KR) {
+        acc = mul(dgr[r], ur);
+        const unsigned char* rb = (const unsigned char*)(vl + (i - q.iu));  // row iw of V
+#pragma unroll
+        for (int e = 0; e < E; e++) acc = fmac(acc, uval[e], *(const V*)(rb + ucol[e]));
+#pragma unroll
+        for (int e = 0; e < E; e++)
+          acc = fmac(acc, dval[r * E + e], *(const V*)((const unsigned char*)vl + dcol[r * E + e]));
+      } else {
+        acc = vzero<V>();
+        if (r < q.nvalid) {
           const int du = (int)a.K.dimup, dd = (int)a.K.dimdw;
           const int iwr = (int)(rix[r] >> 16), iur = (int)(rix[r] & 0xffffu);
           auto d = add(add(aup[iur], adw[iwr]), mk<HC>(uimp[impu[iur] * a.K.nimp + impd[iwr]], 0.0));
-          acc = mul(d, xi);
+          acc = mul(d, ur);
           const V* xrow = vl + iwr * du;
           for (int kk = 0; kk < a.K.degup; kk++) {
-            const int q = kk * du + iur;
-            acc = add(acc, mul(upv[q], xrow[upc[q]]));
+            const int qq = kk * du + iur;
+            acc = add(acc, mul(upv[qq], xrow[upc[qq]]));
           }
           for (int kk = 0; kk < a.K.degdw; kk++) {
-            const int q = kk * dd + iwr;
-            acc = add(acc, mul(dwv[q], vl[dwc[q] * du + iur]));
+            const int qq = kk * dd + iwr;
+            acc = add(acc, mul(dwv[qq], vl[dwc[qq] * du + iur]));
           }
         }
-        if constexpr (PG) w[r] = sub(acc, scl(b, Pg[i]));
-        else w[r] = sub(acc, scl(b, p[r]));
-        ap += redot(xi, w[r]);
-        if (basis) basis[(int64_t)it * dim + i] = xi;
       }
+      const V x = scl(s, ur);  // v_k
+      V pr;
+      if constexpr (PG) pr = Pg[i];  // P has >= NT*RPT rows, padding zero
+      else pr = p[r];
+      w[r] = sub(scl(s, acc), scl(b, pr));
+      ap += redot(x, w[r]);
     }
-    // alpha reads ws, beta ws2; the barrier inside the beta reduction and the
-    // end-of-step barrier separate each read from the next write of its buffer
+    // alpha barrier: every gather of r_k in LDS is done -> r_k's slots may
+    // be overwritten by w below
     const double alpha = pblock_sum<NT, false>(ap, ws);
-    // ---- w -= alpha v ; beta
+    // ---- w -= alpha v ; beta ; p <- v_k ; publish w (= r_{k+1}) in LDS
     double bp = 0.0;
 #pragma unroll
     for (int r = 0; r < RPT; r++) {
-      const int64_t i = tid + (int64_t)r * NT;
-      if (i < dim) {
-        w[r] = sub(w[r], scl(alpha, vl[i]));
-        bp += redot(w[r], w[r]);
+      const int i = PROW(r);
+      const V x = scl(s, UREG ? u[r] : vl[i]);
+      w[r] = sub(w[r], scl(alpha, x));
+      bp += redot(w[r], w[r]);
+      if (basis && r < q.nvalid) basis[(int64_t)it * dim + i] = x;  // column k = v_k
+      if constexpr (PG) {
+        Pg[i] = x;
+      } else {
+        p[r] = x;
       }
+      if constexpr (UREG) u[r] = w[r];
+      vl[i] = w[r];
     }
+    // beta barrier: also publishes r_{k+1}
     const double bn = sqrt(pblock_sum<NT, false>(bp, ws2));
     if (tid == 0) {
       alpha_out[it] = alpha;
       beta_out[it + 1] = bn;
     }
-    const bool stop = bn < thresh;
-    // ---- p <- v ; v <- w / b
-    const double inv = 1.0 / bn;
-#pragma unroll
-    for (int r = 0; r < RPT; r++) {
-      const int64_t i = tid + (int64_t)r * NT;
-      if (i < dim) {
-        if constexpr (PG) Pg[i] = vl[i];
-        else p[r] = vl[i];
-        vl[i] = scl(inv, w[r]);
-      }
-    }
     b = bn;
-    __syncthreads();
-    if (stop) {
+    s = 1.0 / bn;
+    if (bn < thresh) {
       if (tid == 0) {
         st->done = 1;
         st->iter = it + 1;
@@ -356,19 +485,19 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC>* __res
       return;
     }
   }
-  // ---- state out
+  // ---- state out: R = r_k (unnormalised), P = v_{k-1}, st->beta = b_k
 #pragma unroll
   for (int r = 0; r < RPT; r++) {
-    const int64_t i = tid + (int64_t)r * NT;
-    if (i < dim) {
-      Rg[i] = vl[i];
-      if constexpr (!PG) Pg[i] = p[r];
+    if (r < q.nvalid) {
+      Rg[PROW(r)] = UREG ? u[r] : vl[PROW(r)];
+      if constexpr (!PG) Pg[PROW(r)] = p[r];
     }
   }
   if (tid == 0) {
     st->iter = it0 + a.niter;
     st->beta = b;
   }
+#undef PROW
 }
 
 }  // namespace edg

@@ -84,7 +84,7 @@ def test_real_lanczos_c2():
         assert abs(e1 - e0) <= 1e-10 * abs(e0)
 
 
-@pytest.mark.parametrize("path", ["stored_l2", "stored_reg", "kron_lds", "kron_reg"])
+@pytest.mark.parametrize("path", ["stored_l2", "stored_reg", "stored_kr", "kron_lds", "kron_reg", "kron_kr"])
 def test_persistent_matches_multikernel(path, monkeypatch):
     """Same start vector, same sector: the two recurrences agree step by step
     (first 40 steps to 1e-9; only the reduction order differs)."""
@@ -97,8 +97,11 @@ def test_persistent_matches_multikernel(path, monkeypatch):
         monkeypatch.setenv("ED_GPU_PERSIST_STORED", "1")
     if path == "kron_lds":
         monkeypatch.setenv("ED_GPU_NO_PREG", "1")
+    if path in ("stored_reg", "kron_reg"):
+        monkeypatch.setenv("ED_GPU_NO_PKRON", "1")
     with Sector(cfg, 4, 4, real=True, **kw) as S:
-        want = {"stored_l2": 0, "stored_reg": 2, "kron_lds": 1, "kron_reg": 3}[path]
+        want = {"stored_l2": 0, "stored_reg": 2, "stored_kr": 4, "kron_lds": 1, "kron_reg": 3,
+                "kron_kr": 4}[path]
         assert S.lanc_mode(real=True) == want
         v0 = np.sin(np.arange(1, S.dim + 1, dtype=np.float64))
         a1, b1, n1 = S.lanc_tridiag(v0, 60)
