@@ -417,12 +417,14 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC>* __res
         }
       } else if constexpr (KR) {
         acc = mul(dgr[r], ur);
+        {
         const unsigned char* rb = (const unsigned char*)(vl + (i - q.iu));  // row iw of V
 #pragma unroll
         for (int e = 0; e < E; e++) acc = fmac(acc, uval[e], *(const V*)(rb + ucol[e]));
 #pragma unroll
         for (int e = 0; e < E; e++)
           acc = fmac(acc, dval[r * E + e], *(const V*)((const unsigned char*)vl + dcol[r * E + e]));
+        }
       } else {
         acc = vzero<V>();
         if (r < q.nvalid) {

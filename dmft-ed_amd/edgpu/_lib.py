@@ -11,6 +11,9 @@ import sys
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(_PKG_ROOT, "libedgpu.so")
+# experiment hook (tools/): load a variant build of the same library
+if os.environ.get("ED_GPU_LIB_VARIANT"):
+    LIB_PATH = os.path.join(_PKG_ROOT, "libedgpu_" + os.environ["ED_GPU_LIB_VARIANT"] + ".so")
 
 ED_STORED, ED_DIRECT, ED_REAL = 0x1, 0x2, 0x4
 ED_OK = 0
