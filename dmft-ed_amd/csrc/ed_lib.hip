@@ -106,7 +106,7 @@ struct ed_sector {
   int64_t bytes = 0;
   std::vector<void*> allocs;
   // persistent one-workgroup Lanczos (small sectors)
-  void* d_prun = nullptr;   // PersistRun<HC> in device memory
+  double pthresh = 0.0;     // breakdown threshold of the current persistent run
   // register-resident stored matrix for the persistent kernel (MODE 2)
   int preg_E = 0;           // 0 not built, -1 ineligible, else ELL row width W
   int preg_rpt = 0;         // rows per thread (template value)
@@ -941,7 +941,7 @@ static int64_t persist_lds(const ed_sector* s, int vc, int mode) {
 }
 
 template <bool HC, bool VC, int MODE, int RPT, int E = 1>
-static int persist_launch_t(ed_sector* s, int64_t lds, hipStream_t st) {
+static int persist_launch_t(ed_sector* s, const PersistRun<HC>& run, int64_t lds, hipStream_t st) {
   if constexpr ((MODE == 2 || MODE == 3) && RPT * E > preg_cap(HC, VC)) {
     return fail(ED_ERR_UNSUPPORTED, "register-resident ELL exceeds the spill-free budget");
   } else if constexpr (MODE == 4 && (HC || VC || !pkr_fits(E, RPT))) {
@@ -950,51 +950,51 @@ static int persist_launch_t(ed_sector* s, int64_t lds, hipStream_t st) {
   constexpr int NT = MODE >= 2 ? kPRegBlock : kPBlock;
   auto fn = k_lanc_persist<HC, VC, MODE, RPT, E, NT>;
   HIPCK(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(fn, dim3(1), dim3(NT), (size_t)lds, st, (const PersistRun<HC>*)s->d_prun);
+  hipLaunchKernelGGL(fn, dim3(1), dim3(NT), (size_t)lds, st, run);
   HIPCK(hipGetLastError());
   return ED_OK;
   }
 }
 
 template <bool HC, bool VC, int MODE, int W>
-static int persist_launch_e(ed_sector* s, int64_t lds, hipStream_t st) {
+static int persist_launch_e(ed_sector* s, const PersistRun<HC>& run, int64_t lds, hipStream_t st) {
   switch (MODE == 2 ? s->preg_rpt : MODE == 3 ? s->kreg_rpt : s->pkr_rpt) {
-    case 2: return persist_launch_t<HC, VC, MODE, 2, W>(s, lds, st);
-    case 4: return persist_launch_t<HC, VC, MODE, 4, W>(s, lds, st);
-    case 6: return persist_launch_t<HC, VC, MODE, 6, W>(s, lds, st);
-    case 8: return persist_launch_t<HC, VC, MODE, 8, W>(s, lds, st);
-    default: return persist_launch_t<HC, VC, MODE, 10, W>(s, lds, st);
+    case 2: return persist_launch_t<HC, VC, MODE, 2, W>(s, run, lds, st);
+    case 4: return persist_launch_t<HC, VC, MODE, 4, W>(s, run, lds, st);
+    case 6: return persist_launch_t<HC, VC, MODE, 6, W>(s, run, lds, st);
+    case 8: return persist_launch_t<HC, VC, MODE, 8, W>(s, run, lds, st);
+    default: return persist_launch_t<HC, VC, MODE, 10, W>(s, run, lds, st);
   }
 }
 
 template <bool HC, bool VC, int MODE>
-static int persist_launch_m(ed_sector* s, int64_t lds, hipStream_t st) {
+static int persist_launch_m(ed_sector* s, const PersistRun<HC>& run, int64_t lds, hipStream_t st) {
   if constexpr (MODE == 4) {
     if constexpr (HC || VC) {
       return fail(ED_ERR_UNSUPPORTED, "MODE 4 needs real H and vectors");
     } else {
-      return s->pkr_E == 4 ? persist_launch_e<HC, VC, 4, 4>(s, lds, st)
-                           : persist_launch_e<HC, VC, 4, 8>(s, lds, st);
+      return s->pkr_E == 4 ? persist_launch_e<HC, VC, 4, 4>(s, run, lds, st)
+                           : persist_launch_e<HC, VC, 4, 8>(s, run, lds, st);
     }
   } else if constexpr (MODE >= 2) {
     switch (MODE == 2 ? s->preg_E : s->kreg_W) {
-      case 8: return persist_launch_e<HC, VC, MODE, 8>(s, lds, st);
-      case 12: return persist_launch_e<HC, VC, MODE, 12>(s, lds, st);
-      case 14: return persist_launch_e<HC, VC, MODE, 14>(s, lds, st);
-      default: return persist_launch_e<HC, VC, MODE, 16>(s, lds, st);
+      case 8: return persist_launch_e<HC, VC, MODE, 8>(s, run, lds, st);
+      case 12: return persist_launch_e<HC, VC, MODE, 12>(s, run, lds, st);
+      case 14: return persist_launch_e<HC, VC, MODE, 14>(s, run, lds, st);
+      default: return persist_launch_e<HC, VC, MODE, 16>(s, run, lds, st);
     }
   } else {
   switch (persist_rpt01(s->dim)) {
-    case 1: return persist_launch_t<HC, VC, MODE, 1>(s, lds, st);
-    case 2: return persist_launch_t<HC, VC, MODE, 2>(s, lds, st);
-    case 3: return persist_launch_t<HC, VC, MODE, 3>(s, lds, st);
-    case 4: return persist_launch_t<HC, VC, MODE, 4>(s, lds, st);
-    case 5: return persist_launch_t<HC, VC, MODE, 5>(s, lds, st);
-    case 6: return persist_launch_t<HC, VC, MODE, 6>(s, lds, st);
-    case 8: return persist_launch_t<HC, VC, MODE, 8>(s, lds, st);
-    case 10: return persist_launch_t<HC, VC, MODE, 10>(s, lds, st);
-    case 12: return persist_launch_t<HC, VC, MODE, 12>(s, lds, st);
-    default: return persist_launch_t<HC, VC, MODE, 16>(s, lds, st);
+    case 1: return persist_launch_t<HC, VC, MODE, 1>(s, run, lds, st);
+    case 2: return persist_launch_t<HC, VC, MODE, 2>(s, run, lds, st);
+    case 3: return persist_launch_t<HC, VC, MODE, 3>(s, run, lds, st);
+    case 4: return persist_launch_t<HC, VC, MODE, 4>(s, run, lds, st);
+    case 5: return persist_launch_t<HC, VC, MODE, 5>(s, run, lds, st);
+    case 6: return persist_launch_t<HC, VC, MODE, 6>(s, run, lds, st);
+    case 8: return persist_launch_t<HC, VC, MODE, 8>(s, run, lds, st);
+    case 10: return persist_launch_t<HC, VC, MODE, 10>(s, run, lds, st);
+    case 12: return persist_launch_t<HC, VC, MODE, 12>(s, run, lds, st);
+    default: return persist_launch_t<HC, VC, MODE, 16>(s, run, lds, st);
   }
   }
 }
@@ -1003,7 +1003,6 @@ static int persist_launch_m(ed_sector* s, int64_t lds, hipStream_t st) {
 template <bool VC>
 static int persist_iters(ed_sector* s, int mode, bool basis, int niter, int first, hipStream_t st) {
   LancWS& w = s->ws;
-  if (!s->d_prun) CK(dalloc(s, &s->d_prun, sizeof(PersistRun<true>)));
   auto fill = [&](auto& r) {
     using RT = std::remove_reference_t<decltype(r)>;
     using HT = std::remove_const_t<std::remove_pointer_t<decltype(r.diag)>>;
@@ -1021,6 +1020,7 @@ static int persist_iters(ed_sector* s, int mode, bool basis, int niter, int firs
     r.basis = basis ? w.basis : nullptr;
     r.niter = niter;
     r.first = first;
+    r.thresh = s->pthresh;
     r.pk = s->d_pk;
     r.dict = (const HT*)s->d_dict;
     r.ndict = s->ndict;
@@ -1041,35 +1041,30 @@ static int persist_iters(ed_sector* s, int mode, bool basis, int niter, int firs
       PersistRun<true> r;
       fill(r);
       if (mode == 1 || mode == 3) r.K = kron_args<true>(s);
-      HIPCK(hipMemcpyAsync(s->d_prun, &r, sizeof(r), hipMemcpyHostToDevice, st));
-      HIPCK(hipStreamSynchronize(st));  // r is a stack temporary
       if (mode == 4) return fail(ED_ERR_UNSUPPORTED, "MODE 4 needs real H");
-      return mode == 0 ? persist_launch_m<true, true, 0>(s, lds, st)
-             : mode == 1 ? persist_launch_m<true, true, 1>(s, lds, st)
-             : mode == 2 ? persist_launch_m<true, true, 2>(s, lds, st)
-                         : persist_launch_m<true, true, 3>(s, lds, st);
+      return mode == 0 ? persist_launch_m<true, true, 0>(s, r, lds, st)
+             : mode == 1 ? persist_launch_m<true, true, 1>(s, r, lds, st)
+             : mode == 2 ? persist_launch_m<true, true, 2>(s, r, lds, st)
+                         : persist_launch_m<true, true, 3>(s, r, lds, st);
     }
   }
   PersistRun<false> r;
   fill(r);
   if (mode == 1 || mode == 3 || (mode == 4 && s->kron)) r.K = kron_args<false>(s);
-  HIPCK(hipMemcpyAsync(s->d_prun, &r, sizeof(r), hipMemcpyHostToDevice, st));
-  HIPCK(hipStreamSynchronize(st));  // r is a stack temporary
-  return mode == 0 ? persist_launch_m<false, VC, 0>(s, lds, st)
-         : mode == 1 ? persist_launch_m<false, VC, 1>(s, lds, st)
-         : mode == 2 ? persist_launch_m<false, VC, 2>(s, lds, st)
-         : mode == 3 ? persist_launch_m<false, VC, 3>(s, lds, st)
-                     : persist_launch_m<false, VC, 4>(s, lds, st);
+  return mode == 0 ? persist_launch_m<false, VC, 0>(s, r, lds, st)
+         : mode == 1 ? persist_launch_m<false, VC, 1>(s, r, lds, st)
+         : mode == 2 ? persist_launch_m<false, VC, 2>(s, r, lds, st)
+         : mode == 3 ? persist_launch_m<false, VC, 3>(s, r, lds, st)
+                     : persist_launch_m<false, VC, 4>(s, r, lds, st);
 }
 
 static int persist_set_thresh(ed_sector* s, double thresh, hipStream_t st) {
-  LancState h;
-  memset(&h, 0, sizeof(h));
-  h.thresh = thresh;
-  HIPCK(hipMemcpyAsync(s->ws.st, &h, sizeof(h), hipMemcpyHostToDevice, st));
+  // stream-ordered, no host sync: the threshold travels in the kernel
+  // argument, the kernel initialises the LancState fields on its first launch
+  s->pthresh = thresh;
+  HIPCK(hipMemsetAsync(s->ws.st, 0, sizeof(LancState), st));
   HIPCK(hipMemsetAsync(s->ws.beta, 0, (s->ws.cap + 2) * sizeof(double), st));
   HIPCK(hipMemsetAsync(s->ws.alpha, 0, (s->ws.cap + 2) * sizeof(double), st));
-  HIPCK(hipStreamSynchronize(st));
   return ED_OK;
 }
 
@@ -1737,13 +1732,14 @@ int ed_sector_lanc_run(ed_sector* s, int32_t vtype, const void* v0_dev, int32_t 
     rc = d.iters(niter, true);
     HIPCK(hipEventRecord(e1, d.st));
   }
+  // one host sync for the run and both coefficient copies
+  if (rc == ED_OK && alfa) HIPCK(hipMemcpyAsync(alfa, s->ws.alpha, niter * sizeof(double), hipMemcpyDeviceToHost, d.st));
+  if (rc == ED_OK && beta) HIPCK(hipMemcpyAsync(beta, s->ws.beta, niter * sizeof(double), hipMemcpyDeviceToHost, d.st));
   HIPCK(hipStreamSynchronize(d.st));
   if (ms && rc == ED_OK) HIPCK(hipEventElapsedTime(ms, e0, e1));
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   CK(rc);
-  if (alfa) CK(dcopy(s, alfa, s->ws.alpha, niter * sizeof(double), hipMemcpyDeviceToHost));
-  if (beta) CK(dcopy(s, beta, s->ws.beta, niter * sizeof(double), hipMemcpyDeviceToHost));
   return ED_OK;
 }
 

@@ -2,28 +2,25 @@
 //
 // For sectors whose Lanczos vector fits in LDS (configs[1]: dim 4,900 real =
 // 39 KB) the per-iteration cost of the multi-kernel recurrence is launch and
-// grid-reduction latency, not bandwidth (≈10 µs per iteration for 4,900 rows).
-// Here one 1024-thread workgroup (16 wavefronts, one CU) runs many
-// iterations of the .repo/PLAIN_LANCZOS.f90:87-118 recurrence without leaving
-// the CU:
-//   * v (the current normalised Lanczos vector) lives in LDS and is gathered
-//     by the H·v; p = v_{k-1} and w live in registers of the thread that owns
-//     the row (row i = tid + r*1024, r < RPT);
-//   * H is the stored SELL-64 matrix streamed from L2 (MODE 0, same element
-//     order as k_spmv -> same H·v bits), the Kronecker tables copied into
-//     LDS (MODE 1, normal mode without Jx/Jp), or the stored matrix held in
-//     REGISTERS (MODE 2, ELL layout): row i = tid + r*NT keeps its W
-//     off-diagonal entries as 32-bit words {col:17 | value byte offset:14}
-//     into a dictionary of the distinct values (hoppings/exchange: a few
-//     dozen), padded with the dictionary's 0.0; diagonal, dictionary and v in
-//     LDS.  No matrix byte leaves the CU after the first iteration and the
-//     entry loop has no branch, so every gather of a row is in flight at once;
-//     MODE 3 is the matrix-free twin: the same words generated in-kernel
-//     from the Kronecker hop tables (dictionary = the tables' values);
-//   * alpha and beta are block reductions (wave shuffles + 16-entry LDS),
-//     three barriers per iteration, no global synchronisation.
-// Independent runs (GF seeds, sector replicas) use one workgroup each
-// (blockIdx.x indexes PersistRun[]), so up to 256 chains run side by side.
+// grid-reduction latency, not bandwidth (≈9 µs per iteration for 4,900 rows).
+// Here one workgroup (one CU) runs many iterations of the
+// .repo/PLAIN_LANCZOS.f90:87-118 recurrence without leaving the CU:
+//   * r_k = b_k v_k (unnormalised) lives in LDS and is gathered by the H·v;
+//     p = v_{k-1}, w and (real vectors) the own rows of r_k live in registers
+//     of the thread that owns the row; every thread owns RPT row slots, padded
+//     to NT*RPT rows with zero entries so that no per-row branch exists;
+//   * H is the stored SELL-64 matrix streamed from L2 (MODE 0), the Kronecker
+//     tables copied into LDS (MODE 1, normal mode without Jx/Jp), the stored
+//     matrix held in REGISTERS as ELL words {col:17 | value byte offset:14}
+//     into an LDS dictionary of the distinct values (MODE 2), the same words
+//     generated in-kernel from the Kronecker hop tables (MODE 3), or the
+//     Kronecker register layout (MODE 4, real H and vectors): thread (g, iu)
+//     owns rows (iw = g + G*r, iu), keeps its up-hop list (target, value) once
+//     and per row the down-hop entries and the diagonal — no dictionary, the
+//     down-hop gathers of a wavefront are contiguous;
+//   * alpha and beta are block reductions (DPP wave sums + one LDS stage),
+//     two barriers per iteration, no global synchronisation.
+// configs[1]: MODE 4 2.4 µs per step (MODE 2 4.4 µs before this layout).
 #pragma once
 #include "ed_kernels.hpp"
 
@@ -46,7 +43,7 @@ struct PersistRun {
   int64_t dim;
   void* R;           // in: start vector (first) or saved unnormalised r_k; out: saved r_k
   void* P;           // saved p = v_{k-1}
-  LancState* st;     // beta (norm of R), iter, done, thresh
+  LancState* st;     // beta (norm of R), iter, done
   double* alpha;     // [niter_total]
   double* beta;      // [niter_total+1]
   void* basis;       // optional Krylov basis (column k = v_k), or null
@@ -62,6 +59,7 @@ struct PersistRun {
   const double* kdwv;
   const double* kdiag;  // [dim] real diagonal, or null: from K (aup + adw + U)
   int kdu, kdd, kdegu, kdegd;
+  double thresh;     // breakdown threshold (|b| < thresh stops)
   int niter;         // iterations in this launch
   int first;         // 1: R holds the unnormalised start vector
 };
@@ -146,10 +144,9 @@ __device__ __forceinline__ PRows persist_rows(int tid, int64_t dim, int du, int 
 // (all gathers of the step are behind the alpha barrier) and the next step
 // scales H r by 1/b — two barriers per step (alpha, beta), one LDS vector.
 template <bool HC, bool VC, int MODE, int RPT, int E = 1, int NT = kPBlock>
-__global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC>* __restrict__ runs) {
+__global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
   using V = val_t<VC>;
   using H = val_t<HC>;
-  const PersistRun<HC>& a = runs[blockIdx.x];  // uniform: scalar loads, no VGPR copy
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ double ws[NT / 64];
   __shared__ double ws2[NT / 64];
@@ -358,7 +355,7 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC>* __res
     __syncthreads();
   }
   if (st->done && !a.first) return;
-  const double thresh = st->thresh;   // hoisted: a global read per iteration costs ~1 µs
+  const double thresh = a.thresh;
   double* const alpha_out = a.alpha;
   double* const beta_out = a.beta;
   V* const basis = (V*)a.basis;
