@@ -747,6 +747,87 @@ static int pkr_geom(ed_sector* s, int64_t du, int64_t dd, int degu, int degd) {
   return 1;
 }
 
+// MODE 4 up-hop slot order.  Slot e of every lane is gathered by one
+// ds_read_b64 per row; its 32-lane halves hit bank pair (g*DimUp + target)
+// mod 32 (the iw*DimUp part common to a wave's rows drops out, so one order
+// serves every row slot r), and each extra distinct address on a bank pair
+// costs one LDS cycle.  The up list of iu is shared by the G lanes (g, iu):
+// permute each list (all orders for E=4, pairwise swaps for E=8) to minimise
+// the summed conflict cycles over the halves containing one of its lanes.
+// Entries stay the same (target, value) pairs, so H is unchanged; only the
+// per-row summation order moves.  configs[1]: 1150 -> ~890 LDS cycles/step.
+using PkrHop = std::pair<int32_t, uint64_t>;
+static void pkr_order_up(std::vector<std::vector<PkrHop>>& ul, int du, int E) {
+  const int G = kPRegBlock / du;
+  for (auto& l : ul) l.resize(E, PkrHop{0, 0});  // padding: (col 0, 0.0) reads the row base
+  auto half_cost = [&](int h, int e) {
+    int nb[32] = {0}, cyc = 0;
+    int seen[32][32];
+    for (int l = 0; l < 32; l++) {
+      const int t = 32 * h + l;
+      if (t >= G * du) break;
+      const int g = t / du, iu = t - g * du;
+      const int addr = g * du + ul[iu][e].first, b = addr & 31;
+      bool dup = false;
+      for (int k = 0; k < nb[b]; k++) dup |= seen[b][k] == addr;
+      if (!dup) { seen[b][nb[b]++] = addr; cyc = std::max(cyc, nb[b]); }
+    }
+    return cyc;
+  };
+  auto cost_of = [&](int iu) {
+    int c = 0;
+    for (int g = 0; g < G; g++) {
+      const int h = (g * du + iu) / 32;
+      for (int e = 0; e < E; e++) c += half_cost(h, e);
+    }
+    return c;
+  };
+  for (int sweep = 0; sweep < 3; sweep++) {
+    bool moved = false;
+    for (int iu = 0; iu < du; iu++) {
+      std::vector<PkrHop>& l = ul[iu];
+      int best = cost_of(iu);
+      if (E <= 4) {
+        std::vector<PkrHop> cur = l, keep = l;
+        std::sort(cur.begin(), cur.end());
+        do {
+          l = cur;
+          const int c = cost_of(iu);
+          if (c < best) { best = c; keep = cur; moved = true; }
+        } while (std::next_permutation(cur.begin(), cur.end()));
+        l = keep;
+      } else {
+        for (int a = 0; a < E; a++)
+          for (int b = a + 1; b < E; b++) {
+            std::swap(l[a], l[b]);
+            const int c = cost_of(iu);
+            if (c < best) { best = c; moved = true; } else { std::swap(l[a], l[b]); }
+          }
+      }
+    }
+    if (!moved) break;
+  }
+}
+
+static int pkr_upload(ed_sector* s, const std::vector<std::vector<PkrHop>>& L, int deg, int64_t n,
+                      const int32_t** dc, const double** dv) {
+  std::vector<int32_t> c((size_t)std::max(deg, 1) * n, 0);
+  std::vector<double> v((size_t)std::max(deg, 1) * n, 0.0);
+  for (int64_t r = 0; r < n; r++)
+    for (size_t e = 0; e < L[r].size() && (int)e < deg; e++) {
+      c[e * n + r] = L[r][e].first;
+      memcpy(&v[e * n + r], &L[r][e].second, 8);
+    }
+  int32_t* pc;
+  void* pv;
+  CK(upload(s, &pc, c));
+  CK(dalloc(s, &pv, v.size() * 8));
+  CK(dcopy(s, pv, v.data(), v.size() * 8, hipMemcpyHostToDevice));
+  *dc = pc;
+  *dv = (const double*)pv;
+  return ED_OK;
+}
+
 // MODE 4 tables of a stored sector: read back from the stored SELL matrix
 // and accepted only when it has the Kronecker form H = D + Hup(x)1 + 1(x)Hdw
 // on the DimDw x DimUp view (row = iw*DimUp + iu): every entry of row
@@ -770,7 +851,7 @@ static int build_pkron_stored(ed_sector* s) {
   CK(dcopy(s, sptr.data(), s->d_sptr, (ns + 1) * 8, hipMemcpyDeviceToHost));
   CK(dcopy(s, sc.data(), s->d_cols, slots * 4, hipMemcpyDeviceToHost));
   CK(dcopy(s, sv.data(), s->d_vals, slots * 8, hipMemcpyDeviceToHost));
-  using Hop = std::pair<int32_t, uint64_t>;
+  using Hop = PkrHop;
   std::vector<std::vector<Hop>> ul(du), dl(dd);
   std::vector<char> useen(du, 0), dseen(dd, 0);
   std::vector<Hop> lu, ld;
@@ -794,26 +875,10 @@ static int build_pkron_stored(ed_sector* s) {
   for (auto& l : ul) degu = std::max<int>(degu, (int)l.size());
   for (auto& l : dl) degd = std::max<int>(degd, (int)l.size());
   if (pkr_geom(s, du, dd, degu, degd) < 0) return -1;
-  auto table = [&](const std::vector<std::vector<Hop>>& L, int deg, int64_t n, const int32_t** dc,
-                   const double** dv) {
-    std::vector<int32_t> c((size_t)std::max(deg, 1) * n, 0);
-    std::vector<double> v((size_t)std::max(deg, 1) * n, 0.0);
-    for (int64_t r = 0; r < n; r++)
-      for (size_t e = 0; e < L[r].size(); e++) {
-        c[e * n + r] = L[r][e].first;
-        memcpy(&v[e * n + r], &L[r][e].second, 8);
-      }
-    int32_t* pc;
-    void* pv;
-    CK(upload(s, &pc, c));
-    CK(dalloc(s, &pv, v.size() * 8));
-    CK(dcopy(s, pv, v.data(), v.size() * 8, hipMemcpyHostToDevice));
-    *dc = pc;
-    *dv = (const double*)pv;
-    return ED_OK;
-  };
-  CK(table(ul, degu, du, &s->d_kupc, &s->d_kupv));
-  CK(table(dl, degd, dd, &s->d_kdwc, &s->d_kdwv));
+  pkr_order_up(ul, (int)du, s->pkr_E);
+  s->pkr_degu = s->pkr_E;
+  CK(pkr_upload(s, ul, s->pkr_degu, du, &s->d_kupc, &s->d_kupv));
+  CK(pkr_upload(s, dl, degd, dd, &s->d_kdwc, &s->d_kdwv));
   s->d_kdiag = (const double*)s->d_diag;
   s->pkr_state = 1;
   return 1;
@@ -828,8 +893,25 @@ static int build_pkron_direct(ed_sector* s) {
   if (s->hc || !s->kron || !s->K.diag_real) return -1;
   const KronHost& K = s->K;
   if (pkr_geom(s, K.dimup, K.dimdw, K.degup, K.degdw) < 0) return -1;
-  s->d_kupc = K.upc;
-  s->d_kupv = (const double*)K.upv;
+  // up lists from the hop tables ([deg][DimUp], padded with (own column, 0)),
+  // reordered for the LDS banks like the stored ones
+  const int64_t du = K.dimup;
+  std::vector<int32_t> uc((size_t)K.degup * du);
+  std::vector<double> uv((size_t)K.degup * du);
+  if (K.degup) {
+    CK(dcopy(s, uc.data(), K.upc, uc.size() * 4, hipMemcpyDeviceToHost));
+    CK(dcopy(s, uv.data(), K.upv, uv.size() * 8, hipMemcpyDeviceToHost));
+  }
+  std::vector<std::vector<PkrHop>> ul(du);
+  for (int64_t r = 0; r < du; r++)
+    for (int e = 0; e < K.degup; e++) {
+      uint64_t bits;
+      memcpy(&bits, &uv[(size_t)e * du + r], 8);
+      ul[r].push_back({uc[(size_t)e * du + r], bits});
+    }
+  pkr_order_up(ul, (int)du, s->pkr_E);
+  s->pkr_degu = s->pkr_E;
+  CK(pkr_upload(s, ul, s->pkr_degu, du, &s->d_kupc, &s->d_kupv));
   s->d_kdwc = K.dwc;
   s->d_kdwv = (const double*)K.dwv;
   s->d_kdiag = nullptr;
