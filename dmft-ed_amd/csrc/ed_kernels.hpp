@@ -165,9 +165,9 @@ struct DevIndex {
 // ------------------------------------------------------------- basis / map
 __global__ void __launch_bounds__(kBlock) k_build_map(const int64_t* __restrict__ blk_off,
                                                       const uint32_t* __restrict__ blk_idw, int nblk,
-                                                      const int32_t* __restrict__ need_nup,
-                                                      const uint32_t* __restrict__ by_pc,
-                                                      const int32_t* __restrict__ pc_start, int ns,
+                                                      const int32_t* __restrict__ need_cls,
+                                                      const uint32_t* __restrict__ by_cls,
+                                                      const int32_t* __restrict__ cls_start, int ns,
                                                       int64_t dim, uint32_t* __restrict__ map) {
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < dim;
        i += (int64_t)gridDim.x * kBlock) {
@@ -178,8 +178,7 @@ __global__ void __launch_bounds__(kBlock) k_build_map(const int64_t* __restrict_
       else hi = mid;
     }
     uint32_t idw = blk_idw[lo];
-    int nup = need_nup[idw];
-    uint32_t iup = by_pc[pc_start[nup] + (i - blk_off[lo])];
+    uint32_t iup = by_cls[cls_start[need_cls[idw]] + (i - blk_off[lo])];
     map[i] = iup | (idw << ns);
   }
 }

@@ -336,8 +336,8 @@ static int build_kron(ed_sector* s) {
   K.dimdw = T.dimdw;
   K.nimp = 1 << M.norb;
   const uint32_t mask = T.nst - 1;
-  const uint32_t* ups = &T.by_pc[T.pc_start[nup]];
-  const uint32_t* dws = &T.by_pc[T.pc_start[ndw]];
+  const uint32_t* ups = &T.by_cls[T.cls_start[nup]];  // normal mode: class = popcount
+  const uint32_t* dws = &T.by_cls[T.cls_start[ndw]];
   const size_t hv = s->hc ? 16 : 8;
   for (int sp = 0; sp < 2; sp++) {
     const int64_t nr = sp == 0 ? K.dimup : K.dimdw;
@@ -1536,6 +1536,27 @@ extern "C" {
 
 const char* ed_gpu_last_error(void) { return g_err.c_str(); }
 
+// Jz_basis sectors: every off-diagonal element must land inside the sector
+// (the reference would insert it at column binary_search(...) = 0).  Host
+// pass over the sector with the element generator, before any device build.
+struct JzCheckAcc {
+  const SectorTables* T;
+  bool ok = true;
+  void diag(double, double) {}
+  void off(uint32_t k, double, double) { ok = ok && table_index(*T, k) >= 0; }
+};
+static bool jz_conserved(const EdModel& M, const SectorTables& T) {
+  JzCheckAcc acc;
+  acc.T = &T;
+  for (size_t b = 0; b + 1 < T.blk_off.size() && acc.ok; b++) {
+    const uint32_t idw = T.blk_idw[b];
+    const int32_t c0 = T.cls_start[T.need_cls[idw]];
+    for (int64_t r = 0; r < T.blk_off[b + 1] - T.blk_off[b] && acc.ok; r++)
+      gen_row(M, T.by_cls[c0 + r] | (idw << T.ns), acc);
+  }
+  return acc.ok;
+}
+
 int ed_sector_create(const ed_params* p, int32_t q1, int32_t q2, int32_t flags, int32_t device,
                      void* stream, ed_sector** out) {
   (void)stream;
@@ -1560,7 +1581,8 @@ int ed_sector_create(const ed_params* p, int32_t q1, int32_t q2, int32_t flags, 
   }
   s->hc = !(flags & ED_REAL);
   s->flags = flags;
-  rc = build_tables(s->Mh.ns, s->Mh.mode, q1, s->Mh.mode == ED_MODE_NORMAL ? q2 : 0, &s->T);
+  rc = build_tables(s->Mh.ns, s->Mh.mode, q1, (s->Mh.mode == ED_MODE_NORMAL || s->Mh.jz) ? q2 : 0, &s->T,
+                    s->Mh.jz ? s->Mh.lz2 : nullptr);
   if (rc != ED_OK) {
     delete s;
     return fail(rc, "sector tables: bad quantum numbers or dimension beyond int32");
@@ -1568,6 +1590,11 @@ int ed_sector_create(const ed_params* p, int32_t q1, int32_t q2, int32_t flags, 
   if (s->T.dim == 0) {
     delete s;
     return fail(ED_ERR_ARG, "empty sector");
+  }
+  if (s->Mh.jz && !jz_conserved(s->Mh, s->T)) {
+    delete s;
+    return fail(ED_ERR_UNSUPPORTED,
+                "Jz_basis: H moves states out of the (n, twoJz) sector (impHloc / bath / Jp not Jz-conserving)");
   }
   s->dim = s->T.dim;
   s->nslice = (s->dim + 63) / 64;
@@ -1597,9 +1624,9 @@ int ed_sector_create(const ed_params* p, int32_t q1, int32_t q2, int32_t flags, 
     int32_t *nn, *ps;
     TRY(upload(s, &bo, s->T.blk_off));
     TRY(upload(s, &bi, s->T.blk_idw));
-    TRY(upload(s, &nn, s->T.need_nup));
-    TRY(upload(s, &bp, s->T.by_pc));
-    TRY(upload(s, &ps, s->T.pc_start));
+    TRY(upload(s, &nn, s->T.need_cls));
+    TRY(upload(s, &bp, s->T.by_cls));
+    TRY(upload(s, &ps, s->T.cls_start));
     TRY(dalloc_t(s, &s->d_map, s->dim));
     hipLaunchKernelGGL(k_build_map, dim3(grid_for(s->dim)), dim3(kBlock), 0, s->stream, bo, bi,
                        (int)s->T.blk_idw.size(), nn, bp, ps, s->T.ns, s->dim, s->d_map);
@@ -1869,8 +1896,10 @@ static int check_op_target(const ed_sector* src, const ed_sector* dst, int32_t o
     e1 += up ? d : -d;
   } else {
     e1 += d;
+    // getCsector_Jz / getCDGsector_Jz (ED_SETUP.f90:769-805): twoJz -/+ (2*Lzdiag(iorb) + Szdiag(ispin))
+    if (src->Mh.jz) e2 += d * (src->Mh.lz2[up ? level : level - ns] + (up ? 1 : -1));
   }
-  if (dst->Mh.mode != src->Mh.mode || dst->T.q1 != e1 || dst->T.q2 != e2)
+  if (dst->Mh.mode != src->Mh.mode || dst->Mh.jz != src->Mh.jz || dst->T.q1 != e1 || dst->T.q2 != e2)
     return fail(ED_ERR_ARG, "dst is not the sector reached by the operator");
   return ED_OK;
 }

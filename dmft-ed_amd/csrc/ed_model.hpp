@@ -26,6 +26,8 @@ namespace edg {
 
 struct EdModel {
   int32_t ns, norb, nbath, nspin, S, mode, bath, ne, jhflag, hfmode;
+  int32_t jz;                 // nonsu2 Jz_basis sectors (n, twoJz)
+  int32_t lz2[ED_MAX_NS];     // 2*Lzdiag(iorb) of level l, iorb-1 = l mod Norb (ED_SETUP.f90:954)
   int32_t stride[ED_MAX_NORB][ED_MAX_NBATH];  // getBathStride, 0-based bit
   double hloc_re[ED_MAX_NSPIN][ED_MAX_NSPIN][ED_MAX_NORB][ED_MAX_NORB];
   double hloc_im[ED_MAX_NSPIN][ED_MAX_NSPIN][ED_MAX_NORB][ED_MAX_NORB];
@@ -57,6 +59,15 @@ inline int model_from_params(const ed_params* p, EdModel* M) {
   if (M->ns > ED_MAX_NS) return ED_ERR_UNSUPPORTED;
   M->ne = (p->bath_type == ED_BATH_HYBRID) ? 1 : p->norb;
   M->jhflag = (p->norb > 1 && (p->jx != 0.0 || p->jp != 0.0)) ? 1 : 0;
+  if (p->jz_basis) {
+    // Lzdiag = [-1,+1,0] (ED_VARS_GLOBAL.f90:207) is defined for Norb <= 3 and
+    // the level -> orbital map of build_sector assumes Ns = Norb*(Nbath+1)
+    if (p->ed_mode != ED_MODE_NONSU2 || p->norb > 3 || p->bath_type == ED_BATH_HYBRID)
+      return ED_ERR_UNSUPPORTED;
+    static const int lzd[3] = {-1, +1, 0};
+    M->jz = 1;
+    for (int l = 0; l < M->ns; l++) M->lz2[l] = 2 * lzd[l % p->norb];
+  }
   for (int k = 0; k < p->nbath; k++)
     for (int o = 0; o < p->norb; o++) {
       int lev;

@@ -24,7 +24,7 @@ import numpy as np
 from .hamiltonian import Sector
 from .params import EDConfig
 from .sectors import Sector as SectorId
-from .sectors import setup_pointers
+from .sectors import diag_sectors
 
 
 @dataclass
@@ -167,7 +167,7 @@ def ed_diag(cfg: EDConfig, opt: Optional[DiagOptions] = None,
             sectors: Optional[Iterable[int]] = None, device: int = 0):
     """Diagonalise all (or the given) sectors; returns (results, state_list)."""
     opt = opt or DiagOptions()
-    secs = setup_pointers(cfg)
+    secs = diag_sectors(cfg)
     pick = set(sectors) if sectors is not None else None
     todo = [sec for sec in secs if pick is None or sec.isector in pick]
     results = solve_many(cfg, todo, opt, device)

@@ -27,7 +27,7 @@ import numpy as np
 from .diag import DiagOptions, SectorResult, StateList, lanczos_params, state_list
 from .params import EDConfig
 from .sectors import Sector as SectorId
-from .sectors import setup_pointers
+from .sectors import diag_sectors
 
 
 def _dist():
@@ -86,7 +86,7 @@ def farm_diag(cfg: EDConfig, opt: Optional[DiagOptions] = None, *, device: int =
     dist = _dist()
     rank = dist.get_rank() if dist else 0
     world = dist.get_world_size() if dist else 1
-    secs = [s for s in setup_pointers(cfg) if sectors is None or s.isector in set(sectors)]
+    secs = [s for s in diag_sectors(cfg) if sectors is None or s.isector in set(sectors)]
     parts = lpt_partition([sector_cost(cfg, s, opt) for s in secs], world)
     assignment = [[secs[i].isector for i in p] for p in parts]
     local: Dict[int, SectorResult] = {}

@@ -133,8 +133,8 @@ def _tridiag_dev(S: Sector, seed, nlanc: int, real: bool, threshold: float):
     return a, b, int(n.value)
 
 
-def _target(cfg: EDConfig, sec, op: int, ispin: int):
-    return cdg_sector(cfg, sec, ispin) if op == 1 else c_sector(cfg, sec, ispin)
+def _target(cfg: EDConfig, sec, op: int, ispin: int, iorb: int = 0):
+    return cdg_sector(cfg, sec, ispin, iorb) if op == 1 else c_sector(cfg, sec, ispin, iorb)
 
 
 class _SectorCache:
@@ -158,6 +158,29 @@ class _SectorCache:
         self.d.clear()
 
 
+def mixed_pairs(cfg: EDConfig):
+    """(ispin, jspin, iorb) of the spin-off-diagonal nonsu2 components
+    (build_gf_nonsu2 ED_GF_NONSU2.f90:39-48 normal/hybrid: all of them;
+    :203-217 replica: only where dmft_bath%mask(ispin,jspin,iorb,iorb,:) is set,
+    i.e. |Re or Im impHloc(ispin,jspin,iorb,iorb)| > 1e-6, init_dmft_bath_mask
+    ED_BATH/dmft_aux.f90:261-302)."""
+    if cfg.ed_mode != "nonsu2":
+        return []
+    Nsp, No = cfg.Nspin, cfg.Norb
+    out = []
+    for s1 in range(Nsp):
+        for s2 in range(Nsp):
+            for o in range(No):
+                if s1 == s2:
+                    continue
+                if cfg.bath_type == "replica":
+                    h = 0j if cfg.impHloc is None else cfg.impHloc[s1, s2, o, o]
+                    if not (abs(h.real) > 1e-6 or abs(h.imag) > 1e-6):
+                        continue
+                out.append((s1, s2, o))
+    return out
+
+
 def _job_list(cfg: EDConfig, states: StateList):
     """Every (component, kept state, seed spec) of build_gf in the serial
     accumulation order: diagonal components (ispin, iorb), then for nonSU2 the
@@ -171,9 +194,12 @@ def _job_list(cfg: EDConfig, states: StateList):
             i = site(iorb, ispin)
             chans.append(((ispin, ispin, iorb), ("diag", ispin, iorb),
                           [(1, +1, ispin, [(i, 1)], 1.0), (0, -1, ispin, [(i, 1)], 1.0)]))
-    pairs = []
-    if cfg.ed_mode == "nonsu2" and cfg.bath_type in ("normal", "hybrid"):
-        pairs = [(s1, s2, o) for s1 in range(Nsp) for s2 in range(Nsp) for o in range(No) if s1 != s2]
+    pairs = mixed_pairs(cfg)
+    if pairs:
+        if cfg.Jz_basis:
+            # the reference builds the second term of a mixed seed in the sector
+            # of (jorb,jspin) (ED_GF_NONSU2.f90:576-584), a different Jz sector
+            raise NotImplementedError("mixed nonsu2 seeds in the Jz basis")
         for ispin, jspin, iorb in pairs:
             i, j = site(iorb, ispin), site(iorb, jspin)
             chans.append(((ispin, jspin, iorb), ("mix", ispin, jspin, iorb), [
@@ -188,7 +214,7 @@ def _job_list(cfg: EDConfig, states: StateList):
         for k, isec in enumerate(states.sectors):
             sec = secs[isec - 1]
             for spec in seeds:
-                jsec = _target(cfg, sec, spec[0], spec[2])
+                jsec = _target(cfg, sec, spec[0], spec[2], comp[2])
                 if jsec is not None:
                     jobs.append((comp, tag, k, spec, sec, jsec))
     return jobs, pairs

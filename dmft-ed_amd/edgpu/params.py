@@ -48,6 +48,7 @@ class EdParams(ctypes.Structure):
         ("bath_u", _c_double * _B3), ("bath_d", _c_double * _B3),
         ("bath_h_re", _c_double * _B5), ("bath_h_im", _c_double * _B5),
         ("bath_vr_re", _c_double * ED_MAX_NBATH), ("bath_vr_im", _c_double * ED_MAX_NBATH),
+        ("jz_basis", _c_int32), ("pad_", _c_int32),
     ]
 
 
@@ -88,6 +89,10 @@ class EDConfig:
     ed_bath_noise_thr: float = 0.0
     impHloc: Optional[np.ndarray] = None  # (Nspin, Nspin, Norb, Norb) complex
     bath: Bath = field(default_factory=Bath)
+    # nonsu2 sectors labelled (n, twoJz) (ED_INPUT_VARS.f90:78-80, 193-195)
+    Jz_basis: bool = False
+    Jz_max: bool = False
+    Jz_max_value: float = 1000.0
 
     # --------------------------------------------------------------- derived
     @property
@@ -118,6 +123,8 @@ class EDConfig:
             raise ValueError("ED msg: ed_mode=nonSU2 with Nspin!=2 is not allowed.")
         if self.ed_mode not in MODES or self.bath_type not in BATHS:
             raise ValueError("unknown ed_mode / bath_type")
+        if self.Jz_basis and (self.ed_mode != "nonsu2" or self.bath_type == "hybrid"):
+            raise ValueError("Jz_basis needs ed_mode=nonsu2 and a normal/replica bath (Ns = Norb*(Nbath+1))")
         if self.Nbath > ED_MAX_NBATH or self.Ns > ED_MAX_NS:
             raise ValueError(f"Ns={self.Ns} exceeds the {ED_MAX_NS}-level limit of 32-bit states")
 
@@ -164,6 +171,7 @@ class EDConfig:
         put(p.bath_h_im, B5, None if b.h is None else np.imag(b.h))
         put(p.bath_vr_re, (ED_MAX_NBATH,), None if b.vr is None else np.real(b.vr))
         put(p.bath_vr_im, (ED_MAX_NBATH,), None if b.vr is None else np.imag(b.vr))
+        p.jz_basis = int(bool(self.Jz_basis))
         return p
 
 

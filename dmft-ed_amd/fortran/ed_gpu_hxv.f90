@@ -34,6 +34,7 @@ module ED_GPU_HXV
      real(c_double)     :: bath_h_im(ED_MAX_NBATH,ED_MAX_NORB,ED_MAX_NORB,ED_MAX_NSPIN,ED_MAX_NSPIN)
      real(c_double)     :: bath_vr_re(ED_MAX_NBATH)
      real(c_double)     :: bath_vr_im(ED_MAX_NBATH)
+     integer(c_int32_t) :: jz_basis, pad_
   end type ed_params_t
 
   interface
@@ -173,6 +174,7 @@ contains
     p%imphloc_re = 0d0 ; p%imphloc_im = 0d0
     p%bath_e = 0d0 ; p%bath_v = 0d0 ; p%bath_u = 0d0 ; p%bath_d = 0d0
     p%bath_h_re = 0d0 ; p%bath_h_im = 0d0 ; p%bath_vr_re = 0d0 ; p%bath_vr_im = 0d0
+    p%jz_basis = 0 ; p%pad_ = 0
     do is = 1, Nspin
        do js = 1, Nspin
           do io = 1, Norb

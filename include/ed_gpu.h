@@ -99,6 +99,13 @@ typedef struct ed_params {
   double bath_h_im[ED_MAX_NSPIN][ED_MAX_NSPIN][ED_MAX_NORB][ED_MAX_NORB][ED_MAX_NBATH];
   double bath_vr_re[ED_MAX_NBATH];
   double bath_vr_im[ED_MAX_NBATH];
+  /* Jz_basis (ED_INPUT_VARS.f90:78, nonsu2 only): sectors are (n, twoJz) with
+   * twoJz = twoSz + twoLz, twoLz = sum over levels of 2*Lzdiag(iorb) with
+   * Lzdiag = [-1,+1,0] (ED_VARS_GLOBAL.f90:207) and iorb-1 = level mod Norb
+   * (build_sector ED_SETUP.f90:940-965); q1 = n, q2 = twoJz.  H must conserve
+   * Jz (replica bath with an Lz-basis Hloc): ed_sector_create checks it. */
+  int32_t jz_basis;
+  int32_t pad_;
 } ed_params;
 
 typedef struct ed_sector_info {

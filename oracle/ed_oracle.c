@@ -113,12 +113,19 @@ static int64_t bsearch_ref(const uint32_t* a, int64_t n, uint32_t value) {
 }
 
 /* ------------------------------------------------------------------ basis */
-/* build_sector ED_SETUP.f90:886-984 (Jz_basis=F).  map may be NULL (count). */
+/* Lzdiag ED_VARS_GLOBAL.f90:207 */
+static const int kLzdiag[3] = {-1, +1, 0};
+
+/* build_sector ED_SETUP.f90:886-984, incl. the nonsu2 Jz_basis branch
+ * (:940-965: keep nt_==n .and. twoJz==twoSz_+twoLz_, with twoLz_ summed over
+ * ivec(iorb+Norb*ibath), ibath=0..Nbath).  map may be NULL (count). */
 int64_t orc_build_sector(const ed_params* p, int32_t q1, int32_t q2, uint32_t* map) {
   model_t M;
   if (model_init(&M, p)) return -1;
   const int ns = M.ns;
   const uint32_t nst = 1u << ns;
+  const int jz = (M.mode == ED_MODE_NONSU2 && p->jz_basis);
+  if (jz && (M.norb > 3 || ns != M.norb * (M.nbath + 1))) return -1;
   int64_t dim = 0;
   for (uint32_t idw = 0; idw < nst; idw++) {
     int ndw_ = popc(idw);
@@ -129,6 +136,16 @@ int64_t orc_build_sector(const ed_params* p, int32_t q1, int32_t q2, uint32_t* m
       if (M.mode == ED_MODE_NORMAL) keep = (nup_ == q1);
       else if (M.mode == ED_MODE_SUPERC) keep = (nup_ - ndw_ == q1);
       else keep = (nup_ + ndw_ == q1);
+      if (keep && jz) {
+        int twoLz = 0;
+        for (int ibath = 0; ibath <= M.nbath; ibath++)
+          for (int iorb = 0; iorb < M.norb; iorb++) {
+            const int b = iorb + M.norb * ibath;
+            twoLz += 2 * kLzdiag[iorb] * btest(iup, b) + 2 * kLzdiag[iorb] * btest(idw, b);
+          }
+        const int twoSz = nup_ - ndw_;
+        keep = (q2 == twoSz + twoLz);
+      }
       if (!keep) continue;
       if (map) map[dim] = iup + idw * nst;
       dim++;

@@ -110,6 +110,42 @@ def nonsu2_replica():
     return cfg
 
 
+def _soc(lam, Norb=3):
+    """lam * L.S in the Lz basis iorb -> m = Lzdiag = (-1, +1, 0) (ED_VARS_GLOBAL.f90:207):
+    h[s, s', a, b] multiplies c+_{a s} c_{b s'}; conserves twoJz = 2Lz + 2Sz."""
+    m = (-1, 1, 0)
+    io = {mm: i for i, mm in enumerate(m)}
+    h = np.zeros((2, 2, Norb, Norb), dtype=np.complex128)
+    for a in range(Norb):
+        h[0, 0, a, a] += 0.5 * lam * m[a]
+        h[1, 1, a, a] -= 0.5 * lam * m[a]
+    for mm in (-1, 0):                      # L+ S- /2 : c+_{m+1,dn} c_{m,up}
+        a, b = io[mm + 1], io[mm]
+        h[1, 0, a, b] += 0.5 * lam * np.sqrt(2.0)
+        h[0, 1, b, a] += 0.5 * lam * np.sqrt(2.0)
+    return h
+
+
+def nonsu2_jz():
+    """Jz_basis sectors (n, twoJz): t2g (Norb=3) replica bath, spin-orbit
+    coupling in the Lz basis on the impurity and in every bath replica."""
+    cfg = EDConfig(Norb=3, Nbath=1, Nspin=2, ed_mode="nonsu2", bath_type="replica",
+                   Uloc=(2.0, 2.0, 2.0), Ust=1.2, Jh=0.4, xmu=1.0, Jz_basis=True)
+    cfg.impHloc = _soc(0.35)
+    for s in range(2):
+        for a in range(3):
+            cfg.impHloc[s, s, a, a] += (-0.1, 0.15, 0.05)[a]
+    b = init_dmft_bath(cfg)
+    for k in range(cfg.Nbath):
+        b.h[..., k] = _soc(0.2 + 0.1 * k)
+        for s in range(2):
+            for a in range(3):
+                b.h[s, s, a, a, k] += 0.3 - 0.2 * a + 0.5 * k
+        b.vr[k] = 0.45 + 0.1 * k
+    cfg.bath = b
+    return cfg
+
+
 def superc():
     cfg = make_config(Norb=1, Nbath=4, Nspin=1, ed_mode="superc", deltasc=0.15, bath="random",
                       seed=17)
@@ -133,6 +169,7 @@ CASES = [
     ("replica_cplx", replica_cplx, [(3, 3), (2, 4)]),
     ("nonsu2_rand", nonsu2_rand, [(6, 0), (5, 0)]),
     ("nonsu2_replica", nonsu2_replica, [(4, 0), (3, 0)]),
+    ("nonsu2_jz", nonsu2_jz, [(6, 0), (6, 2), (5, 1), (7, -3)]),
     ("superc", superc, [(0, 0), (1, 0), (-2, 0)]),
     ("superc_2orb", superc_2orb, [(0, 0), (1, 0)]),
 ]

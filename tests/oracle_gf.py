@@ -98,7 +98,7 @@ def build_gf_oracle(cfg, states, gopt):
             sec = secs[isec - 1]
             hmap_i = orc.build_sector(sec.q1, sec.q2)
             for op, isign, ispin, terms, weight in specs:
-                jsec = cdg_sector(cfg, sec, ispin) if op == 1 else c_sector(cfg, sec, ispin)
+                jsec = cdg_sector(cfg, sec, ispin, idx[2]) if op == 1 else c_sector(cfg, sec, ispin, idx[2])
                 if jsec is None:
                     continue
                 hmap_j, v = seed_combo(orc, hmap_i, jsec, op, terms, vec.astype(np.complex128))
@@ -124,7 +124,9 @@ def build_gf_oracle(cfg, states, gopt):
             i = site(iorb, ispin)
             channel((ispin, ispin, iorb, iorb), [(1, 1, ispin, [(i, 1)], 1.0), (0, -1, ispin, [(i, 1)], 1.0)])
     if cfg.ed_mode == "nonsu2":
-        pairs = [(s1, s2, o) for s1 in range(Nsp) for s2 in range(Nsp) for o in range(No) if s1 != s2]
+        pairs = [(s1, s2, o) for s1 in range(Nsp) for s2 in range(Nsp) for o in range(No) if s1 != s2
+                 and (cfg.bath_type != "replica"      # dmft_bath%mask, ED_BATH/dmft_aux.f90:283-295
+                      or abs(cfg.impHloc[s1, s2, o, o].real) > 1e-6 or abs(cfg.impHloc[s1, s2, o, o].imag) > 1e-6)]
         for ispin, jspin, iorb in pairs:
             i, j = site(iorb, ispin), site(iorb, jspin)
             channel((ispin, jspin, iorb, iorb), [

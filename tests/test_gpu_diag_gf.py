@@ -81,3 +81,22 @@ def test_gf_nonsu2_matches_oracle(cfg_kw):
     assert np.max(np.abs(Gr - Gr0)) / np.max(np.abs(Gr0)) < 1e-5
     # spin-off-diagonal components are present (ed_vsf_ratio != 0 mixes spins)
     assert np.max(np.abs(Gm0[0, 1, 0, 0])) > 1e-6 * scale
+
+
+def test_gf_nonsu2_replica_matches_oracle():
+    """build_gf_nonsu2 with a replica bath: the spin-off-diagonal components
+    are computed where dmft_bath%mask is set (impHloc spin flip on the orbital,
+    ED_GF_NONSU2.f90:203-217, ED_BATH/dmft_aux.f90:283-295)."""
+    from cases import nonsu2_replica
+    from edgpu.gf import GFOptions, build_gf, mixed_pairs
+    from oracle_gf import build_gf_oracle
+
+    cfg = nonsu2_replica()
+    assert mixed_pairs(cfg)              # the case's impHloc has a spin flip
+    _, sl = ed_diag(cfg, DiagOptions(lanc_method="lanczos"))
+    gopt = GFOptions(Lmats=300, Lreal=300)
+    Gm, Gr = build_gf(cfg, sl, gopt)
+    Gm0, Gr0 = build_gf_oracle(cfg, sl, gopt)
+    scale = np.max(np.abs(Gm0))
+    assert np.max(np.abs(Gm - Gm0)) / scale < 1e-10
+    assert np.max(np.abs(Gm0[0, 1, 0, 0])) > 1e-6 * scale

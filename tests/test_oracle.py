@@ -59,8 +59,10 @@ def test_oracle_vs_second_quantisation(name, factory, sectors):
 def test_sector_enumeration_matches_dimension_formulas():
     from edgpu.sectors import setup_pointers
 
+    from cases import nonsu2_jz
+
     for cfg in (make_config(Norb=1, Nbath=4), make_config(Norb=1, Nbath=3, Nspin=2, ed_mode="nonsu2"),
-                make_config(Norb=1, Nbath=3, ed_mode="superc")):
+                make_config(Norb=1, Nbath=3, ed_mode="superc"), nonsu2_jz()):
         orc = Oracle(cfg)
         for s in setup_pointers(cfg):
             assert len(orc.build_sector(s.q1, s.q2)) == s.dim
@@ -120,3 +122,34 @@ def test_complex_vr_reference_quirk():
     assert np.max(np.abs(A[mask] - np.conj(B[mask]))) < 1e-13
     # ... and everything else is the Hermitian operator
     assert np.max(np.abs(D[~mask])) < 1e-13
+
+
+def test_jz_sectors_partition_and_targets():
+    """Jz_basis (ED_SETUP.f90:636-664, 769-805, 940-965): the (n, twoJz)
+    sectors of the t2g case tile the whole Fock space, each n-sector is the
+    disjoint union of its Jz sectors (same states as the n basis), and
+    c+/c of (iorb, ispin) move twoJz by +-(2*Lzdiag(iorb) + Szdiag(ispin))."""
+    from cases import nonsu2_jz
+    from edgpu.sectors import cdg_sector, c_sector, setup_pointers
+
+    cfg = nonsu2_jz()
+    secs = setup_pointers(cfg)
+    assert sum(s.dim for s in secs) == 4 ** cfg.Ns
+    orc = Oracle(cfg)
+    import copy
+
+    cn = copy.deepcopy(cfg)
+    cn.Jz_basis = False
+    on = Oracle(cn)
+    for n in (5, 6):
+        whole = set(on.build_sector(n, 0).tolist())
+        parts = [set(orc.build_sector(s.q1, s.q2).tolist()) for s in secs if s.q1 == n]
+        assert sum(len(p) for p in parts) == len(whole) and set().union(*parts) == whole
+    lz = (-1, 1, 0)
+    sec = [s for s in secs if (s.q1, s.q2) == (6, 0)][0]
+    for iorb in range(3):
+        for ispin, sz in ((0, 1), (1, -1)):
+            t = cdg_sector(cfg, sec, ispin, iorb)
+            assert (t.q1, t.q2) == (7, 2 * lz[iorb] + sz)
+            t = c_sector(cfg, sec, ispin, iorb)
+            assert (t.q1, t.q2) == (5, -(2 * lz[iorb] + sz))
