@@ -506,7 +506,8 @@ __global__ void __launch_bounds__(kBlock) k_spmv(const val_t<HC>* __restrict__ d
                                                  const int64_t* __restrict__ sptr,
                                                  const int32_t* __restrict__ cols,
                                                  const val_t<HC>* __restrict__ vals,
-                                                 const val_t<VC>* __restrict__ x, int64_t dim,
+                                                 const val_t<VC>* __restrict__ x,
+                                                 const val_t<VC>* __restrict__ xr, int64_t dim,
                                                  int64_t nslice, Epi epi, int xcd) {
   using V = val_t<VC>;
   using H = val_t<HC>;
@@ -522,7 +523,7 @@ __global__ void __launch_bounds__(kBlock) k_spmv(const val_t<HC>* __restrict__ d
       const int w = (int)((sptr[s + 1] - s0) >> 6);
       const int32_t* cp = cols + s0 + (i & 63);
       const H* vp = vals + s0 + (i & 63);
-      const V xi = x[i];
+      const V xi = xr[i];  // own entry: xr = x + first row (row-split sectors)
       // spMatVec_cc: Hv=0; Hv(i)=Hv(i)+vals(j)*v(cols(j)), diagonal first
       V acc = add(vzero<V>(), mul(ldh<NT>(diag + i), xi));
       for (int k0 = 0; k0 < w; k0 += kChunk) {
@@ -611,7 +612,8 @@ __global__ void __launch_bounds__(kBlock) k_spmv_pk(const double* __restrict__ d
                                                     const int64_t* __restrict__ sptr,
                                                     const uint32_t* __restrict__ words,
                                                     const double* __restrict__ dict,
-                                                    const val_t<VC>* __restrict__ x, int64_t dim,
+                                                    const val_t<VC>* __restrict__ x,
+                                                    const val_t<VC>* __restrict__ xr, int64_t dim,
                                                     int64_t nslice, Epi epi, int xcd) {
   using V = val_t<VC>;
   if (epi.skip()) return;
@@ -632,7 +634,7 @@ __global__ void __launch_bounds__(kBlock) k_spmv_pk(const double* __restrict__ d
       const int64_t s0 = sptr[s];
       const int w = (int)((sptr[s + 1] - s0) >> 6);
       const uint32_t* wp = words + s0 + (i & 63);
-      const V xi = x[i];
+      const V xi = xr[i];
       V acc = add(vzero<V>(), mul(ldm<NT>(diag + i), xi));
       for (int k0 = 0; k0 < w; k0 += kChunk) {
         uint32_t c[kChunk];
@@ -660,11 +662,12 @@ template <bool HC, bool VC>
 struct GatherAcc {
   using V = val_t<VC>;
   const V* x;
+  const V* xr;
   DevIndex idx;
   int64_t i;
   V acc, xi;
   __device__ __forceinline__ void diag(double re, double im) {
-    xi = x[i];
+    xi = xr[i];
     acc = add(vzero<V>(), mul(mk<HC>(re, im), xi));
   }
   __device__ __forceinline__ void off(uint32_t kst, double re, double im) {
@@ -675,7 +678,8 @@ struct GatherAcc {
 template <bool HC, bool VC, class Epi>
 __global__ void __launch_bounds__(kBlock) k_direct(const EdModel* __restrict__ Mp,
                                                    const uint32_t* __restrict__ map, DevIndex idx,
-                                                   const val_t<VC>* __restrict__ x, int64_t dim,
+                                                   const val_t<VC>* __restrict__ x,
+                                                   const val_t<VC>* __restrict__ xr, int64_t dim,
                                                    int64_t nslice, Epi epi) {
   if (epi.skip()) return;
   epi.prepare();
@@ -686,6 +690,7 @@ __global__ void __launch_bounds__(kBlock) k_direct(const EdModel* __restrict__ M
     if (i < dim) {
       GatherAcc<HC, VC> g;
       g.x = x;
+      g.xr = xr;
       g.idx = idx;
       g.i = i;
       gen_row(M, map[i], g);

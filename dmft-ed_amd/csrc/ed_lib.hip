@@ -83,6 +83,9 @@ struct ed_sector {
   int flags = 0;
   bool hc = true;      // complex H values
   int64_t dim = 0, nslice = 0;
+  // rows of the operator held here: [row0, row0+nrows) of the sector (the
+  // reference's MPI row split, ED_HAMILTONIAN.f90:55-62); whole sector: 0, dim
+  int64_t row0 = 0, nrows = 0;
   int32_t* d_off = nullptr;
   uint32_t* d_rank = nullptr;
   uint32_t* d_map = nullptr;
@@ -235,8 +238,16 @@ static int build_pack(ed_sector* s) {
   return ED_OK;
 }
 
+// Row-split sectors (ed_sector_create_rows) hold rows [row0, row0+nrows) of
+// H: H·v from a whole-sector vector and the CSR dump only.
+static int whole_only(const ed_sector* s) {
+  if (s->nrows == s->dim) return ED_OK;
+  return fail(ED_ERR_UNSUPPORTED, "row-split sector: only ed_sector_hxv_dev[_path] and ed_sector_dump_csr apply");
+}
+
 static int build_stored(ed_sector* s) {
-  const int64_t dim = s->dim, ns = s->nslice;
+  const int64_t dim = s->nrows, ns = s->nslice;  // rows held by this sector object
+  const uint32_t* map = s->d_map + s->row0;
   uint16_t* cnt;
   int32_t* width;
   int64_t* bsum;
@@ -249,7 +260,7 @@ static int build_stored(ed_sector* s) {
   HIPCK(hipMallocAsync((void**)&bsum, std::max<int64_t>(nb, 1) * sizeof(int64_t), s->stream));
   HIPCK(hipMallocAsync((void**)&total, sizeof(int64_t), s->stream));
   CK(dalloc_t(s, &s->d_sptr, ns + 1));
-  hipLaunchKernelGGL(k_count, dim3(grid_for(ns * 64)), dim3(kBlock), 0, s->stream, s->Md, s->d_map,
+  hipLaunchKernelGGL(k_count, dim3(grid_for(ns * 64)), dim3(kBlock), 0, s->stream, s->Md, map,
                      dim, ns, cnt, width);
   HIPCK(hipGetLastError());
   hipLaunchKernelGGL(k_scan_blocks, dim3((unsigned)nb), dim3(1024), 0, s->stream, width, ns,
@@ -272,11 +283,11 @@ static int build_stored(ed_sector* s) {
   DevIndex idx{s->d_off, s->d_rank, s->T.ns, s->T.nst - 1};
   if (s->hc)
     hipLaunchKernelGGL(k_fill<true>, dim3(grid_for(dim)), dim3(kBlock), 0, s->stream, s->Md,
-                       s->d_map, dim, idx, s->d_sptr, (double2*)s->d_diag, s->d_cols,
+                       map, dim, idx, s->d_sptr, (double2*)s->d_diag, s->d_cols,
                        (double2*)s->d_vals);
   else
     hipLaunchKernelGGL(k_fill<false>, dim3(grid_for(dim)), dim3(kBlock), 0, s->stream, s->Md,
-                       s->d_map, dim, idx, s->d_sptr, (double*)s->d_diag, s->d_cols,
+                       map, dim, idx, s->d_sptr, (double*)s->d_diag, s->d_cols,
                        (double*)s->d_vals);
   HIPCK(hipGetLastError());
   // nnz = dim (diagonal) + sum(cnt)
@@ -286,7 +297,7 @@ static int build_stored(ed_sector* s) {
   int64_t nnz = dim;
   for (int64_t i = 0; i < dim; i++) nnz += hc[i];
   s->nnz = nnz;
-  if (!s->hc && dim <= (int64_t)kPackColMask + 1 && !getenv("ED_GPU_NO_PACK")) CK(build_pack(s));
+  if (!s->hc && s->dim <= (int64_t)kPackColMask + 1 && !getenv("ED_GPU_NO_PACK")) CK(build_pack(s));
   return ED_OK;
 }
 
@@ -453,33 +464,34 @@ static int hxv_blocks(const ed_sector* s, int path) {
 template <bool HC, bool VC, class Epi>
 static int launch_hxv_t(ed_sector* s, int path, const void* x, Epi epi, hipStream_t st) {
   using V = val_t<VC>;
-  const int64_t dim = s->dim, ns = s->nslice;
+  const int64_t dim = s->nrows, ns = s->nslice;  // rows of this object; x is the whole sector vector
   const int g = grid_for(ns * 64);
   const int gx = hxv_blocks(s, path);
   const int xr = xcd_on(s, path) ? 1 : 0;
+  const V* xo = (const V*)x + s->row0;  // the rows' own entries
   if (path == 0 && !HC && s->d_words) {
     const int64_t mbytes = s->padded * 4 + dim * 8;
     if (mbytes > (int64_t)192 << 20)
       hipLaunchKernelGGL((k_spmv_pk<VC, 1, Epi>), dim3(gx), dim3(kBlock), 0, st, (const double*)s->d_diag,
-                         s->d_sptr, s->d_words, s->d_pdict, (const V*)x, dim, ns, epi, xr);
+                         s->d_sptr, s->d_words, s->d_pdict, (const V*)x, xo, dim, ns, epi, xr);
     else
       hipLaunchKernelGGL((k_spmv_pk<VC, 0, Epi>), dim3(gx), dim3(kBlock), 0, st, (const double*)s->d_diag,
-                         s->d_sptr, s->d_words, s->d_pdict, (const V*)x, dim, ns, epi, xr);
+                         s->d_sptr, s->d_words, s->d_pdict, (const V*)x, xo, dim, ns, epi, xr);
   } else if (path == 0) {
     // non-temporal matrix loads once the matrix cannot stay in the 256 MB MALL
     const int64_t mbytes = s->padded * (4 + (HC ? 16 : 8)) + dim * (HC ? 16 : 8);
     if (mbytes > (int64_t)192 << 20)
       hipLaunchKernelGGL((k_spmv<HC, VC, 1, Epi>), dim3(gx), dim3(kBlock), 0, st,
                          (const val_t<HC>*)s->d_diag, s->d_sptr, s->d_cols,
-                         (const val_t<HC>*)s->d_vals, (const V*)x, dim, ns, epi, xr);
+                         (const val_t<HC>*)s->d_vals, (const V*)x, xo, dim, ns, epi, xr);
     else
       hipLaunchKernelGGL((k_spmv<HC, VC, 0, Epi>), dim3(gx), dim3(kBlock), 0, st,
                          (const val_t<HC>*)s->d_diag, s->d_sptr, s->d_cols,
-                         (const val_t<HC>*)s->d_vals, (const V*)x, dim, ns, epi, xr);
+                         (const val_t<HC>*)s->d_vals, (const V*)x, xo, dim, ns, epi, xr);
   } else if (path == 1) {
     DevIndex idx{s->d_off, s->d_rank, s->T.ns, s->T.nst - 1};
-    hipLaunchKernelGGL((k_direct<HC, VC, Epi>), dim3(g), dim3(kBlock), 0, st, s->Md, s->d_map, idx,
-                       (const V*)x, dim, ns, epi);
+    hipLaunchKernelGGL((k_direct<HC, VC, Epi>), dim3(g), dim3(kBlock), 0, st, s->Md, s->d_map + s->row0,
+                       idx, (const V*)x, xo, dim, ns, epi);
   } else {
     hipLaunchKernelGGL((k_kron<HC, VC, Epi>), dim3(g), dim3(kBlock), 0, st, kron_args<HC>(s),
                        (const V*)x, dim, ns, epi);
@@ -1557,9 +1569,8 @@ static bool jz_conserved(const EdModel& M, const SectorTables& T) {
   return acc.ok;
 }
 
-int ed_sector_create(const ed_params* p, int32_t q1, int32_t q2, int32_t flags, int32_t device,
-                     void* stream, ed_sector** out) {
-  (void)stream;
+static int sector_create(const ed_params* p, int32_t q1, int32_t q2, int32_t flags, int64_t row0,
+                         int64_t nrows, int32_t device, ed_sector** out) {
   if (!out) return fail(ED_ERR_ARG, "out == NULL");
   *out = nullptr;
   if (!(flags & (ED_STORED | ED_DIRECT))) return fail(ED_ERR_ARG, "flags need ED_STORED or ED_DIRECT");
@@ -1597,7 +1608,17 @@ int ed_sector_create(const ed_params* p, int32_t q1, int32_t q2, int32_t flags, 
                 "Jz_basis: H moves states out of the (n, twoJz) sector (impHloc / bath / Jp not Jz-conserving)");
   }
   s->dim = s->T.dim;
-  s->nslice = (s->dim + 63) / 64;
+  if (nrows < 0) {
+    row0 = 0;
+    nrows = s->dim;
+  }
+  if (row0 < 0 || nrows < 1 || row0 + nrows > s->dim) {
+    delete s;
+    return fail(ED_ERR_ARG, "row range outside the sector");
+  }
+  s->row0 = row0;
+  s->nrows = nrows;
+  s->nslice = (nrows + 63) / 64;
 #define TRY(x)            \
   do {                    \
     int r2_ = (x);        \
@@ -1636,7 +1657,7 @@ int ed_sector_create(const ed_params* p, int32_t q1, int32_t q2, int32_t flags, 
     }
   }
   // Kronecker form: normal mode without Jx/Jp terms (no term moves both spins)
-  s->kron = (flags & ED_DIRECT) && s->Mh.mode == ED_MODE_NORMAL && !s->Mh.jhflag;
+  s->kron = (flags & ED_DIRECT) && s->Mh.mode == ED_MODE_NORMAL && !s->Mh.jhflag && nrows == s->dim;
   if (flags & ED_STORED) TRY(build_stored(s));
   if (s->kron) TRY(build_kron(s));
   if (hipStreamSynchronize(s->stream) != hipSuccess) {
@@ -1648,6 +1669,18 @@ int ed_sector_create(const ed_params* p, int32_t q1, int32_t q2, int32_t flags, 
   return ED_OK;
 }
 
+int ed_sector_create(const ed_params* p, int32_t q1, int32_t q2, int32_t flags, int32_t device,
+                     void* stream, ed_sector** out) {
+  (void)stream;
+  return sector_create(p, q1, q2, flags, 0, -1, device, out);
+}
+
+int ed_sector_create_rows(const ed_params* p, int32_t q1, int32_t q2, int32_t flags, int64_t row0,
+                          int64_t nrows, int32_t device, void* stream, ed_sector** out) {
+  (void)stream;
+  return sector_create(p, q1, q2, flags, row0, nrows, device, out);
+}
+
 int ed_sector_destroy(ed_sector* s) {
   sector_free(s);
   return ED_OK;
@@ -1657,6 +1690,8 @@ int ed_sector_get_info(const ed_sector* s, ed_sector_info* info) {
   if (!s || !info) return fail(ED_ERR_ARG, "null");
   memset(info, 0, sizeof(*info));
   info->dim = s->dim;
+  info->row0 = s->row0;
+  info->nrows = s->nrows;
   info->nnz = (s->flags & ED_STORED) ? s->nnz : 0;
   info->padded = s->padded;
   info->ns = s->Mh.ns;
@@ -1707,6 +1742,7 @@ int ed_sector_hxv_dev(ed_sector* s, int32_t vtype, const void* v, void* hv, void
 
 int ed_sector_hxv(ed_sector* s, int32_t nloc, const double* v, double* hv) {
   if (!s || !v || !hv) return fail(ED_ERR_ARG, "null");
+  CK(whole_only(s));
   // directMatVec_cc: "Nloc != dim(isector)" (DIRECT_HxV.f90:50)
   if ((int64_t)nloc != s->dim) return fail(ED_ERR_ARG, "ed_gpu_hxv ERROR: Nloc != dim(isector)");
   HIPCK(hipSetDevice(s->device));
@@ -1732,7 +1768,7 @@ int ed_sector_dump_csr(const ed_sector* s, int64_t* rowptr, int32_t* cols, doubl
   if (!s || !rowptr || !cols || !vals) return fail(ED_ERR_ARG, "null");
   if (!(s->flags & ED_STORED)) return fail(ED_ERR_STATE, "sector was built without ED_STORED");
   HIPCK(hipSetDevice(s->device));
-  const int64_t dim = s->dim, ns = s->nslice, slots = s->padded;
+  const int64_t dim = s->nrows, ns = s->nslice, slots = s->padded;  // local rows, global columns
   const int hw = s->hc ? 2 : 1;
   std::vector<uint16_t> cnt(dim);
   std::vector<int64_t> sptr(ns + 1);
@@ -1746,7 +1782,7 @@ int ed_sector_dump_csr(const ed_sector* s, int64_t* rowptr, int32_t* cols, doubl
   int64_t q = 0;
   rowptr[0] = 0;
   for (int64_t i = 0; i < dim; i++) {
-    cols[q] = (int32_t)i;
+    cols[q] = (int32_t)(s->row0 + i);
     vals[2 * q] = dg[hw * i];
     vals[2 * q + 1] = hw == 2 ? dg[2 * i + 1] : 0.0;
     q++;
@@ -1799,6 +1835,7 @@ struct LancDriver {
 };
 
 static int make_driver(ed_sector* s, int vtype, bool basis, LancDriver* d) {
+  CK(whole_only(s));
   d->s = s;
   d->vc = vtype ? 1 : 0;
   if (d->vc == 0 && s->hc) return fail(ED_ERR_ARG, "complex H needs vtype=1");
@@ -1908,6 +1945,8 @@ int ed_sector_apply_op(const ed_sector* src, const ed_sector* dst, int32_t op, i
                        int32_t vtype, const void* src_vec, void* dst_vec, void* stream) {
   if (!src_vec || !dst_vec) return fail(ED_ERR_ARG, "null");
   CK(check_op_target(src, dst, op, level));
+  CK(whole_only(src));
+  CK(whole_only(dst));
   HIPCK(hipSetDevice(src->device));
   hipStream_t st = (hipStream_t)stream;
   const size_t vs = vtype ? 16 : 8;
@@ -1928,6 +1967,8 @@ int ed_sector_apply_op_acc(const ed_sector* src, const ed_sector* dst, int32_t o
                            void* dst_vec, void* stream) {
   if (!src_vec || !dst_vec) return fail(ED_ERR_ARG, "null");
   if (!vtype && coef_im != 0.0) return fail(ED_ERR_ARG, "complex coefficient needs vtype=1");
+  CK(whole_only(src));
+  CK(whole_only(dst));
   CK(check_op_target(src, dst, op, level));
   HIPCK(hipSetDevice(src->device));
   hipStream_t st = (hipStream_t)stream;
@@ -2092,6 +2133,7 @@ int ed_sector_eigh(ed_sector* s, int32_t vtype, int32_t nev, int32_t ncv, int32_
                               double tol, const void* v0, double* evals, void* evecs, int32_t* nconv,
                               int32_t* nhv) {
   if (!s || !evals || maxit < 1) return fail(ED_ERR_ARG, "bad args");
+  CK(whole_only(s));
   if (vtype == 0 && s->hc) return fail(ED_ERR_ARG, "complex H needs vtype=1");
   if (ncv > 64) return fail(ED_ERR_ARG, "ncv > 64 not supported");
   HIPCK(hipSetDevice(s->device));

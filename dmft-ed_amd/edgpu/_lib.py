@@ -25,6 +25,7 @@ _P = ctypes.c_void_p
 _i32, _i64, _f64 = ctypes.c_int32, ctypes.c_int64, ctypes.c_double
 SIGNATURES = {
     "ed_sector_create": ([_P, _i32, _i32, _i32, _i32, _P, _P], ctypes.c_int),
+    "ed_sector_create_rows": ([_P, _i32, _i32, _i32, _i64, _i64, _i32, _P, _P], ctypes.c_int),
     "ed_sector_destroy": ([_P], ctypes.c_int),
     "ed_sector_get_info": ([_P, _P], ctypes.c_int),
     "ed_sector_hxv_dev": ([_P, _i32, _P, _P, _P], ctypes.c_int),
@@ -63,7 +64,7 @@ class SectorInfo(ctypes.Structure):
     _fields_ = [("dim", _i64), ("nnz", _i64), ("padded", _i64), ("ns", _i32), ("mode", _i32),
                 ("q1", _i32), ("q2", _i32), ("flags", _i32), ("kron", _i32),
                 ("dimup", _i64), ("dimdw", _i64), ("device_bytes", _i64),
-                ("packed", _i32), ("npdict", _i32)]
+                ("packed", _i32), ("npdict", _i32), ("row0", _i64), ("nrows", _i64)]
 
 
 class EDGPUError(RuntimeError):

@@ -26,6 +26,11 @@ holds only its 1/P of v.  `dist_lanczos` runs the plain recurrence
 (.repo/PLAIN_LANCZOS.f90:87-118) on the split vector with two all-reduces of
 scalars per step.
 
+Any other sector (superc, nonsu2, Jx/Jp, Jz_basis ...) uses `DistRowSector`:
+the reference's own layout — each rank builds rows [r0, r0+n) of the stored
+(or matrix-free generic) H on its GPU (ed_sector_create_rows) and all-gathers
+the vector before each product, exactly spMatVec_mpi_cc's Allgatherv.
+
 The collective backend is the default process group (nccl = RCCL on the GPU
 box; gloo in the CPU tests, where `ops` injects reference factor products).
 """
@@ -220,6 +225,98 @@ class DistKronSector:
             self._S = None
 
 
+def mpi_split(n: int, parts: int) -> Tuple[List[int], List[int]]:
+    """build_Hv_sector's row split (ED_HAMILTONIAN.f90:55-62): mpiQ = n/parts
+    rows per rank, the remainder on the last rank."""
+    q = n // parts
+    starts = [r * q for r in range(parts)]
+    counts = [q + (n % parts if r == parts - 1 else 0) for r in range(parts)]
+    return starts, counts
+
+
+class DistRowSector:
+    """One sector split by rows over the ranks of the default process group,
+    any ed_mode (build_Hv_sector with MpiStatus, ED_HAMILTONIAN.f90:55-62,
+    `mpi_split`).
+    Vectors are 1-D tensors holding this rank's rows; H·v all-gathers the
+    whole vector (spMatVec_mpi_cc STORED_HxV.f90:147-197) and applies the
+    local rows with global columns.  `hxv_rows` (injectable, CPU tests)
+    maps a whole vector to the local rows of H·v."""
+
+    def __init__(self, cfg=None, q1: int = 0, q2: int = 0, *, device: int = 0, real: Optional[bool] = None,
+                 stored: bool = True, hxv_rows=None, dim: Optional[int] = None, dtype=None):
+        import torch
+
+        dist = _dist()
+        self.rank = dist.get_rank() if dist else 0
+        self.world = dist.get_world_size() if dist else 1
+        self._S = None
+        if hxv_rows is None:
+            from .hamiltonian import Sector
+            from .sectors import sector_dim
+
+            real = cfg.is_real() if real is None else real
+            dim = sector_dim(cfg, q1, q2)
+            r0, n = mpi_split(dim, self.world)
+            self._S = Sector(cfg, q1, q2, stored=stored, direct=not stored, real=real, device=device,
+                             rows=(r0[self.rank], n[self.rank]))
+            self.dtype = torch.float64 if real else torch.complex128
+            self.device = torch.device("cuda", device)
+            S = self._S
+
+            def hxv_rows(v):
+                y = torch.empty(S.nrows, dtype=v.dtype, device=v.device)
+                S.hxv_dev(v, y)
+                return y
+        else:
+            self.dtype = dtype or torch.complex128
+            self.device = torch.device("cpu")
+        self.dim = dim
+        self.r0, self.n = mpi_split(dim, self.world)
+        self._rows = hxv_rows
+        self.comm_cpu = dist is not None and dist.get_backend() != "nccl"
+
+    @property
+    def local_rows(self) -> Tuple[int, int]:
+        return self.r0[self.rank], self.n[self.rank]
+
+    @property
+    def local_dim(self) -> int:
+        return self.n[self.rank]
+
+    def scatter(self, v_full):
+        r0, n = self.local_rows
+        return v_full[r0:r0 + n].contiguous()
+
+    def gather(self, v_loc):
+        """Allgatherv of the split vector (equal-size all_gather of padded
+        blocks: RCCL and gloo both take it)."""
+        import torch
+
+        dist = _dist()
+        if dist is None:
+            return v_loc
+        m = max(self.n)
+        pad = torch.zeros(m, dtype=v_loc.dtype, device=v_loc.device)
+        pad[:v_loc.numel()] = v_loc
+        parts = [torch.empty(m, dtype=v_loc.dtype, device=v_loc.device) for _ in self.n]
+        if self.comm_cpu:
+            cpu = [p.cpu() for p in parts]
+            dist.all_gather(cpu, pad.cpu())
+            parts = [p.to(v_loc.device) for p in cpu]
+        else:
+            dist.all_gather(parts, pad)
+        return torch.cat([p[:k] for p, k in zip(parts, self.n)])
+
+    def hxv(self, x):
+        return self._rows(self.gather(x))
+
+    def close(self):
+        if self._S is not None:
+            self._S.close()
+            self._S = None
+
+
 def _allreduce_sum(t):
     dist = _dist()
     if dist is None:
@@ -232,7 +329,7 @@ def _allreduce_sum(t):
     return t
 
 
-def dist_lanczos(ds: DistKronSector, v0_loc, nitermax: int, threshold: float = 1e-13):
+def dist_lanczos(ds, v0_loc, nitermax: int, threshold: float = 1e-13):
     """sp_lanc_tridiag on the split vector: (alfa, beta, nlanc); beta[0] = 0,
     beta[k+1] couples k, k+1 (.repo/PLAIN_LANCZOS.f90:87-118, 154-180)."""
     import torch

@@ -43,14 +43,22 @@ class Sector:
     """One symmetry sector resident on one GPU (handle API of include/ed_gpu.h)."""
 
     def __init__(self, cfg: EDConfig, q1: int, q2: int = 0, *, stored: bool = True,
-                 direct: bool = False, real: bool = False, device: int = 0):
+                 direct: bool = False, real: bool = False, device: int = 0, rows=None):
+        """rows=(row0, nrows): hold only those rows of H (ed_sector_create_rows,
+        the reference's MPI row split); H·v then maps a whole-sector vector to
+        the nrows local entries."""
         lib = _lib.load()
         self.cfg = cfg
         self._params = cfg.to_ctypes()
         flags = (ED_STORED if stored else 0) | (ED_DIRECT if direct else 0) | (ED_REAL if real else 0)
         h = ctypes.c_void_p()
-        check(lib.ed_sector_create(ctypes.byref(self._params), q1, q2, flags, device, None,
-                                   ctypes.byref(h)), "ed_sector_create")
+        if rows is None:
+            check(lib.ed_sector_create(ctypes.byref(self._params), q1, q2, flags, device, None,
+                                       ctypes.byref(h)), "ed_sector_create")
+        else:
+            check(lib.ed_sector_create_rows(ctypes.byref(self._params), q1, q2, flags, int(rows[0]),
+                                            int(rows[1]), device, None, ctypes.byref(h)),
+                  "ed_sector_create_rows")
         self._h = h
         self.device = device
         self.real = real
@@ -59,6 +67,7 @@ class Sector:
         self.info = info
         self.dim = int(info.dim)
         self.nnz = int(info.nnz)
+        self.row0, self.nrows = int(info.row0), int(info.nrows)
 
     # ------------------------------------------------------------------ life
     def close(self):
@@ -91,7 +100,7 @@ class Sector:
 
     def dump_csr(self):
         """spH0 in reference row order (sp_dump_matrix, ED_SPARSE_MATRIX.f90:331-388)."""
-        rowptr = np.zeros(self.dim + 1, dtype=np.int64)
+        rowptr = np.zeros(self.nrows + 1, dtype=np.int64)
         cols = np.zeros(self.nnz, dtype=np.int32)
         vals = np.zeros(self.nnz, dtype=np.complex128)
         check(_lib.load().ed_sector_dump_csr(self._h, _ptr(rowptr), _ptr(cols), _ptr(vals)),
@@ -121,7 +130,7 @@ class Sector:
             vt = 0
         else:
             raise TypeError("vectors must be float64 or complex128")
-        if hv.dtype != v.dtype or v.numel() != self.dim or hv.numel() != self.dim:
+        if hv.dtype != v.dtype or v.numel() != self.dim or hv.numel() != self.nrows:
             raise ValueError("shape/dtype mismatch")
         if not (v.is_contiguous() and hv.is_contiguous()):
             raise ValueError("vectors must be contiguous")

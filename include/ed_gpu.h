@@ -114,13 +114,14 @@ typedef struct ed_sector_info {
   int64_t padded;   /* SELL-64 slots actually stored (>= nnz - dim)     */
   int32_t ns;       /* levels per spin                                  */
   int32_t mode;     /* ED_MODE_*                                        */
-  int32_t q1, q2;   /* (nup,ndw) | (sz,0) | (n,0)                       */
+  int32_t q1, q2;   /* (nup,ndw) | (sz,0) | (n,0) | (n,twoJz)           */
   int32_t flags;    /* ED_STORED|ED_DIRECT|ED_REAL as built             */
   int32_t kron;     /* 1 if the direct path uses the (DimUp x DimDw) form */
   int64_t dimup, dimdw;   /* factor dimensions (normal mode), else 0    */
   int64_t device_bytes;   /* device memory held by the sector           */
   int32_t packed;   /* 1 if stored H·v reads 32-bit {col|value index} words */
   int32_t npdict;   /* distinct off-diagonal values (packed dictionary)  */
+  int64_t row0, nrows;    /* rows held: [row0, row0+nrows) (whole: 0, dim) */
 } ed_sector_info;
 
 typedef struct ed_sector ed_sector; /* opaque */
@@ -130,6 +131,15 @@ typedef struct ed_sector ed_sector; /* opaque */
  * q1,q2: (nup,ndw) for normal, (sz,-) for superc, (n,-) for nonsu2. */
 int ed_sector_create(const ed_params* p, int32_t q1, int32_t q2, int32_t flags,
                      int32_t device, void* stream, ed_sector** out);
+/* The reference's MPI row split of one sector (build_Hv_sector with
+ * MpiStatus, ED_HAMILTONIAN.f90:55-62; spMatVec_mpi_cc STORED_HxV.f90:147-197):
+ * build only rows [row0, row0+nrows) of H (ED_STORED, or ED_DIRECT generic).
+ * ed_sector_hxv_dev[_path] then takes the WHOLE sector vector v (the
+ * Allgatherv result) and writes the nrows local entries of Hv; columns stay
+ * global.  Lanczos/eigh/apply_op refuse such a sector (ED_ERR_UNSUPPORTED):
+ * the distributed recurrence runs on the host side (edgpu.dist). */
+int ed_sector_create_rows(const ed_params* p, int32_t q1, int32_t q2, int32_t flags, int64_t row0,
+                          int64_t nrows, int32_t device, void* stream, ed_sector** out);
 int ed_sector_destroy(ed_sector* s);
 int ed_sector_get_info(const ed_sector* s, ed_sector_info* info);
 

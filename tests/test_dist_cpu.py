@@ -86,3 +86,76 @@ def test_gloo_split_matches_full(world):
         assert err < 1e-12
         assert nl == nr == 40
         assert da < 1e-10 and db < 1e-10
+
+
+# ---------------------------------------------------------------- row split
+def _row_cfg():
+    from cases import nonsu2_rand
+
+    return nonsu2_rand()                 # nonsu2 with Jx/Jp and spin flips: no Kronecker form
+
+
+def test_mpi_split_matches_reference_rule():
+    """build_Hv_sector: mpiQ = dim/size rows per rank, remainder on the last
+    rank (ED_HAMILTONIAN.f90:55-62)."""
+    from edgpu.dist import mpi_split
+
+    assert mpi_split(10, 3) == ([0, 3, 6], [3, 3, 4])
+    assert mpi_split(4900, 8)[1][-1] == 4900 // 8 + 4900 % 8
+
+
+def _row_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from edgpu.dist import DistRowSector, dist_lanczos
+    from oracle.oracle import Oracle, lanc_tridiag
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = _row_cfg()
+    orc = Oracle(cfg)
+    hmap = orc.build_sector(6, 0)
+    rp, cols, vals = orc.build_csr(hmap)
+    import scipy.sparse as sp
+
+    n = len(hmap)
+    H = sp.csr_matrix((vals, cols, rp), shape=(n, n))
+    from edgpu.dist import mpi_split
+
+    r0, cnt = mpi_split(n, world)
+    Hloc = H[r0[rank]:r0[rank] + cnt[rank]]
+    ds = DistRowSector(hxv_rows=lambda v: torch.from_numpy(Hloc @ v.numpy()), dim=n)
+    i = np.arange(1, n + 1, dtype=np.float64)
+    x = torch.from_numpy(np.sin(i) + 1j * np.cos(3 * i))
+    y = ds.gather(ds.hxv(ds.scatter(x)))
+    err = float(np.max(np.abs(y.numpy() - H @ x.numpy())))
+    a, b, nl = dist_lanczos(ds, ds.scatter(x), 40)
+    ar, br, nr = lanc_tridiag((rp, cols, vals), x.numpy(), 40)
+    q.put((rank, err, float(np.max(np.abs(a[:30] - ar[:30]))), float(np.max(np.abs(b[:30] - br[:30]))), nl, nr,
+           ds.local_dim))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_row_split_matches_full(world):
+    """spMatVec_mpi_cc semantics on `world` gloo ranks: local rows, Allgatherv
+    of the vector, distributed plain Lanczos."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_row_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from oracle.oracle import Oracle
+
+    dim = len(Oracle(_row_cfg()).build_sector(6, 0))
+    assert sum(o[6] for o in out) == dim
+    for rank, err, da, db, nl, nr, _ in out:
+        assert err < 1e-12
+        assert nl == nr == 40
+        assert da < 1e-10 and db < 1e-10

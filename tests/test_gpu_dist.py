@@ -93,3 +93,95 @@ def test_split_two_ranks_one_gpu():
         assert p.exitcode == 0
     assert sum(o[2] for o in out) == 252 * 252
     assert all(o[1] < 1e-13 for o in out)
+
+
+# ---------------------------------------------------------------- row split
+@pytest.mark.parametrize("name", ["nonsu2_rand", "superc_2orb", "normal_jh", "nonsu2_jz"])
+@pytest.mark.parametrize("stored", [True, False])
+def test_row_sectors_match_oracle(name, stored):
+    """ed_sector_create_rows: every row block of H·v equals the oracle's
+    spMatVec_cc rows bit for bit (stored) / to 1e-13 (matrix-free generic)."""
+    import cases
+    from edgpu.dist import mpi_split
+    from edgpu.hamiltonian import Sector
+    from oracle.oracle import Oracle, spmv, start_vector
+
+    cfg = getattr(cases, name)()
+    q = [c for c in cases.CASES if c[0] == name][0][2][0]
+    orc = Oracle(cfg)
+    hmap = orc.build_sector(*q)
+    csr = orc.build_csr(hmap)
+    n = len(hmap)
+    x = start_vector(n)
+    ref = spmv(csr, x)
+    xd = torch.from_numpy(x).cuda()
+    r0, cnt = mpi_split(n, 3)
+    parts = []
+    for a, c in zip(r0, cnt):
+        with Sector(cfg, *q, stored=stored, direct=not stored, rows=(a, c)) as S:
+            assert (S.row0, S.nrows, S.dim) == (a, c, n)
+            y = torch.empty(c, dtype=torch.complex128, device="cuda")
+            S.hxv_dev(xd, y)
+            if stored:
+                rp, cols, vals = S.dump_csr()
+                assert rp[-1] == csr[0][a + c] - csr[0][a]
+                assert np.array_equal(cols, csr[1][csr[0][a]:csr[0][a + c]])
+            parts.append(y.cpu().numpy())
+    y = np.concatenate(parts)
+    if stored:
+        assert np.array_equal(y, ref)
+    else:
+        assert np.max(np.abs(y - ref)) <= 1e-13 * np.max(np.abs(ref))
+
+
+def test_row_sector_refuses_whole_sector_calls():
+    from edgpu._lib import EDGPUError
+    from edgpu.hamiltonian import Sector
+
+    cfg = make_config(Norb=1, Nbath=5)
+    with Sector(cfg, 3, 3, stored=True, rows=(0, 100)) as S:
+        with pytest.raises(EDGPUError, match="row-split"):
+            S.lanc_eigh(nitermax=50, threshold=1e-12)
+
+
+def _row_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "dmft-ed_amd"), os.path.join(root, "tests")]
+    import torch.distributed as dist
+    from cases import nonsu2_rand
+    from edgpu.dist import DistRowSector, dist_lanczos
+    from oracle.oracle import Oracle, lanc_tridiag, spmv, start_vector
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)                       # both ranks share the box's one GPU
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = nonsu2_rand()
+    ds = DistRowSector(cfg, 6, 0)
+    orc = Oracle(cfg)
+    csr = orc.build_csr(orc.build_sector(6, 0))
+    x = start_vector(ds.dim)
+    y = ds.gather(ds.hxv(ds.scatter(torch.from_numpy(x).cuda())))
+    exact = bool(np.array_equal(y.cpu().numpy(), spmv(csr, x)))
+    a, b, nl = dist_lanczos(ds, ds.scatter(torch.from_numpy(x).cuda()), 30)
+    ar, br, nr = lanc_tridiag(csr, x, 30)
+    q.put((rank, exact, float(np.max(np.abs(a[:20] - ar[:20]))), nl, nr, ds.local_dim))
+    ds.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_row_split_two_ranks_one_gpu():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_row_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=300) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for rank, exact, da, nl, nr, _ in out:
+        assert exact and nl == nr == 30 and da < 1e-10
