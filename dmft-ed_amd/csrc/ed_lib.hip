@@ -1331,6 +1331,7 @@ struct Trlan {
   hipStream_t st = nullptr;
   int64_t dim = 0;
   int G = 1, m = 0;
+  bool fused = true;  // ED_GPU_TRLAN_UNFUSED=1: the four-sweep CGS2 (A/B)
   V *Vb = nullptr, *Xb = nullptr, *w = nullptr;
   double2 *h = nullptr, *coef = nullptr, *part = nullptr;
   double *Y = nullptr, *npart = nullptr, *alpha = nullptr, *beta = nullptr;
@@ -1349,7 +1350,30 @@ struct Trlan {
   V* col(V* b, int c) { return b + (int64_t)c * dim; }
   // x -= V[:, :ncol] V[:, :ncol]^H x, twice; coef = summed coefficients;
   // with jn >= 0: alpha[jn], beta[jn] = ||x|| afterwards
+  // one fused sweep (k_cgs) with the column group rounded up to 8/16/24/32
+  bool cgs(int ncol, const double2* hin, V* x, double2* pt, double* np) {
+    const int nc = (ncol + 7) / 8 * 8;
+#define ED_CGS(NCV) \
+  hipLaunchKernelGGL((k_cgs<VC, NCV>), dim3(G), dim3(kBlock), 0, st, Vb, ncol, hin, x, dim, pt, np)
+    if (nc <= 8) ED_CGS(8);
+    else if (nc <= 16) ED_CGS(16);
+    else if (nc <= 24) ED_CGS(24);
+    else if (!VC && nc <= 32) ED_CGS(32);
+    else return false;
+#undef ED_CGS
+    return true;
+  }
   int orth(int ncol, V* x, int jn) {
+    // fused CGS2: dots | x -= V h1, dots | x -= V h2, |x|^2  (V streamed 3x)
+    if (fused && ncol > 0 && cgs(ncol, nullptr, x, part, nullptr)) {
+      hipLaunchKernelGGL(k_vdot_fin<VC>, dim3(ncol), dim3(kBlock), 0, st, part, G, h, coef, 0);
+      cgs(ncol, h, x, part, nullptr);
+      hipLaunchKernelGGL(k_vdot_fin<VC>, dim3(ncol), dim3(kBlock), 0, st, part, G, h, coef, 1);
+      cgs(ncol, h, x, nullptr, npart);
+      hipLaunchKernelGGL(k_trl_coef, dim3(1), dim3(kBlock), 0, st, npart, G, coef, jn >= 0 ? jn : m,
+                         jn >= 0 ? alpha : nullptr, beta);
+      return ED_OK;
+    }
     if (ncol == 0) {
       hipLaunchKernelGGL(k_vaxpy<VC>, dim3(G), dim3(kBlock), 0, st, Vb, 0, h, x, dim, npart);
     }
@@ -1404,6 +1428,13 @@ struct Trlan {
   }
 };
 
+// blocks of the O(dim) Krylov sweeps (ED_GPU_TRLAN_GRID overrides, A/B)
+static int trlan_grid_cap() {
+  const char* e = getenv("ED_GPU_TRLAN_GRID");
+  const int g = e ? atoi(e) : 1024;
+  return std::max(1, std::min(g, 8192));
+}
+
 template <bool VC>
 static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, const void* v0,
                      double* evals, void* evecs, int32_t* nconv, int32_t* nhv) {
@@ -1413,7 +1444,8 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
   T.path = resolve_path(s, -1);
   T.st = s->stream;
   T.dim = s->dim;
-  T.G = (int)std::min<int64_t>(grid_for(s->dim), 512);
+  T.G = (int)std::min<int64_t>(grid_for(s->dim), trlan_grid_cap());
+  T.fused = !getenv("ED_GPU_TRLAN_UNFUSED");
   const int64_t dim = s->dim;
   const int m = (int)std::min<int64_t>(ncv, dim);
   T.m = m;

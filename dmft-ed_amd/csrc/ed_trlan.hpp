@@ -10,9 +10,13 @@
 //   k_vaxpy       w -= sum_c V_c h_c
 //   k_rotate      X_k = sum_c V_c Y(c,k)      (restart / Ritz vectors)
 //   k_scale_into  V_{j+1} = w / beta
+//   k_cgs         fused CGS2 sweep: x -= V h (optional), then the block
+//                 partials of <V_c, x> and/or |x|^2 from the same V loads, so
+//                 a CGS2 orthogonalisation streams V three times, not four
 // All loops are grid-strided over rows with coalesced column accesses.
 #pragma once
 #include "ed_kernels.hpp"
+#include "ed_persist.hpp"
 
 namespace edg {
 
@@ -151,6 +155,98 @@ __global__ void __launch_bounds__(kBlock) k_scale_into(const val_t<VC>* __restri
   const double inv = nrm[0] > 0.0 ? 1.0 / nrm[0] : 0.0;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < dim; i += (int64_t)gridDim.x * kBlock)
     y[i] = scl(inv, x[i]);
+}
+
+// Fused CGS sweep over the rows of x (one column group of up to NC columns
+// held in registers per row):
+//   hin != nullptr : x_i -= sum_{c<ncol} V_c,i hin_c   (written back)
+//   part != nullptr: part[c*G + b] = block partial of <V_c, x> after the update
+//   npart != nullptr: npart[b]     = block partial of |x|^2 after the update
+// The row loop, the per-thread accumulation order and the subtraction order
+// are those of k_vdot_part / k_vaxpy; the block sums use DPP wave sums and one
+// barrier for all 2*NC+1 partials.
+template <bool VC, int NC>
+__global__ void __launch_bounds__(kBlock) k_cgs(const val_t<VC>* __restrict__ V, int ncol,
+                                                const double2* __restrict__ hin,
+                                                val_t<VC>* __restrict__ x, int64_t dim,
+                                                double2* __restrict__ part, double* __restrict__ npart) {
+  constexpr int NW = kBlock / 64;
+  constexpr int NR = (VC ? 2 * NC : NC) + 1;  // partial slots per wave
+  __shared__ double2 hs[NC];
+  __shared__ double red[NW][NR];
+  if (hin) {
+    for (int c = threadIdx.x; c < ncol; c += kBlock) hs[c] = hin[c];
+    __syncthreads();
+  }
+  double are[NC], aim[VC ? NC : 1];
+#pragma unroll
+  for (int c = 0; c < NC; c++) {
+    are[c] = 0.0;
+    if constexpr (VC) aim[c] = 0.0;
+  }
+  double n2 = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < dim; i += (int64_t)gridDim.x * kBlock) {
+    val_t<VC> v[NC];
+#pragma unroll
+    for (int c = 0; c < NC; c++) v[c] = c < ncol ? V[(int64_t)c * dim + i] : vzero<val_t<VC>>();
+    auto xi = x[i];
+    if (hin) {
+#pragma unroll
+      for (int c = 0; c < NC; c++) {
+        if (c >= ncol) continue;  // uniform
+        if constexpr (VC) {
+          xi.x -= v[c].x * hs[c].x - v[c].y * hs[c].y;
+          xi.y -= v[c].x * hs[c].y + v[c].y * hs[c].x;
+        } else {
+          xi -= v[c] * hs[c].x;
+        }
+      }
+      x[i] = xi;
+    }
+    if (part) {
+#pragma unroll
+      for (int c = 0; c < NC; c++) {
+        const double2 t = cdotc(v[c], xi);
+        are[c] += t.x;
+        if constexpr (VC) aim[c] += t.y;
+      }
+    }
+    if (npart) n2 += redot(xi, xi);
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (part) {
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+      if (c >= ncol) continue;  // uniform
+      const double r = wave_sum_dpp(are[c]);
+      if (lane == 63) red[wv][c] = r;
+      if constexpr (VC) {
+        const double q = wave_sum_dpp(aim[c]);
+        if (lane == 63) red[wv][NC + c] = q;
+      }
+    }
+  }
+  if (npart) {
+    const double r = wave_sum_dpp(n2);
+    if (lane == 63) red[wv][NR - 1] = r;
+  }
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (part && t < ncol) {
+    double re = 0.0, im = 0.0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+      re = re + red[w][t];
+      if constexpr (VC) im = im + red[w][NC + t];
+    }
+    part[(int64_t)t * gridDim.x + blockIdx.x] = make_double2(re, im);
+  }
+  if (npart && t == kBlock - 1) {
+    double r = 0.0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) r = r + red[w][NR - 1];
+    npart[blockIdx.x] = r;
+  }
 }
 
 }  // namespace edg
