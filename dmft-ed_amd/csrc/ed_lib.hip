@@ -1363,15 +1363,19 @@ struct Trlan {
 #undef ED_CGS
     return true;
   }
-  int orth(int ncol, V* x, int jn) {
+  int orth(int ncol, V* x, int jn, V* out = nullptr) {
     // fused CGS2: dots | x -= V h1, dots | x -= V h2, |x|^2  (V streamed 3x)
     if (fused && ncol > 0 && cgs(ncol, nullptr, x, part, nullptr)) {
       hipLaunchKernelGGL(k_vdot_fin<VC>, dim3(ncol), dim3(kBlock), 0, st, part, G, h, coef, 0);
       cgs(ncol, h, x, part, nullptr);
       hipLaunchKernelGGL(k_vdot_fin<VC>, dim3(ncol), dim3(kBlock), 0, st, part, G, h, coef, 1);
       cgs(ncol, h, x, nullptr, npart);
-      hipLaunchKernelGGL(k_trl_coef, dim3(1), dim3(kBlock), 0, st, npart, G, coef, jn >= 0 ? jn : m,
-                         jn >= 0 ? alpha : nullptr, beta);
+      if (out && jn >= 0)  // + V_{j+1} = x / beta_j in the same launch
+        hipLaunchKernelGGL(k_coef_scale<VC>, dim3(G), dim3(kBlock), 0, st, npart, G, coef, jn, alpha, beta,
+                           x, out, dim);
+      else
+        hipLaunchKernelGGL(k_trl_coef, dim3(1), dim3(kBlock), 0, st, npart, G, coef, jn >= 0 ? jn : m,
+                           jn >= 0 ? alpha : nullptr, beta);
       return ED_OK;
     }
     if (ncol == 0) {
@@ -1386,6 +1390,8 @@ struct Trlan {
     }
     hipLaunchKernelGGL(k_trl_coef, dim3(1), dim3(kBlock), 0, st, npart, G, coef, jn >= 0 ? jn : m,
                        jn >= 0 ? alpha : nullptr, beta);  // beta[m]: scratch slot
+    if (out && jn >= 0)
+      hipLaunchKernelGGL(k_scale_into<VC>, dim3(grid_for(dim)), dim3(kBlock), 0, st, x, out, beta + jn, dim);
     return ED_OK;
   }
   // Lanczos step j: w = H V_j, CGS2, alpha_j, beta_j; V_{j+1} = w / beta_j
@@ -1393,10 +1399,7 @@ struct Trlan {
     nhv++;
     EpiStore<VC> e{w};
     CK(launch_hxv<VC>(s, path, col(Vb, j), e, st));
-    CK(orth(j + 1, w, j));
-    if (j + 1 < m)
-      hipLaunchKernelGGL(k_scale_into<VC>, dim3(grid_for(dim)), dim3(kBlock), 0, st, w, col(Vb, j + 1),
-                         beta + j, dim);
+    CK(orth(j + 1, w, j, j + 1 < m ? col(Vb, j + 1) : nullptr));
     return ED_OK;
   }
   int sweep(int j0) {

@@ -157,6 +157,28 @@ __global__ void __launch_bounds__(kBlock) k_scale_into(const val_t<VC>* __restri
     y[i] = scl(inv, x[i]);
 }
 
+// k_trl_coef + k_scale_into in one launch (grid-strided): every block forms
+// the same fixed-order sum of the norm partials; block 0 stores alpha/beta,
+// all blocks write out = x / ||x|| (zeros for a zero norm).
+template <bool VC>
+__global__ void __launch_bounds__(kBlock) k_coef_scale(const double* __restrict__ npart, int G,
+                                                       const double2* __restrict__ coef, int j,
+                                                       double* __restrict__ alpha, double* __restrict__ beta,
+                                                       const val_t<VC>* __restrict__ x,
+                                                       val_t<VC>* __restrict__ out, int64_t dim) {
+  double t = 0.0;
+  for (int b = threadIdx.x; b < G; b += kBlock) t += npart[b];
+  t = block_sum(t);
+  const double nrm = sqrt(t);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    beta[j] = nrm;
+    if (alpha) alpha[j] = coef[j].x;
+  }
+  const double inv = nrm > 0.0 ? 1.0 / nrm : 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < dim; i += (int64_t)gridDim.x * kBlock)
+    out[i] = scl(inv, x[i]);
+}
+
 // Fused CGS sweep over the rows of x (one column group of up to NC columns
 // held in registers per row):
 //   hin != nullptr : x_i -= sum_{c<ncol} V_c,i hin_c   (written back)
