@@ -2020,6 +2020,96 @@ int ed_sector_apply_op_acc(const ed_sector* src, const ed_sector* dst, int32_t o
   return ED_OK;
 }
 
+// Poles of one GF continued fraction: eigenvalues of tridiag(alfa[0:n],
+// beta[1:n]) and the squared first components of the eigenvectors, the
+// quantities add_to_lanczos_gf_nonsu2 takes from tql2 (ED_GF_NONSU2.f90:936,
+// ED_GF_SHARED.f90:76-214; add_to_lanczos_gf_normal uses eigh,
+// ED_GF_NORMAL.f90:612-618).  The EISPACK implicit-QL iteration with the
+// rotations applied to the first row of Z only (Z starts as the identity, so
+// that row starts as e_1): O(n^2) instead of the O(n^3) full eigenvector
+// accumulation; same pythag, shifts and convergence test as tql2.
+static double ql_pythag(double a, double b) {
+  double p = std::max(fabs(a), fabs(b));
+  if (p == 0.0) return p;
+  double r = std::min(fabs(a), fabs(b)) / p;
+  r = r * r;
+  for (;;) {
+    const double t = 4.0 + r;
+    if (t == 4.0) break;
+    const double q = r / t, u = 1.0 + 2.0 * q;
+    p = u * p;
+    const double qu = q / u;
+    r = (qu * qu) * r;
+  }
+  return p;
+}
+
+int ed_tridiag_poles(int32_t n, const double* alfa, const double* beta, double* E, double* z2) {
+  if (n < 1 || !alfa || !beta || !E || !z2) return fail(ED_ERR_ARG, "bad args");
+  std::vector<double> e(n, 0.0), z(n, 0.0);
+  for (int i = 0; i < n; i++) E[i] = alfa[i];
+  for (int i = 0; i + 1 < n; i++) e[i] = beta[i + 1];  // e[i] = T(i, i+1); e[n-1] = 0
+  z[0] = 1.0;
+  double f = 0.0, tst1 = 0.0;
+  for (int l = 0; l < n; l++) {
+    tst1 = std::max(tst1, fabs(E[l]) + fabs(e[l]));
+    int m = l;
+    while (m < n && tst1 + fabs(e[m]) != tst1) m++;
+    if (m >= n) m = n - 1;  // e[n-1] == 0 stops the scan at n-1
+    if (m != l) {
+      for (int it = 0;; it++) {
+        if (it >= 30) return fail(ED_ERR_NOCONV, "tridiagonal QL: no convergence");
+        const double g0 = E[l];
+        double p = (E[l + 1] - g0) / (2.0 * e[l]);
+        double r = ql_pythag(p, 1.0);
+        const double sr = p >= 0.0 ? fabs(r) : -fabs(r);
+        E[l] = e[l] / (p + sr);
+        E[l + 1] = e[l] * (p + sr);
+        const double dl1 = E[l + 1];
+        double h = g0 - E[l];
+        for (int i = l + 2; i < n; i++) E[i] -= h;
+        f += h;
+        p = E[m];
+        double c = 1.0, c2 = 1.0, c3 = 1.0, s = 0.0, s2 = 0.0;
+        const double el1 = e[l + 1];
+        for (int i = m - 1; i >= l; i--) {
+          c3 = c2;
+          c2 = c;
+          s2 = s;
+          const double g = c * e[i];
+          h = c * p;
+          r = ql_pythag(p, e[i]);
+          e[i + 1] = s * r;
+          s = e[i] / r;
+          c = p / r;
+          p = c * E[i] - s * g;
+          E[i + 1] = h + s * (c * g + s * E[i]);
+          const double zh = z[i + 1];  // first row of Z only
+          z[i + 1] = s * z[i] + c * zh;
+          z[i] = c * z[i] - s * zh;
+        }
+        p = -s * s2 * c3 * el1 * e[l] / dl1;
+        e[l] = s * p;
+        E[l] = c * p;
+        if (!(tst1 + fabs(e[l]) > tst1)) break;
+      }
+    }
+    E[l] += f;
+  }
+  // ascending order (selection sort, as tql2)
+  for (int i = 0; i + 1 < n; i++) {
+    int k = i;
+    for (int j = i + 1; j < n; j++)
+      if (E[j] < E[k]) k = j;
+    if (k != i) {
+      std::swap(E[i], E[k]);
+      std::swap(z[i], z[k]);
+    }
+  }
+  for (int i = 0; i < n; i++) z2[i] = z[i] * z[i];
+  return ED_OK;
+}
+
 int ed_sector_lanc_tridiag_dev(ed_sector* s, int32_t vtype, const void* v0_dev, int32_t nitermax,
                                double threshold, double* alfa, double* beta, int32_t* nlanc) {
   if (!s || !alfa || !beta || !v0_dev || nitermax < 1) return fail(ED_ERR_ARG, "bad args");

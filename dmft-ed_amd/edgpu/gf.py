@@ -10,13 +10,13 @@ G_{aa,ss}.  Per kept state |gs> (energy E_i), orbital a, spin s:
   * norm2 = <seed|seed>, seed /= sqrt(norm2);
   * nlanc = min(jdim, lanc_nGFiter) steps of sp_lanc_tridiag on the GPU
     (device-resident plain Lanczos from a device start vector);
-  * poles: eigen-decomposition of the tridiagonal (diag alfa, subdiag beta(2:),
-    LAPACK like the reference's eigh), weight norm2/Z * Z(1,j)^2,
+  * poles: eigenvalues and squared first eigenvector components of the
+    tridiagonal (diag alfa, subdiag beta(2:)) by `ed_tridiag_poles` (implicit
+    QL on the first row of Z, the tql2 iteration), weight norm2/Z * Z(1,j)^2,
     G(iw_n) += w/(iw_n - isign*(E_j - E_i)), G(w) += w/(w + i eps - isign*(E_j - E_i))
     with w_n = pi/beta (2n-1) and w = linspace(wini, wfin, Lreal)
     (allocate_grids, ED_AUX_FUNX.f90:449-461).
-The pole sum runs in torch on the GPU when one is present (200 poles x 10^4
-frequencies per seed), else in numpy.
+The pole sum runs in torch on the GPU (200 poles x 10^4 frequencies per seed).
 """
 from __future__ import annotations
 
@@ -58,39 +58,37 @@ def realaxis(wini: float, wfin: float, L: int) -> np.ndarray:
 
 
 def tridiag_poles(alfa: np.ndarray, beta: np.ndarray, n: int) -> Tuple[np.ndarray, np.ndarray]:
-    """Eigenvalues of tridiag(alfa(1:n), beta(2:n)) and squared first components."""
-    from scipy.linalg import eigh_tridiagonal
-
-    if n == 1:
-        return np.array([alfa[0]]), np.array([1.0])
-    # implicit QL/QR (LAPACK dstev, like SciFortran's tridiagonal eigh): MRRR
-    # (stemr) can fail on the near-degenerate ghost clusters that long
-    # unreorthogonalised GF runs produce
-    w, z = eigh_tridiagonal(alfa[:n], beta[1:n], lapack_driver="stev")
-    return w, z[0, :] ** 2
+    """Eigenvalues of tridiag(alfa(1:n), beta(2:n)) and squared first components
+    (tql2 / eigh of add_to_lanczos_gf_*, ED_GF_NONSU2.f90:936, ED_GF_NORMAL.f90:
+    612-618): `ed_tridiag_poles`, the implicit-QL iteration carrying only the
+    first row of the eigenvector matrix (O(n^2))."""
+    a = np.ascontiguousarray(alfa[:n], dtype=np.float64)
+    b = np.zeros(n, dtype=np.float64)
+    b[1:n] = beta[1:n]
+    E = np.empty(n, dtype=np.float64)
+    z2 = np.empty(n, dtype=np.float64)
+    check(_lib.load().ed_tridiag_poles(n, a.ctypes.data, b.ctypes.data, E.ctypes.data, z2.ctypes.data),
+          "ed_tridiag_poles")
+    return E, z2
 
 
 def add_poles(G_mats, G_real, peso_bz: float, Ei: float, E: np.ndarray, z2: np.ndarray,
               isign: int, wm: np.ndarray, wr: np.ndarray, eps: float) -> None:
-    """add_to_lanczos_gf_normal inner loops (ED_GF_NORMAL.f90:620-631), vectorised."""
+    """add_to_lanczos_gf_normal inner loops (ED_GF_NORMAL.f90:620-631), as one
+    (L x nlanc) broadcast on the GPU (no host fallback)."""
+    import torch
+
+    if not torch.cuda.is_available():
+        raise RuntimeError("add_poles: the Green's function pole sum runs on the GPU")
     de = E - Ei
     peso = peso_bz * z2
-    try:
-        import torch
-
-        if torch.cuda.is_available():
-            dev = "cuda"
-            iw = torch.from_numpy(1j * wm).to(dev)
-            rw = torch.from_numpy(wr + 1j * eps).to(dev)
-            p = torch.from_numpy(peso.astype(np.complex128)).to(dev)
-            d = torch.from_numpy((isign * de).astype(np.complex128)).to(dev)
-            G_mats += (p[None, :] / (iw[:, None] - d[None, :])).sum(1).cpu().numpy()
-            G_real += (p[None, :] / (rw[:, None] - d[None, :])).sum(1).cpu().numpy()
-            return
-    except Exception:
-        pass
-    G_mats += (peso[None, :] / ((1j * wm)[:, None] - isign * de[None, :])).sum(1)
-    G_real += (peso[None, :] / ((wr + 1j * eps)[:, None] - isign * de[None, :])).sum(1)
+    dev = "cuda"
+    iw = torch.from_numpy(1j * wm).to(dev)
+    rw = torch.from_numpy(wr + 1j * eps).to(dev)
+    p = torch.from_numpy(peso.astype(np.complex128)).to(dev)
+    d = torch.from_numpy((isign * de).astype(np.complex128)).to(dev)
+    G_mats += (p[None, :] / (iw[:, None] - d[None, :])).sum(1).cpu().numpy()
+    G_real += (p[None, :] / (rw[:, None] - d[None, :])).sum(1).cpu().numpy()
 
 
 def _seed(src: Sector, dst: Sector, op: int, terms, vec: np.ndarray, cplx: bool):

@@ -70,6 +70,7 @@ extern "C" {
 #define ED_ERR_HIP         3
 #define ED_ERR_OOM         4
 #define ED_ERR_UNSUPPORTED 5
+#define ED_ERR_NOCONV      6 /* iterative solve did not converge */
 
 /* ---------------------------------------------------------------- params
  * All arrays are C row-major over the MAXIMUM dimensions below; only the
@@ -240,6 +241,12 @@ int ed_sector_apply_op_acc(const ed_sector* src, const ed_sector* dst, int32_t o
 /* sp_lanc_tridiag from a device start vector (not modified). */
 int ed_sector_lanc_tridiag_dev(ed_sector* s, int32_t vtype, const void* v0_dev, int32_t nitermax,
                                double threshold, double* alfa, double* beta, int32_t* nlanc);
+/* GF poles of one continued fraction (host, O(n^2)): E[n] ascending eigenvalues
+ * of tridiag(alfa[0:n], beta[1:n]) and z2[n] the squared first components of
+ * their eigenvectors.  Replaces tql2 in add_to_lanczos_gf_nonsu2
+ * (ED_GF_NONSU2.f90:936; ED_GF_SHARED.f90:76-214) and eigh in
+ * add_to_lanczos_gf_normal (ED_GF_NORMAL.f90:612-618). */
+int ed_tridiag_poles(int32_t n, const double* alfa, const double* beta, double* E, double* z2);
 
 /* ------------------------------------------------------ reference-style API */
 int ed_gpu_init(const ed_params* p);          /* ed_init_solver parameter hand-over */

@@ -4,9 +4,20 @@ target H%map), tridiagonalisation by the oracle's lanczos_plain_tridiag_c,
 poles as add_to_lanczos_gf_normal (:580-632)."""
 import numpy as np
 
-from edgpu.gf import matsubara, realaxis, tridiag_poles
+from edgpu.gf import matsubara, realaxis
 from edgpu.sectors import c_sector, cdg_sector, setup_pointers
 from oracle.oracle import Oracle, lanc_tridiag
+
+
+def tridiag_poles(alfa, beta, n):
+    """Oracle poles for the normal-mode GF: LAPACK dstev (the eigh of
+    add_to_lanczos_gf_normal, ED_GF_NORMAL.f90:612-618), full eigenvectors."""
+    from scipy.linalg import eigh_tridiagonal
+
+    if n == 1:
+        return np.array([alfa[0]]), np.array([1.0])
+    w, z = eigh_tridiagonal(alfa[:n], beta[1:n], lapack_driver="stev")
+    return w, z[0, :] ** 2
 
 
 def _popcount_below(states, level):

@@ -92,3 +92,38 @@ def test_fortran_shim_compiles_and_binds():
     for sym in ("ed_gpu_hxv", "ed_gpu_init", "ed_gpu_build_sector", "ed_gpu_lanc_eigh",
                 "ed_gpu_lanc_tridiag", "ed_gpu_delete_sector", "ed_gpu_vecdim"):
         assert re.search(r"\sU\s+%s$" % sym, out, re.M), sym
+
+
+def test_tridiag_poles_host_matches_tql2_and_lapack():
+    """ed_tridiag_poles (host code of the C-ABI library, no device call): the
+    first-row implicit QL is bit-identical to the oracle's tql2
+    (ED_GF_SHARED.f90:76-214) and agrees with LAPACK dstev (the normal-mode
+    eigh, ED_GF_NORMAL.f90:612-618) to 1e-12 on GF-sized tridiagonals."""
+    from scipy.linalg import eigh_tridiagonal
+
+    from edgpu.gf import tridiag_poles
+    from oracle.oracle import tql2
+
+    rng = np.random.default_rng(7)
+    for n in (1, 2, 5, 64, 200):
+        a = rng.normal(size=n)
+        b = np.concatenate([[0.0], np.abs(rng.normal(size=n - 1))])
+        E, z2 = tridiag_poles(a, b, n)
+        assert np.all(np.diff(E) >= 0)
+        assert abs(z2.sum() - 1.0) < 1e-13
+        if n == 1:
+            assert E[0] == a[0] and z2[0] == 1.0
+            continue
+        W, Z, ierr = tql2(a.copy(), b.copy())
+        assert ierr == 0
+        np.testing.assert_array_equal(E, W)
+        np.testing.assert_array_equal(z2, Z[0] ** 2)
+        w, z = eigh_tridiagonal(a, b[1:], lapack_driver="stev")
+        np.testing.assert_allclose(E, w, atol=1e-12)
+        np.testing.assert_allclose(z2, z[0] ** 2, atol=1e-12)
+    # split tridiagonal (a zero off-diagonal: invariant subspace of the seed)
+    a = np.array([1.0, -2.0, 0.5, 3.0])
+    b = np.array([0.0, 0.7, 0.0, 0.2])
+    E, z2 = tridiag_poles(a, b, 4)
+    np.testing.assert_allclose(z2.sum(), 1.0, atol=1e-15)
+    assert np.count_nonzero(z2 > 1e-30) == 2
