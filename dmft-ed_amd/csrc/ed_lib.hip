@@ -69,7 +69,9 @@ struct LancWS {
   LancState* st = nullptr;
   double* partials = nullptr;   // [kMaxGrid]
   unsigned int* counter = nullptr;
-  double *alpha = nullptr, *beta = nullptr, *z = nullptr;
+  double *alpha = nullptr, *beta = nullptr, *z = nullptr;  // one block: alpha | beta | z, cap+2 each
+  double* h_ab = nullptr;       // pinned host staging for alpha | beta (2*(cap+2))
+  hipEvent_t ev[2] = {nullptr, nullptr};  // lanc_run timing
   void* basis = nullptr;
   int basis_cols = 0;
 };
@@ -173,11 +175,14 @@ static void sector_free(ed_sector* s) {
   if (!s) return;
   (void)hipSetDevice(s->device);
   if (s->gexec) (void)hipGraphExecDestroy(s->gexec);
+  for (hipEvent_t& e : s->ws.ev)
+    if (e) (void)hipEventDestroy(e);
   if (s->stream) {
     for (void* p : s->allocs) (void)hipFreeAsync(p, s->stream);
     (void)hipStreamSynchronize(s->stream);
     (void)hipStreamDestroy(s->stream);
   }
+  if (s->ws.h_ab) (void)hipHostFree(s->ws.h_ab);
   delete s;
 }
 
@@ -556,9 +561,17 @@ static int lanc_prepare(ed_sector* s, int vc, int cap, bool want_basis, int basi
 sized:
   if (cap > w.cap) {
     drop_graph(s);
-    CK(dalloc_t(s, &w.alpha, cap + 2));
-    CK(dalloc_t(s, &w.beta, cap + 2));
-    CK(dalloc_t(s, &w.z, cap + 2));
+    double* blk = nullptr;
+    CK(dalloc_t(s, &blk, 3 * ((size_t)cap + 2)));
+    w.alpha = blk;
+    w.beta = blk + (cap + 2);
+    w.z = blk + 2 * ((size_t)cap + 2);
+    if (w.h_ab) {
+      HIPCK(hipStreamSynchronize(s->stream));  // no copy into the old staging in flight
+      HIPCK(hipHostFree(w.h_ab));
+      w.h_ab = nullptr;
+    }
+    HIPCK(hipHostMalloc((void**)&w.h_ab, 2 * ((size_t)cap + 2) * sizeof(double), hipHostMallocDefault));
     w.cap = cap;
   }
   if (want_basis && basis_cols > w.basis_cols) {
@@ -585,8 +598,7 @@ template <bool VC>
 static int lanc_start(ed_sector* s, double thresh, hipStream_t st) {
   LancWS& w = s->ws;
   RedSlot slot{w.partials, w.counter};
-  HIPCK(hipMemsetAsync(w.beta, 0, (w.cap + 2) * sizeof(double), st));
-  HIPCK(hipMemsetAsync(w.alpha, 0, (w.cap + 2) * sizeof(double), st));
+  HIPCK(hipMemsetAsync(w.alpha, 0, 2 * (w.cap + 2) * sizeof(double), st));  // alpha | beta
   hipLaunchKernelGGL(k_lanc_init<VC>, dim3(grid_once(s->dim)), dim3(kBlock), 0, st,
                      (const val_t<VC>*)w.R, (val_t<VC>*)w.P, s->dim, w.st, thresh, slot);
   HIPCK(hipGetLastError());
@@ -1157,8 +1169,7 @@ static int persist_set_thresh(ed_sector* s, double thresh, hipStream_t st) {
   // argument, the kernel initialises the LancState fields on its first launch
   s->pthresh = thresh;
   HIPCK(hipMemsetAsync(s->ws.st, 0, sizeof(LancState), st));
-  HIPCK(hipMemsetAsync(s->ws.beta, 0, (s->ws.cap + 2) * sizeof(double), st));
-  HIPCK(hipMemsetAsync(s->ws.alpha, 0, (s->ws.cap + 2) * sizeof(double), st));
+  HIPCK(hipMemsetAsync(s->ws.alpha, 0, 2 * (s->ws.cap + 2) * sizeof(double), st));  // alpha | beta
   return ED_OK;
 }
 
@@ -1904,23 +1915,25 @@ int ed_sector_lanc_run(ed_sector* s, int32_t vtype, const void* v0_dev, int32_t 
   CK(make_driver(s, vtype, false, &d));
   CK(lanc_prepare(s, d.vc, niter, false, 0));
   CK(lanc_load_start(s, d.vc, v0_dev, true));
-  hipEvent_t e0, e1;
-  HIPCK(hipEventCreate(&e0));
-  HIPCK(hipEventCreate(&e1));
+  LancWS& w = s->ws;
+  for (hipEvent_t& e : w.ev)
+    if (!e) HIPCK(hipEventCreate(&e));
+  hipEvent_t e0 = w.ev[0], e1 = w.ev[1];
   int rc = d.start(1e-300);
   if (rc == ED_OK) {
     HIPCK(hipEventRecord(e0, d.st));
     rc = d.iters(niter, true);
     HIPCK(hipEventRecord(e1, d.st));
   }
-  // one host sync for the run and both coefficient copies
-  if (rc == ED_OK && alfa) HIPCK(hipMemcpyAsync(alfa, s->ws.alpha, niter * sizeof(double), hipMemcpyDeviceToHost, d.st));
-  if (rc == ED_OK && beta) HIPCK(hipMemcpyAsync(beta, s->ws.beta, niter * sizeof(double), hipMemcpyDeviceToHost, d.st));
+  // one host sync for the run and one pinned copy of alpha | beta
+  const size_t nab = (size_t)w.cap + 2 + niter;
+  if (rc == ED_OK && (alfa || beta))
+    HIPCK(hipMemcpyAsync(w.h_ab, w.alpha, nab * sizeof(double), hipMemcpyDeviceToHost, d.st));
   HIPCK(hipStreamSynchronize(d.st));
-  if (ms && rc == ED_OK) HIPCK(hipEventElapsedTime(ms, e0, e1));
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
   CK(rc);
+  if (alfa) memcpy(alfa, w.h_ab, niter * sizeof(double));
+  if (beta) memcpy(beta, w.h_ab + w.cap + 2, niter * sizeof(double));
+  if (ms) HIPCK(hipEventElapsedTime(ms, e0, e1));
   return ED_OK;
 }
 
