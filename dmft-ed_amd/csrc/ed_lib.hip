@@ -2130,7 +2130,9 @@ int ed_sector_lanc_tridiag_dev(ed_sector* s, int32_t vtype, const void* v0_dev, 
   LancDriver d;
   CK(make_driver(s, vtype, false, &d));
   CK(lanc_prepare(s, d.vc, nitermax, false, 0));
-  HIPCK(hipDeviceSynchronize());  // v0 may come from another stream
+  // v0_dev must be complete when this is called (the caller synchronises the
+  // stream that produced it): no device-wide sync, which would fail while
+  // another host thread captures a graph on its own sector stream
   CK(lanc_load_start(s, d.vc, v0_dev, true));
   CK(d.start(threshold));
   CK(d.iters(nitermax, true));

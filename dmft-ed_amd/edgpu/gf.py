@@ -47,6 +47,10 @@ class GFOptions:
     wfin: float = 5.0
     threshold: float = 1e-13      # sp_lanc_tridiag breakdown test (.repo/PLAIN_LANCZOS.f90:27)
     sparse_H: bool = True         # ed_sparse_H
+    # seeds solved concurrently on one GPU (host threads, each with its own
+    # device sectors); contributions are added to G in job order, so the
+    # result is bit-identical to the serial loop
+    workers: int = 4
 
 
 def matsubara(beta: float, L: int) -> np.ndarray:
@@ -115,8 +119,9 @@ def _seed(src: Sector, dst: Sector, op: int, terms, vec: np.ndarray, cplx: bool)
     norm2 = float(torch.sum(y.abs() ** 2).item())
     if norm2 > 0:
         y = y / np.sqrt(norm2)
-    torch.cuda.synchronize(x.device)
-    return y.contiguous(), norm2
+    y = y.contiguous()
+    st.synchronize()   # the seed is complete for the library's stream (no device-wide sync:
+    return y, norm2    # other threads may be capturing graphs)
 
 
 def _tridiag_dev(S: Sector, seed, nlanc: int, real: bool, threshold: float):
@@ -239,6 +244,45 @@ def _run_job(cfg, states, gopt, job, cache, wm, wr, G_m, G_r, record, zeta):
     add_poles(G_m, G_r, weight * norm2 / zeta, e_i, E, z2, isign, wm, wr, gopt.eps)
 
 
+def _run_jobs_threaded(cfg, states, gopt, jobs, todo, device, wm, wr, Gm, Gr, zeta):
+    """The seed loop on `gopt.workers` host threads (one sector cache per
+    thread); each job's pole sum goes into its own zero arrays, which are then
+    added to G in job order — the same sequence of additions as the serial
+    loop."""
+    import threading
+    from concurrent.futures import ThreadPoolExecutor
+
+    import torch
+
+    local = threading.local()
+    caches, lock = [], threading.Lock()
+
+    def init():
+        torch.cuda.set_device(device)   # the current device is per thread
+        local.cache = _SectorCache(cfg, gopt, device)
+        with lock:
+            caches.append(local.cache)
+
+    def work(n):
+        c_m = np.zeros(gopt.Lmats, dtype=np.complex128)
+        c_r = np.zeros(gopt.Lreal, dtype=np.complex128)
+        _run_job(cfg, states, gopt, jobs[n], local.cache, wm, wr, c_m, c_r, None, zeta)
+        return c_m, c_r
+
+    order = sorted(todo, key=lambda n: -jobs[n][5].dim)   # longest first
+    try:
+        with ThreadPoolExecutor(max_workers=min(gopt.workers, len(todo)), initializer=init) as ex:
+            futs = {n: ex.submit(work, n) for n in order}
+            for n in todo:
+                c_m, c_r = futs[n].result()
+                ispin, jspin, iorb = jobs[n][0]
+                Gm[ispin, jspin, iorb, iorb] += c_m
+                Gr[ispin, jspin, iorb, iorb] += c_r
+    finally:
+        for c in caches:
+            c.close()
+
+
 def _dist():
     try:
         import torch.distributed as dist
@@ -296,19 +340,22 @@ def build_gf(cfg: EDConfig, states: StateList, gopt: Optional[GFOptions] = None,
     else:
         mine = set(range(len(jobs)))
     zeta = float(states.size)       # T=0: zeta_function = state_list%size (ED_DIAG.f90:411)
-    cache = _SectorCache(cfg, gopt, device)
-    try:
-        for n, job in enumerate(jobs):
-            if n not in mine:
-                continue
-            ispin, jspin, iorb = job[0]
-            g_m, g_r = Gm[ispin, jspin, iorb, iorb], Gr[ispin, jspin, iorb, iorb]
-            if runner is None:
-                _run_job(cfg, states, gopt, job, cache, wm, wr, g_m, g_r, record, zeta)
-            else:
-                runner(cfg, states, gopt, job, wm, wr, g_m, g_r, zeta)
-    finally:
-        cache.close()
+    todo = [n for n in range(len(jobs)) if n in mine]
+    if runner is None and record is None and gopt.workers > 1 and len(todo) > 1:
+        _run_jobs_threaded(cfg, states, gopt, jobs, todo, device, wm, wr, Gm, Gr, zeta)
+    else:
+        cache = _SectorCache(cfg, gopt, device)
+        try:
+            for n in todo:
+                job = jobs[n]
+                ispin, jspin, iorb = job[0]
+                g_m, g_r = Gm[ispin, jspin, iorb, iorb], Gr[ispin, jspin, iorb, iorb]
+                if runner is None:
+                    _run_job(cfg, states, gopt, job, cache, wm, wr, g_m, g_r, record, zeta)
+                else:
+                    runner(cfg, states, gopt, job, wm, wr, g_m, g_r, zeta)
+        finally:
+            cache.close()
     if world > 1:
         import torch
 

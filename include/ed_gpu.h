@@ -239,6 +239,7 @@ int ed_sector_apply_op_acc(const ed_sector* src, const ed_sector* dst, int32_t o
                            double coef_re, double coef_im, int32_t vtype, const void* src_vec,
                            void* dst_vec, void* stream);
 /* sp_lanc_tridiag from a device start vector (not modified). */
+/* v0_dev must be complete on entry (synchronise the stream that wrote it). */
 int ed_sector_lanc_tridiag_dev(ed_sector* s, int32_t vtype, const void* v0_dev, int32_t nitermax,
                                double threshold, double* alfa, double* beta, int32_t* nlanc);
 /* GF poles of one continued fraction (host, O(n^2)): E[n] ascending eigenvalues
