@@ -518,7 +518,7 @@ __global__ void __launch_bounds__(kBlock) k_spmv(const val_t<HC>* __restrict__ d
   if (xcd) b = (b & 7) * (gridDim.x >> 3) + (b >> 3);  // one row range per XCD (see k_spmv_pk)
   for (int64_t i = b * kBlock + threadIdx.x; i < nslice * 64; i += (int64_t)gridDim.x * kBlock) {
     if (i < dim) {
-      const int64_t s = i >> 6;
+      const int64_t s = (int64_t)__builtin_amdgcn_readfirstlane((int)(i >> 6));  // wave-uniform (k_spmv_pk)
       const int64_t s0 = sptr[s];
       const int w = (int)((sptr[s + 1] - s0) >> 6);
       const int32_t* cp = cols + s0 + (i & 63);
@@ -630,7 +630,10 @@ __global__ void __launch_bounds__(kBlock) k_spmv_pk(const double* __restrict__ d
   __syncthreads();
   for (int64_t i = b * kBlock + threadIdx.x; i < nslice * 64; i += (int64_t)gridDim.x * kBlock) {
     if (i < dim) {
-      const int64_t s = i >> 6;
+      // one slice per wavefront (kBlock is a multiple of 64 and lane 0 holds the
+      // slice's first row): slice pointer and width are wave-uniform, so the
+      // pointer loads and the k-loop bound live in scalar registers
+      const int64_t s = (int64_t)__builtin_amdgcn_readfirstlane((int)(i >> 6));
       const int64_t s0 = sptr[s];
       const int w = (int)((sptr[s + 1] - s0) >> 6);
       const uint32_t* wp = words + s0 + (i & 63);
