@@ -7,15 +7,27 @@ sector (nup,ndw)=(4,4), dim 4,900, stored H in real(8), synthetic random bath
 `--niter` iterations (lanc_niter=512 by default) from a fixed start vector.
 value = Lanczos iterations/s summed over all ranks (weak scaling: every rank
 runs its own sector replica; sectors are independent, no collective in the
-data path).
-
-Also reported (rank 0):
-  * spmv_gbs: stored SpMV GB/s on the c2 sector (algorithmic bytes, L2-resident);
-  * roofline: stored SpMV on the Nlevels=28 (7,7) sector (dim 11,778,624,
-    nnz 176,679,360, real(8)) — the only size where HBM is the bound
-    (SURVEY §8d) — timed with HIP events on the launch stream;
-  * cpu_baseline: the oracle's row-gather CSR SpMV + plain recurrence
-    (restated reference algorithm), 1 host core, bounded sample.
+data path).  The timed runs take persistent MODE 4: one workgroup holds the
+stored matrix's entries in the Kronecker register layout (the stored SELL
+matrix has the form D + Hup(x)1 + 1(x)Hdw; its values, read back from the
+device matrix, sit in registers — DESIGN.md §1).  Beside it:
+  * stored_mode2_iters_per_s: the same sector with the stored matrix as ELL
+    words in registers (MODE 2, no Kronecker structure used);
+  * direct_iters_per_s: configs[2], matrix-free tables (MODE 4 from the hop
+    tables);
+  * complex_iters_per_s: complex(8) H and vectors (the reference's arithmetic);
+  * validation: the lowest Ritz value of the last timed run's tridiagonal
+    against the committed oracle E0 (tests/golden/c2_e0.json) at 1e-10.
+Sections (rank 0 prints, all ranks take part):
+  * farm_c4 (configs[3]), nonsu2_c5 (configs[4]) — asserted against the
+    committed oracle fixtures tests/golden/c4_diag_random.json /
+    c5_gf_random.npz;
+  * roofline: stored SpMV on the Nlevels=28 (7,7) sector (dim 11,778,624), the
+    only size where HBM is the bound, HIP events on the launch
+    stream; frac on the bytes the timed kernel moves;
+  * kron_n28: the matrix-free two-pass Kronecker H·v on the same sector;
+  * cpu_baseline: the oracle's row-gather CSR + plain recurrence (restated
+    reference loops, complex(8)) on 1 host core and on P processes.
 """
 from __future__ import annotations
 
@@ -26,7 +38,7 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-for p in (ROOT, os.path.join(ROOT, "dmft-ed_amd")):
+for p in (ROOT, os.path.join(ROOT, "dmft-ed_amd"), os.path.join(ROOT, "tests")):
     if p not in sys.path:
         sys.path.insert(0, p)
 
@@ -34,17 +46,19 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+GOLD = os.path.join(ROOT, "tests", "golden")
+PROFILES = os.path.join(ROOT, "profiles", "r2")
 
 
 def spmv_bytes_real(nnz, dim):
-    """Algorithmic bytes of one real(8) stored SpMV in the reference's CSR form
-    (SURVEY §8d): 12 nnz + 8 (dim+1) + 16 dim."""
+    """SURVEY §8(d) real(8) stored SpMV bytes in the reference's CSR form:
+    12 nnz + 8 (dim+1) + 16 dim."""
     return 12 * nnz + 8 * (dim + 1) + 16 * dim
 
 
 def spmv_bytes_packed(padded, dim):
-    """Algorithmic bytes of one packed SELL-64 SpMV (k_spmv_pk): 4-B words per
-    slot, slice pointers, real(8) diagonal, read v, write Hv."""
+    """Bytes the packed SELL-64 kernel (k_spmv_pk) moves: 4-B words per slot,
+    slice pointers, real(8) diagonal, read v, write Hv."""
     nslice = (dim + 63) // 64
     return 4 * padded + 8 * (nslice + 1) + 8 * dim + 16 * dim
 
@@ -61,8 +75,9 @@ def time_kernel(fn, iters, stream):
     return e0.elapsed_time(e1) / iters
 
 
-def measure_spmv(Sector, cfg, q, iters, warm=5, info=None):
-    with Sector(cfg, q[0], q[1], stored=True, direct=False, real=True) as S:
+def measure_hxv(Sector, cfg, q, iters, path=0, warm=5, info=None):
+    stored = path == 0
+    with Sector(cfg, q[0], q[1], stored=stored, direct=not stored, real=True) as S:
         dim, nnz = S.dim, S.nnz
         if info is not None:
             info.update(packed=int(S.info.packed), padded=int(S.info.padded), npdict=int(S.info.npdict))
@@ -70,31 +85,53 @@ def measure_spmv(Sector, cfg, q, iters, warm=5, info=None):
         y = torch.empty_like(x)
         st = torch.cuda.current_stream()
         for _ in range(warm):
-            S.hxv_dev(x, y, path=0, stream=st)
-        ms = time_kernel(lambda: S.hxv_dev(x, y, path=0, stream=st), iters, st)
+            S.hxv_dev(x, y, path=path, stream=st)
+        ms = time_kernel(lambda: S.hxv_dev(x, y, path=path, stream=st), iters, st)
         return dim, nnz, ms
 
 
-def cpu_baseline(budget_s=10.0):
-    """Oracle (restated reference loops) on 1 host core: plain Lanczos iters/s on c2."""
-    from edgpu.params import make_config
+def _cpu_worker(args):
+    seed, n, budget = args
+    from golden.golden_configs import c2_config
     from oracle.oracle import Oracle, lanc_tridiag, start_vector
 
-    cfg = make_config(Norb=1, Nbath=7, bath="random", seed=20251015)
-    orc = Oracle(cfg)
+    orc = Oracle(c2_config("random", seed))
     hmap = orc.build_sector(4, 4)
     csr = orc.build_csr(hmap)
     v0 = start_vector(len(hmap))
-    n = 200
     t0 = time.perf_counter()
     runs = 0
-    while time.perf_counter() - t0 < budget_s:
+    while time.perf_counter() - t0 < budget:
         lanc_tridiag(csr, v0, n, threshold=0.0)
         runs += 1
-    dt = time.perf_counter() - t0
-    return {"value": runs * n / dt, "unit": "Lanczos iters/s", "cores": 1, "kind": "port",
-            "sample": f"{runs} x {n}-step plain-Lanczos runs (complex(8), row-gather CSR, "
-                      f"c2 (4,4) sector, random bath) in {dt:.1f}s on 1 core"}
+    return runs * n, time.perf_counter() - t0
+
+
+def cpu_baseline(budget_s=8.0):
+    """The oracle (restated reference loops: complex(8) row-gather CSR
+    spMatVec_cc + the .repo/PLAIN_LANCZOS.f90 recurrence) on the host cores:
+    1 process, then P independent processes each on its own c2 replica (the
+    CPU analogue of the GPU's sector replicas).  P = the host CPUs this job
+    may use, capped at 16 (one GPU's share of the box)."""
+    from multiprocessing import get_context
+
+    try:
+        ncpu = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncpu = os.cpu_count() or 1
+    P = max(1, min(16, ncpu))
+    it1, dt1 = _cpu_worker((20251015, 200, budget_s))
+    with get_context("spawn").Pool(P) as pool:
+        res = pool.map(_cpu_worker, [(20251015 + r, 200, budget_s) for r in range(P)])
+    itp = sum(r[0] / r[1] for r in res)
+    return {"value": round(itp, 1), "unit": "Lanczos iters/s", "cores": P, "kind": "port",
+            "single_core": {"value": round(it1 / dt1, 1), "cores": 1},
+            "sample": f"c2 (4,4) sector, random bath, 200-step plain-Lanczos runs, complex(8) H and vectors "
+                      f"(the reference's arithmetic); 1 process for {dt1:.1f}s, then {P} processes x {budget_s:.0f}s "
+                      f"(one replica each, iters/s summed)",
+            "note": "the port is a C restatement of the reference loops; the reference's own Fortran "
+                    "(amdflang -O3, 1 core of the CPU container) ran 5,409 it/s on this sector "
+                    "(SURVEY §6, BASELINE.md), ~3.9x below the port's single-core rate"}
 
 
 def _timed(dist, fn):
@@ -119,45 +156,62 @@ def _timed(dist, fn):
 
 
 def bench_farm(dist, world, dev):
-    """configs[3]: all 169 (Nup,Ndw) sectors of Norb=2 Nbath=5 (Nlevels=24) through
-    ed_diag's default path (dense <= 256, device thick-restart Lanczos for the 6
+    """configs[3]: all 169 (Nup,Ndw) sectors of Norb=2 Nbath=5 through ed_diag's
+    default path (dense <= 256, device thick-restart Lanczos for the 6
     lowest otherwise), sectors farmed over the ranks (LPT), one all_gather of
-    eigenvalues.  Strong scaling: the same job on 1/2/4/8 GPUs."""
+    eigenvalues.  Strong scaling: the same job on 1/2/4/8 GPUs.  The result is
+    checked against the committed oracle fixture."""
     from edgpu.diag import DiagOptions
     from edgpu.farm import farm_diag
-    from edgpu.params import make_config
+    from golden.golden_configs import c4_config
 
-    cfg = make_config(Norb=2, Nbath=5, bath="random", seed=20251015)
+    cfg = c4_config("random")
     opt = DiagOptions()
     farm_diag(cfg, opt, device=dev)        # warm-up (code objects, allocator)
     dt, res = _timed(dist, lambda: farm_diag(cfg, opt, device=dev))
-    nloc = len(res.local)
+    with open(os.path.join(GOLD, "c4_diag_random.json")) as fh:
+        gold = json.load(fh)
+    worst = max(float(np.max(np.abs(np.asarray(res.eigenvalues[int(k)])[: len(g["eigenvalues"])]
+                                    - np.asarray(g["eigenvalues"])))) for k, g in gold["sectors"].items())
+    worst /= abs(gold["E0"])
+    e0_dev = abs(res.states.emin - gold["E0"]) / abs(gold["E0"])
+    assert e0_dev < 1e-10 and worst < 1e-10 and res.states.sectors == gold["states"]["sectors"], \
+        f"farm_c4 differs from the oracle fixture: E0 {e0_dev:.2e}, eigenvalues {worst:.2e}"
     return {"wall_s": round(dt, 4), "sectors": len(res.eigenvalues), "n_gpus": world,
             "E0": round(float(res.states.emin), 10), "gs_states": res.states.size,
-            "rank0_sectors": nloc, "scaling": "strong",
-            "workload": "configs[3]: Norb=2 Nbath=5 random bath, all sectors, lanc_method=arpack "
-                        "(Neigen=6, ncv=23) on device"}
+            "rank0_sectors": len(res.local), "scaling": "strong",
+            "parity": {"fixture": "tests/golden/c4_diag_random.json", "E0_rel_dev": e0_dev,
+                       "worst_eigenvalue_dev_rel_E0": worst, "bar": 1e-10},
+            "workload": "configs[3]: Norb=2 Nbath=5 Uloc=(2,2,0) Ust=1 Jh=0.5 random bath, all 169 sectors, "
+                        "lanc_method=arpack (Neigen=6, ncv=23) on device"}
 
 
 def bench_nonsu2(dist, world, dev):
     """configs[4]: nonSU2 Norb=1 Nbath=6 (Nlevels=14): complex ground state over
     all sectors + the Green's function (diagonal + spin-mixed seeds, 200-step
-    Lanczos each, Lmats=Lreal=5000), seeds farmed over the ranks."""
+    Lanczos each, Lmats=Lreal=5000), seeds farmed over the ranks; G(iw) checked
+    against the committed oracle fixture."""
     from edgpu.diag import DiagOptions
     from edgpu.farm import farm_diag
     from edgpu.gf import GFOptions, _job_list, build_gf
-    from edgpu.params import make_config
+    from golden.golden_configs import c5_config
 
-    cfg = make_config(Norb=1, Nbath=6, Nspin=2, ed_mode="nonsu2", bath="random", seed=20251015)
+    cfg = c5_config("random")
     opt = DiagOptions()
     gopt = GFOptions()
     res = farm_diag(cfg, opt, device=dev)
     build_gf(cfg, res.states, gopt, device=dev, owners=res.owners)   # warm-up
     t_diag, res = _timed(dist, lambda: farm_diag(cfg, opt, device=dev))
     t_gf, (Gm, _) = _timed(dist, lambda: build_gf(cfg, res.states, gopt, device=dev, owners=res.owners))
+    gold = np.load(os.path.join(GOLD, "c5_gf_random.npz"))
+    rel = float(np.max(np.abs(Gm[..., gold["iw_index"]] - gold["Gm"])) / np.max(np.abs(gold["Gm"])))
+    e0_dev = abs(res.states.emin - float(gold["E0"])) / abs(float(gold["E0"]))
+    assert rel < 1e-10 and e0_dev < 1e-10, f"nonsu2_c5 differs from the oracle fixture: G {rel:.2e}, E0 {e0_dev:.2e}"
     return {"diag_s": round(t_diag, 4), "gf_s": round(t_gf, 4), "n_gpus": world,
             "gf_seeds": len(_job_list(cfg, res.states)[0]), "E0": round(float(res.states.emin), 10),
             "G_iw0_00": [round(float(Gm[0, 0, 0, 0, 0].real), 10), round(float(Gm[0, 0, 0, 0, 0].imag), 10)],
+            "parity": {"fixture": "tests/golden/c5_gf_random.npz", "G_iw_max_rel_dev": rel, "E0_rel_dev": e0_dev,
+                       "bar": 1e-10},
             "workload": "configs[4]: nonSU2 Norb=1 Nbath=6 random bath, default (arpack) GS over all sectors "
                         "+ build_gf (diag + mixed seeds, nGFiter=200, L=5000)"}
 
@@ -182,6 +236,35 @@ def bench_split(dist, world, dev, iters=10):
             "dim": ds.du * ds.dd, "local_rows": nw,
             "workload": "Nlevels=28 Norb=1 Nbath=13 (7,7) sector split by down rows; Kronecker rows/cols "
                         "kernels + 2 all_to_all exchanges per H·v (RCCL; strip layout, no transposes)"}
+
+
+def _lanc_rate(S, niter, v0, reps=5, env=None):
+    """Best-of device time of `reps` niter-step runs -> iters/s (and the last α, β)."""
+    old = {k: os.environ.get(k) for k in (env or {})}
+    os.environ.update(env or {})
+    try:
+        for _ in range(2):
+            S.lanc_run(niter, v0_dev=v0)
+        runs = [S.lanc_run(niter, v0_dev=v0) for _ in range(reps)]
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    return niter / (min(r[2] for r in runs) * 1e-3), runs[-1]
+
+
+def _traffic(name):
+    """Per-launch HBM-side bytes from a committed rocprofv3 summary
+    (profiles/r2/<name>.json: 2 x FETCH_SIZE + WRITE_SIZE, the gfx950 x2
+    calibrated for 4/8/16-B lane loads in profiles/r2/fetch_calib.json)."""
+    f = os.path.join(PROFILES, name)
+    if not os.path.exists(f):
+        return None, None
+    with open(f) as fh:
+        tj = json.load(fh)
+    return tj.get("traffic_bytes_per_launch"), f"profiles/r2/{name}"
 
 
 def main():
@@ -219,10 +302,13 @@ def main():
 
     from edgpu.hamiltonian import Sector
     from edgpu.params import make_config
+    from golden.golden_configs import SEED, c2_config
 
-    cfg = make_config(Norb=1, Nbath=7, bath="random", seed=20251015 + rank)
+    seed = SEED + rank
+    cfg = c2_config("random", seed)
     S = Sector(cfg, 4, 4, stored=True, direct=False, real=True, device=dev)
     v0 = torch.sin(torch.arange(1, S.dim + 1, dtype=torch.float64, device="cuda"))
+    mode = S.lanc_mode(real=True, path=0)
 
     def step():
         return S.lanc_run(args.niter, v0_dev=v0)
@@ -238,9 +324,10 @@ def main():
     barrier()
     t0 = time.perf_counter()
     dev_ms = 0.0
+    last = None
     for _ in range(args.steps):
-        _, _, ms = step()
-        dev_ms += ms
+        last = step()
+        dev_ms += last[2]
     barrier()
     dt = time.perf_counter() - t0
     if dist:
@@ -250,14 +337,30 @@ def main():
     iters_total = args.steps * args.niter * world
     value = iters_total / dt
 
-    # configs[2]: the same sector through the matrix-free kernel (rank-local, untimed by the
-    # barrier bracket above; device time of the same 512-iteration runs)
-    Sd = Sector(cfg, 4, 4, stored=False, direct=True, real=True, device=dev)
-    for _ in range(2):
-        Sd.lanc_run(args.niter, v0_dev=v0)
-    dms = [Sd.lanc_run(args.niter, v0_dev=v0)[2] for _ in range(5)]
-    direct_ips = args.niter / (min(dms) * 1e-3)
-    Sd.close()
+    # validation of the timed work: lowest Ritz value of the last run's
+    # tridiagonal vs the oracle's E0 for this rank's bath (committed fixture)
+    from scipy.linalg import eigh_tridiagonal
+
+    a, b, _ = last
+    ritz = float(eigh_tridiagonal(a, b[1:], eigvals_only=True, select="i", select_range=(0, 0))[0])
+    with open(os.path.join(GOLD, "c2_e0.json")) as fh:
+        e0_ref = json.load(fh)["by_seed"].get(str(seed), {}).get("E0")
+    valid = None
+    if e0_ref is not None:
+        valid = {"ritz_min": ritz, "E0_oracle": e0_ref, "rel_dev": abs(ritz - e0_ref) / abs(e0_ref),
+                 "fixture": "tests/golden/c2_e0.json", "bar": 1e-10}
+        assert valid["rel_dev"] < 1e-10, f"timed Lanczos run: lowest Ritz value {ritz} vs oracle E0 {e0_ref}"
+
+    # configs[1] with the stored matrix as ELL words in registers (MODE 2, no
+    # Kronecker structure), complex(8) arithmetic, and configs[2] matrix-free
+    mode2_ips, _ = _lanc_rate(S, args.niter, v0, env={"ED_GPU_NO_PKRON": "1"})
+    with Sector(cfg, 4, 4, stored=True, direct=False, real=False, device=dev) as Sc:
+        vc = v0.to(torch.complex128)
+        cplx_ips, _ = _lanc_rate(Sc, args.niter, vc)
+        cplx_mode = Sc.lanc_mode(real=False, path=0)
+    with Sector(cfg, 4, 4, stored=False, direct=True, real=True, device=dev) as Sd:
+        direct_ips, _ = _lanc_rate(Sd, args.niter, v0)
+        direct_mode = Sd.lanc_mode(real=True, path=2)
 
     split = None if args.no_farm else bench_split(dist, world, dev)
     farm = None if args.no_farm else bench_farm(dist, world, dev)
@@ -266,42 +369,42 @@ def main():
     out = None
     if rank == 0:
         # SpMV GB/s on the headline sector (L2-resident; launch-latency bound)
-        dim2, nnz2, ms2 = measure_spmv(Sector, cfg, (4, 4), 2000)
+        dim2, nnz2, ms2 = measure_hxv(Sector, cfg, (4, 4), 2000)
         gbs2 = spmv_bytes_real(nnz2, dim2) / (ms2 * 1e-3) / 1e9
-        roof = None
+        roof, kron = None, None
         if not args.no_roofline:
-            cfg28 = make_config(Norb=1, Nbath=13, bath="random", seed=20251015)
+            cfg28 = make_config(Norb=1, Nbath=13, bath="random", seed=SEED)
             inf28 = {}
-            dim28, nnz28, ms28 = measure_spmv(Sector, cfg28, (7, 7), 50, info=inf28)
-            # achieved: SURVEY §8(d)'s algorithmic bytes for this unit (real(8) CSR
-            # stored SpMV).  The packed form moves fewer bytes, so this may exceed
-            # the physical rate; `traffic` is the PMC-measured HBM
-            # side and own_format_bytes the packed kernel's own algorithmic bytes.
-            B = spmv_bytes_real(nnz28, dim28)
-            Bown = spmv_bytes_packed(inf28["padded"], dim28) if inf28["packed"] else B
-            ach = B / (ms28 * 1e-3) / 1e9
-            traffic, tsrc = None, None
-            tfile = os.path.join(ROOT, "profiles", "r1", "spmv_n28_traffic.json")
-            if os.path.exists(tfile):   # PMC bytes cannot be read in-process: rocprofv3 passes
-                with open(tfile) as fh:
-                    tj = json.load(fh)
-                if bool(tj.get("packed", False)) == bool(inf28["packed"]):   # same kernel only
-                    traffic = tj["traffic_bytes_per_launch"]
-                    tsrc = ("profiles/r1/spmv_n28_traffic.json (rocprofv3 FETCH_SIZE/WRITE_SIZE "
-                            "passes, same kernel+sector)")
-            roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "traffic_source": tsrc,
-                    "achieved_basis": "SURVEY §8(d) real(8) stored SpMV bytes 12*nnz+8*(dim+1)+16*dim",
+            dim28, nnz28, ms28 = measure_hxv(Sector, cfg28, (7, 7), 50, path=0, info=inf28)
+            # frac on the bytes the timed kernel moves (its own format: 4-B
+            # {col|value index} words when packed); SURVEY §8(d)'s CSR-equivalent
+            # rate is reported beside it and can exceed the physical rate
+            Bcsr = spmv_bytes_real(nnz28, dim28)
+            Bown = spmv_bytes_packed(inf28["padded"], dim28) if inf28["packed"] else Bcsr
+            ach = Bown / (ms28 * 1e-3) / 1e9
+            traffic, tsrc = _traffic("spmv_n28_traffic.json")
+            roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
+                    "achieved_basis": ("bytes the timed kernel moves: 4*padded slots + 8*(nslice+1) + 8*dim "
+                                       "(diagonal) + 16*dim (read v, write Hv)") if inf28["packed"]
+                                      else "12*nnz + 8*(dim+1) + 16*dim",
                     "kernel": ("k_spmv_pk<real> (stored SELL-64, 32-bit {col|value index} words, "
                                f"{inf28['npdict']}-value dictionary)") if inf28["packed"]
                               else "k_spmv<real,real> (stored SELL-64 H·v)",
-                    "workload": f"Nlevels=28 Norb=1 Nbath=13 (7,7) sector, dim {dim28}, nnz {nnz28}, "
-                                f"real(8), {B} algorithmic bytes/launch",
-                    "ms_per_launch": round(ms28, 4),
-                    "own_format_bytes": Bown,
-                    "own_format_gbs": round(Bown / (ms28 * 1e-3) / 1e9, 1),
+                    "workload": f"Nlevels=28 Norb=1 Nbath=13 (7,7) sector, dim {dim28}, nnz {nnz28}, real(8)",
+                    "ms_per_launch": round(ms28, 4), "bytes_per_launch": Bown,
+                    "csr_equivalent_bytes": Bcsr,
+                    "csr_equivalent_gbs": round(Bcsr / (ms28 * 1e-3) / 1e9, 1),
                     "physical_gbs": round(traffic / (ms28 * 1e-3) / 1e9, 1) if traffic else None}
+            dimk, _, msk = measure_hxv(Sector, cfg28, (7, 7), 50, path=2)
+            Bk = 16 * dimk
+            tk, tksrc = _traffic("kron_n28_traffic.json")
+            kron = {"ms_per_hxv": round(msk, 4), "algorithmic_bytes": Bk,
+                    "achieved_gbs": round(Bk / (msk * 1e-3) / 1e9, 1),
+                    "frac": round(Bk / (msk * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                    "traffic": tk, "traffic_source": tksrc,
+                    "basis": "SURVEY §8(d) direct: 16*dim real (read v, write Hv)",
+                    "kernel": "k_kron_up + k_kron_dw (two-pass matrix-free Kronecker H·v)"}
         cpu = None if args.no_cpu else cpu_baseline()
         out = {
             "metric": "Lanczos SpMV GB/s + ground-state iters/s, Ns=16 half-filled sector, 1/2/4/8 GPU",
@@ -317,17 +420,24 @@ def main():
             "dtype": "f64",
             "data": "synthetic (seeded random bath per rank)",
             "config": {"workload": "c2: Norb=1 Nbath=7 (Nlevels=16) half-filled (4,4) sector, dim 4900, "
-                                   f"stored real(8) H, plain Lanczos {args.niter} iters/step",
+                                   f"stored real(8) H, plain Lanczos {args.niter} iters/step, persistent MODE "
+                                   f"{mode} (4 = stored matrix in the Kronecker register layout)",
                        "parallelism": f"sector replicas x{world}"},
             "device_ms_per_step": round(dev_ms / args.steps, 4),
+            "validation": valid,
+            "stored_mode2_iters_per_s": round(mode2_ips, 1),
+            "stored_mode2_note": "configs[1]: stored SELL matrix as ELL words {col|value} in registers (MODE 2)",
             "direct_iters_per_s": round(direct_ips, 1),
-            "direct_note": "configs[2]: same sector, matrix-free H·v (Kronecker form, tables in LDS), one GPU",
+            "direct_note": f"configs[2]: same sector, matrix-free hop tables (persistent MODE {direct_mode})",
+            "complex_iters_per_s": round(cplx_ips, 1),
+            "complex_note": f"complex(8) H and vectors, stored (persistent MODE {cplx_mode}); dtype of cpu_baseline",
             "spmv_gbs_c2": round(gbs2, 1),
             "spmv_ms_c2": round(ms2, 5),
             "farm_c4": farm,
             "split_n28": split,
             "nonsu2_c5": nonsu2,
             "roofline": roof,
+            "kron_n28": kron,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out))

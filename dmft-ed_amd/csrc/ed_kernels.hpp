@@ -311,6 +311,7 @@ template <bool VC>
 struct EpiStore {
   using V = val_t<VC>;
   V* hv;
+  V* scratch() const { return hv; }  // where a two-pass H·v puts its first pass
   __device__ __forceinline__ bool skip() const { return false; }
   __device__ __forceinline__ void prepare() {}
   __device__ __forceinline__ double row(int64_t i, V acc, V) {
@@ -347,6 +348,7 @@ struct EpiLancA {
   RedSlot slot;
   double invb, b;
   V* bcol;
+  V* scratch() const { return W; }  // W is rewritten row by row by row() itself
   __device__ __forceinline__ bool skip() const { return st->done != 0; }
   __device__ __forceinline__ void prepare() {
     invb = st->invb;
@@ -414,6 +416,7 @@ struct EpiLancFused {
   RedSlot slot;
   double invb, b;
   V* bcol;
+  V* scratch() const { return W; }  // W is rewritten row by row by row() itself
   __device__ __forceinline__ bool skip() const { return st->done != 0; }
   __device__ __forceinline__ void prepare() {
     invb = st->invb;
@@ -752,6 +755,205 @@ __global__ void __launch_bounds__(kBlock) k_kron(KronArgs<HC> K, const val_t<VC>
         acc = add(acc, mul(K.dwv[q], x[(int64_t)K.dwc[q] * du + iu]));
       }
       part += epi.row(i, acc, xi);
+    }
+  }
+  epi.finish(part);
+}
+
+// ------------------------------- matrix-free Kronecker form, two passes
+// k_kron reads every V row ~(1 + degdw) times: its down-hop gathers of the
+// rows V[iw'][:] have no cache locality (a hop jumps far in rank) and come
+// from the Infinity Cache, and its up-hop gathers and table loads go through
+// L1/L2 one thread per row (N28: 0.91 GB fetched for 0.19 GB of v/Hv).  Here
+// the two index directions are split so that each pass has locality:
+//   pass U (k_kron_up)  y[iw][:] = D[iw][:] .* V[iw][:] + V[iw][:] Hup^T
+//     one 1024-thread workgroup per 2 rows (1 if LDS is short) at a time:
+//     the rows are staged in LDS (two sets, one barrier per step), the
+//     up-hop gathers are LDS
+//     reads, the thread's up-hop words {col:16 | value index:8} and diagonal
+//     factors sit in registers for all rows of the workgroup;
+//   pass D (k_kron_dw)  Hv[iw][c] = y[iw][c] + sum_k Hdw[iw][k] V[k'][c]
+//     one wavefront per (row, 64-column chunk); each XCD sweeps its own
+//     column chunks, all its workgroups on the same chunk at once, so the
+//     chunk V[:][c0:c0+64] (dimdw x 512 B, 1.8 MB at N28) stays in the XCD's
+//     4 MB L2 and every V element is fetched once; the down-hop words are
+//     wave-uniform (scalar loads), values from an LDS dictionary, and all
+//     loads of a wave's 4 rows are issued before the first use.
+// Term order per element = k_kron's (diagonal, up hops in slot order, down
+// hops in slot order): bit-identical results.  The epilogue runs in pass D;
+// pass U writes into the epilogue's scratch (its output buffer).
+constexpr int kKronUpBlock = 1024;
+constexpr int kKronDictMax = 256;
+constexpr int kKronRowsPerWave = 4;   // pass D tile: 4 waves x 4 rows x 64 columns
+
+template <bool HC, bool VC, int CPT, int DEG, int kKronUpRows>
+__global__ void __launch_bounds__(kKronUpBlock) k_kron_up(KronArgs<HC> K, const uint32_t* __restrict__ upw,
+                                                          const val_t<HC>* __restrict__ updict, int ndict,
+                                                          const val_t<VC>* __restrict__ x, val_t<VC>* y) {
+  using V = val_t<VC>;
+  using H = val_t<HC>;
+  extern __shared__ __align__(16) unsigned char smem[];
+  H* sdict = (H*)smem;
+  const int du = (int)K.dimup;
+  const int64_t dd = K.dimdw;
+  const int dup = (du + 1) & ~1;
+  V* bufs = (V*)(smem + kKronDictMax * sizeof(H));  // 2 sets x kKronUpRows rows
+  const int t = threadIdx.x;
+  const int64_t G = gridDim.x;
+  for (int q = t; q < ndict; q += kKronUpBlock) sdict[q] = updict[q];
+  const int degup = K.degup;
+  uint32_t w[CPT][DEG];
+  H au[CPT];
+  int imu[CPT];
+#pragma unroll
+  for (int j = 0; j < CPT; j++) {
+    const int iu = t + kKronUpBlock * j;
+    const bool ok = iu < du;
+#pragma unroll
+    for (int k = 0; k < DEG; k++) w[j][k] = (ok && k < degup) ? upw[(int64_t)k * du + iu] : 0u;
+    au[j] = ok ? K.aup[iu] : mk<HC>(0.0, 0.0);
+    imu[j] = ok ? (int)K.impu[iu] : 0;
+  }
+  // kKronUpRows rows per step (iw = base + r*G), the next step's rows
+  // prefetched into registers while this step's are computed; with 2 rows
+  // the LDS image is interleaved ([column][row]): one gather fetches the
+  // column of both rows (ds_read_b128 for real vectors)
+  struct Pair {
+    V a, b;
+  };
+  V xr[kKronUpRows][CPT];
+  int64_t base = blockIdx.x;
+#pragma unroll
+  for (int r = 0; r < kKronUpRows; r++)
+#pragma unroll
+    for (int j = 0; j < CPT; j++) {
+      const int iu = t + kKronUpBlock * j;
+      const int64_t iw = base + r * G;
+      xr[r][j] = (iw < dd && iu < du) ? x[iw * du + iu] : vzero<V>();
+    }
+  int pb = 0;
+  for (; base < dd; base += kKronUpRows * G) {
+    V xc[kKronUpRows][CPT];
+#pragma unroll
+    for (int r = 0; r < kKronUpRows; r++)
+#pragma unroll
+      for (int j = 0; j < CPT; j++) xc[r][j] = xr[r][j];
+    V* buf = bufs + (size_t)pb * kKronUpRows * dup;
+#pragma unroll
+    for (int j = 0; j < CPT; j++) {
+      const int iu = t + kKronUpBlock * j;
+      if (iu < du) {
+        if constexpr (kKronUpRows == 2) ((Pair*)buf)[iu] = Pair{xr[0][j], xr[1][j]};
+        else buf[iu] = xr[0][j];
+      }
+    }
+    __syncthreads();  // rows staged; (two sets: the reads of the step before last are done)
+    const int64_t nb = base + kKronUpRows * G;
+#pragma unroll
+    for (int r = 0; r < kKronUpRows; r++)
+#pragma unroll
+      for (int j = 0; j < CPT; j++) {
+        const int iu = t + kKronUpBlock * j;
+        const int64_t iw = nb + r * G;
+        xr[r][j] = (iw < dd && iu < du) ? x[iw * du + iu] : vzero<V>();
+      }
+    H ad[kKronUpRows];
+    int imd[kKronUpRows];
+#pragma unroll
+    for (int r = 0; r < kKronUpRows; r++) {
+      const int64_t iw = base + r * G < dd ? base + r * G : base;
+      ad[r] = K.adw[iw];
+      imd[r] = K.impd[iw];
+    }
+    const bool second = kKronUpRows == 2 && base + G < dd;
+#pragma unroll
+    for (int j = 0; j < CPT; j++) {
+      const int iu = t + kKronUpBlock * j;
+      if (iu < du) {
+        V acc[kKronUpRows];
+#pragma unroll
+        for (int r = 0; r < kKronUpRows; r++) {
+          const auto d = add(add(au[j], ad[r]), mk<HC>(K.uimp[imu[j] * K.nimp + imd[r]], 0.0));
+          acc[r] = mul(d, xc[r][j]);
+        }
+#pragma unroll
+        for (int k = 0; k < DEG; k++)
+          if (k < degup) {
+            const H h = sdict[w[j][k] >> 16];
+            const int col = w[j][k] & 0xffffu;
+            if constexpr (kKronUpRows == 2) {
+              const Pair p = ((const Pair*)buf)[col];
+              acc[0] = add(acc[0], mul(h, p.a));
+              acc[1] = add(acc[1], mul(h, p.b));
+            } else {
+              acc[0] = add(acc[0], mul(h, buf[col]));
+            }
+          }
+        y[base * du + iu] = acc[0];
+        if (second) y[(base + G) * du + iu] = acc[kKronUpRows - 1];
+      }
+    }
+    pb ^= 1;
+  }
+}
+
+template <bool HC, bool VC, int DEG, class Epi>
+__global__ void __launch_bounds__(kBlock) k_kron_dw(KronArgs<HC> K, const uint32_t* __restrict__ dww,
+                                                    const val_t<HC>* __restrict__ dwdict, int ndict,
+                                                    const val_t<VC>* __restrict__ x, const val_t<VC>* ypart,
+                                                    Epi epi) {
+  using V = val_t<VC>;
+  using H = val_t<HC>;
+  if (epi.skip()) return;
+  epi.prepare();
+  __shared__ H sdict[kKronDictMax];
+  for (int q = threadIdx.x; q < ndict; q += kBlock) sdict[q] = dwdict[q];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t du = K.dimup, dd = K.dimdw;
+  const int degdw = K.degdw;
+  const int nchunk = (int)((du + 63) >> 6);
+  constexpr int R = kKronRowsPerWave;
+  constexpr int kTileRows = (kBlock / 64) * R;
+  const int64_t nrb = (dd + kTileRows - 1) / kTileRows;
+  // blocks are dealt round-robin to the 8 XCDs: XCD x = blockIdx % 8 takes
+  // chunks x, x+8, ...; its blocks walk (chunk, row block) tiles in order
+  const int xcd = blockIdx.x & 7;
+  const int64_t jb = blockIdx.x >> 3, g8 = gridDim.x >> 3;
+  const int mine = nchunk > xcd ? (nchunk - xcd + 7) / 8 : 0;
+  double part = 0.0;
+  for (int64_t u = jb; u < (int64_t)mine * nrb; u += g8) {
+    const int c = xcd + 8 * (int)(u / nrb);
+    const int64_t rb = u - (u / nrb) * nrb;
+    const int64_t iu = (int64_t)c * 64 + lane;
+    const bool ok = iu < du;
+    const int64_t r0 = rb * kTileRows + wv * R;  // wave-uniform
+    // every load of the wave's R rows in flight before any use
+    uint32_t wd[R][DEG];
+#pragma unroll
+    for (int r = 0; r < R; r++)
+#pragma unroll
+      for (int k = 0; k < DEG; k++) wd[r][k] = (r0 + r < dd && k < degdw) ? dww[(int64_t)k * dd + r0 + r] : 0u;
+    V g[R][DEG], yv[R], xv[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const int64_t i = (r0 + r) * du + iu;
+      const bool on = ok && r0 + r < dd;
+#pragma unroll
+      for (int k = 0; k < DEG; k++)
+        g[r][k] = (on && k < degdw) ? x[(int64_t)(wd[r][k] & 0xffffu) * du + iu] : vzero<V>();
+      xv[r] = on ? x[i] : vzero<V>();
+      yv[r] = on ? ldh<1>(ypart + i) : vzero<V>();  // streamed once: keep the L2 for the V chunk
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      if (!ok || r0 + r >= dd) continue;
+      V acc = yv[r];
+#pragma unroll
+      for (int k = 0; k < DEG; k++)
+        if (k < degdw) acc = add(acc, mul(sdict[wd[r][k] >> 16], g[r][k]));
+      part += epi.row((r0 + r) * du + iu, acc, xv[r]);
     }
   }
   epi.finish(part);

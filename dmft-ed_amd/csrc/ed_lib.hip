@@ -60,6 +60,12 @@ struct KronHost {
   void *upv = nullptr, *dwv = nullptr, *aup = nullptr, *adw = nullptr;
   double* uimp = nullptr;
   uint8_t *impu = nullptr, *impd = nullptr;
+  // two-pass form (k_kron_up + k_kron_dw): up-hop words {col:16 | value index:8}
+  bool two = false;
+  int cpt = 0, degU = 0, degD = 0;  // template values: columns per thread, slot bounds
+  uint32_t *upw = nullptr, *dww = nullptr;
+  void *updict = nullptr, *dwdict = nullptr;
+  int nupdict = 0, ndwdict = 0;
 };
 
 struct LancWS {
@@ -343,6 +349,65 @@ static void spin_diag(const EdModel& M, int sp, uint32_t x, double* re, double* 
   *im = i;
 }
 
+// Two-pass Kronecker tables (k_kron_up): the up-hop ELL slots as 32-bit words
+// {column:16 | index:8} over a dictionary of the distinct values (bit
+// patterns: exact).  Only for large sectors (dim >= 2^20; the small ones run
+// in the persistent kernels) whose up rows fit the register and LDS budget.
+static constexpr int64_t kKron2MinDim = (int64_t)1 << 20;
+static int build_kron_words(ed_sector* s, int sp, const std::vector<int32_t>& cols,
+                            const std::vector<double>& vals, int64_t nr, int deg) {
+  KronHost& K = s->K;
+  if (sp == 0) {
+    K.two = false;
+    const char* env = getenv("ED_GPU_KRON2");
+    if (env && env[0] == '0') return ED_OK;
+    if (s->dim < kKron2MinDim && !(env && env[0] == '1')) return ED_OK;
+    if (nr > 8192 || deg > 16) return ED_OK;
+    int cpt = 1;
+    while (cpt * kKronUpBlock < nr) cpt *= 2;
+    K.cpt = cpt;
+    K.degU = deg <= 8 ? 8 : 16;
+    if (cpt * K.degU > 64) return ED_OK;
+    K.two = true;
+  } else {
+    if (!K.two) return ED_OK;
+    K.two = false;
+    if (nr > 65535 || deg > 16) return ED_OK;
+    K.degD = deg <= 8 ? 8 : 16;
+  }
+  const int hw = s->hc ? 2 : 1;
+  std::map<std::pair<uint64_t, uint64_t>, uint32_t> idx;
+  std::vector<double> dict;
+  std::vector<uint32_t> words((size_t)deg * nr);
+  for (size_t q = 0; q < words.size(); q++) {
+    uint64_t x0 = 0, x1 = 0;
+    memcpy(&x0, &vals[hw * q], 8);
+    if (hw == 2) memcpy(&x1, &vals[2 * q + 1], 8);
+    auto it = idx.find({x0, x1});
+    uint32_t id;
+    if (it == idx.end()) {
+      id = (uint32_t)idx.size();
+      if (id >= (uint32_t)kKronDictMax) {  // too many distinct values: one-pass k_kron
+        K.two = false;
+        return ED_OK;
+      }
+      idx[{x0, x1}] = id;
+      for (int c = 0; c < hw; c++) dict.push_back(vals[hw * q + c]);
+    } else {
+      id = it->second;
+    }
+    words[q] = (uint32_t)cols[q] | (id << 16);
+  }
+  uint32_t*& wp = sp == 0 ? K.upw : K.dww;
+  void*& dp = sp == 0 ? K.updict : K.dwdict;
+  CK(upload(s, &wp, words));
+  CK(dalloc(s, &dp, dict.size() * 8));
+  CK(dcopy(s, dp, dict.data(), dict.size() * 8, hipMemcpyHostToDevice));
+  (sp == 0 ? K.nupdict : K.ndwdict) = (int)(dict.size() / hw);
+  K.two = true;
+  return ED_OK;
+}
+
 static int build_kron(ed_sector* s) {
   const SectorTables& T = s->T;
   const EdModel& M = s->Mh;
@@ -409,6 +474,7 @@ static int build_kron(ed_sector* s) {
     CK(dalloc(s, &da, a.size() * 8));
     CK(dcopy(s, da, a.data(), a.size() * 8, hipMemcpyHostToDevice));
     CK(upload(s, &di, imp));
+    CK(build_kron_words(s, sp, cols, vals, nr, deg));
     if (sp == 0) {
       K.degup = deg; K.upc = dc; K.upv = dv; K.aup = da; K.impu = di;
     } else {
@@ -461,9 +527,84 @@ static int xcd_remap() {
 static bool xcd_on(const ed_sector* s, int path) {
   return path == 0 && !s->hc && s->d_words && xcd_remap() && grid_for(s->nslice * 64) >= 1024;
 }
-static int hxv_blocks(const ed_sector* s, int path) {
+// pass D of the two-pass Kronecker H·v: a multiple of 8 blocks (XCD column
+// chunks), 8 resident per CU
+static constexpr int kKronDwGrid = 2048;
+// pass U LDS: dictionary + two sets of `rows` staged rows
+static size_t kron_up_lds(bool hc, bool vc, int64_t du, int rows) {
+  return kKronDictMax * (hc ? 16 : 8) + 2 * rows * (size_t)((du + 1) & ~1) * (vc ? 16 : 8);
+}
+static int kron_up_rows(bool hc, bool vc, int64_t du) { return kron_up_lds(hc, vc, du, 2) <= 160 * 1024 ? 2 : 1; }
+static bool kron2_on(const ed_sector* s, int path, int vc) {
+  if (path != 2 || !s->K.two) return false;
+  return kron_up_lds(s->hc, vc, s->K.dimup, 1) <= 160 * 1024;
+}
+static int hxv_blocks(const ed_sector* s, int path, int vc = 0) {
+  if (kron2_on(s, path, vc)) return kKronDwGrid;
   const int g = grid_for(s->nslice * 64);
   return xcd_on(s, path) ? (g & ~7) : g;
+}
+
+template <bool HC, bool VC, int CPT, int DEGU, int RU>
+static int launch_kron_up_t(ed_sector* s, const void* x, void* y, hipStream_t st) {
+  using V = val_t<VC>;
+  using H = val_t<HC>;
+  KronHost& K = s->K;
+  const size_t lds = kron_up_lds(HC, VC, K.dimup, RU);
+  auto fn = k_kron_up<HC, VC, CPT, DEGU, RU>;
+  static thread_local int attr_set = 0;
+  if (!attr_set) {
+    HIPCK(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    attr_set = 1;
+  }
+  static thread_local int up_grid = 0;  // per instantiation and LDS size (occupancy x CUs)
+  static thread_local size_t up_lds = 0;
+  if (!up_grid || up_lds != lds) {
+    up_lds = lds;
+    int per = 0, dev = 0, ncu = 0;
+    HIPCK(hipGetDevice(&dev));
+    HIPCK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)fn, kKronUpBlock, lds));
+    up_grid = std::max(per, 1) * ncu;
+  }
+  hipLaunchKernelGGL(fn, dim3((int)std::min<int64_t>(K.dimdw, up_grid)), dim3(kKronUpBlock), lds, st, kron_args<HC>(s), K.upw,
+                     (const H*)K.updict, K.nupdict, (const V*)x, (V*)y);
+  HIPCK(hipGetLastError());
+  return ED_OK;
+}
+
+template <bool HC, bool VC, int CPT, int DEGU>
+static int launch_kron_up(ed_sector* s, const void* x, void* y, hipStream_t st) {
+  if (kron_up_rows(HC, VC, s->K.dimup) == 2) return launch_kron_up_t<HC, VC, CPT, DEGU, 2>(s, x, y, st);
+  return launch_kron_up_t<HC, VC, CPT, DEGU, 1>(s, x, y, st);
+}
+
+template <bool HC, bool VC, class Epi>
+static int launch_kron2(ed_sector* s, const void* x, Epi epi, hipStream_t st) {
+  using V = val_t<VC>;
+  KronHost& K = s->K;
+  void* y = (void*)epi.scratch();
+  int rc;
+  switch (K.cpt * 100 + K.degU) {
+    case 108: rc = launch_kron_up<HC, VC, 1, 8>(s, x, y, st); break;
+    case 116: rc = launch_kron_up<HC, VC, 1, 16>(s, x, y, st); break;
+    case 208: rc = launch_kron_up<HC, VC, 2, 8>(s, x, y, st); break;
+    case 216: rc = launch_kron_up<HC, VC, 2, 16>(s, x, y, st); break;
+    case 408: rc = launch_kron_up<HC, VC, 4, 8>(s, x, y, st); break;
+    case 416: rc = launch_kron_up<HC, VC, 4, 16>(s, x, y, st); break;
+    case 808: rc = launch_kron_up<HC, VC, 8, 8>(s, x, y, st); break;
+    default: return fail(ED_ERR_STATE, "kron2: no instantiation for this geometry");
+  }
+  CK(rc);
+  using H = val_t<HC>;
+  if (K.degD == 8)
+    hipLaunchKernelGGL((k_kron_dw<HC, VC, 8, Epi>), dim3(kKronDwGrid), dim3(kBlock), 0, st, kron_args<HC>(s),
+                       K.dww, (const H*)K.dwdict, K.ndwdict, (const V*)x, (const V*)y, epi);
+  else
+    hipLaunchKernelGGL((k_kron_dw<HC, VC, 16, Epi>), dim3(kKronDwGrid), dim3(kBlock), 0, st, kron_args<HC>(s),
+                       K.dww, (const H*)K.dwdict, K.ndwdict, (const V*)x, (const V*)y, epi);
+  HIPCK(hipGetLastError());
+  return ED_OK;
 }
 
 template <bool HC, bool VC, class Epi>
@@ -497,6 +638,8 @@ static int launch_hxv_t(ed_sector* s, int path, const void* x, Epi epi, hipStrea
     DevIndex idx{s->d_off, s->d_rank, s->T.ns, s->T.nst - 1};
     hipLaunchKernelGGL((k_direct<HC, VC, Epi>), dim3(g), dim3(kBlock), 0, st, s->Md, s->d_map + s->row0,
                        idx, (const V*)x, xo, dim, ns, epi);
+  } else if (kron2_on(s, path, VC)) {
+    return launch_kron2<HC, VC>(s, x, epi, st);
   } else {
     hipLaunchKernelGGL((k_kron<HC, VC, Epi>), dim3(g), dim3(kBlock), 0, st, kron_args<HC>(s),
                        (const V*)x, dim, ns, epi);
@@ -608,7 +751,7 @@ static int lanc_start(ed_sector* s, double thresh, hipStream_t st) {
 template <bool VC>
 static int lanc_iter(ed_sector* s, int path, bool basis, hipStream_t st) {
   LancWS& w = s->ws;
-  const int g1 = hxv_blocks(s, path), g2 = grid_for(s->dim);
+  const int g1 = hxv_blocks(s, path, VC), g2 = grid_for(s->dim);
   const bool two1 = g1 > kTicketMaxBlocks, two2 = g2 > kTicketMaxBlocks;
   // single-kernel step: opt-in (measured slower on c2: 13.0 vs 8.9 us/step —
   // the last block's serial sc1 pass over all rows is latency-bound)
@@ -1449,6 +1592,102 @@ static int trlan_grid_cap() {
   return std::max(1, std::min(g, 8192));
 }
 
+// One thick-restart Lanczos solve on the columns [k0, m) of the basis; the
+// columns [0, k0) are locked (deflation: every new vector is orthogonalised
+// against them, their coefficients are not part of the projected matrix).
+// Start vector: v0 (host) if given, else a hash vector from `seed`.  Returns
+// the ma = m - k0 Ritz values (ascending) and the ma x ma rotation Z.
+template <bool VC>
+static int trlan_core(Trlan<VC>& T, int k0, int nev, int maxit, double tol, const void* v0, uint64_t seed,
+                      std::vector<double>& theta, std::vector<double>& Z, int* conv_out) {
+  using V = val_t<VC>;
+  const int m = T.m, ma = m - k0;
+  const int64_t dim = T.dim;
+  hipStream_t st = T.st;
+  const int g = grid_for(dim);
+  const int64_t nd = dim * (VC ? 2 : 1);
+  const size_t vs = sizeof(V);
+  // V_k0 = v0 / |v0| (orthogonal to the locked columns)
+  if (v0) HIPCK(hipMemcpyAsync(T.w, v0, dim * vs, hipMemcpyHostToDevice, st));
+  else if (seed == 0) hipLaunchKernelGGL(k_default_start, dim3(grid_for(nd)), dim3(kBlock), 0, st, (double*)T.w, nd);
+  else hipLaunchKernelGGL(k_hash_vec, dim3(grid_for(nd)), dim3(kBlock), 0, st, (double*)T.w, nd, seed);
+  CK(T.orth(k0, T.w, -1));  // CGS2 against the locked columns; the norm -> beta[m]
+  double b0 = 0.0;
+  HIPCK(hipMemcpyAsync(&b0, T.beta + m, sizeof(double), hipMemcpyDeviceToHost, st));
+  HIPCK(hipStreamSynchronize(st));
+  if (!(b0 > 0.0)) return fail(ED_ERR_ARG, "zero start vector");
+  hipLaunchKernelGGL(k_scale_into<VC>, dim3(g), dim3(kBlock), 0, st, T.w, T.col(T.Vb, k0), T.beta + m, dim);
+
+  std::vector<double> Tm((size_t)ma * ma, 0.0), al(m), be(m);
+  auto tm = [&](int i, int j) -> double& { return Tm[i + (size_t)ma * j]; };
+  int jstart = k0, conv = 0;
+  uint64_t rseed = seed * 7919 + 1;
+  for (int it = 0; it < maxit; it++) {
+    int j0 = jstart;
+    for (;;) {  // expansion j0..m-1, restarted past an invariant subspace
+      CK(T.sweep(j0));
+      HIPCK(hipMemcpyAsync(al.data(), T.alpha, m * sizeof(double), hipMemcpyDeviceToHost, st));
+      HIPCK(hipMemcpyAsync(be.data(), T.beta, m * sizeof(double), hipMemcpyDeviceToHost, st));
+      HIPCK(hipStreamSynchronize(st));
+      int jb = -1;
+      for (int j = j0; j < m; j++) {
+        const int l = j - k0;
+        tm(l, l) = al[j];
+        if (l + 1 < ma) tm(l, l + 1) = tm(l + 1, l) = be[j];
+        const double scale = fabs(al[j]) + (l > 0 ? fabs(tm(l - 1, l)) : 0.0) + 1e-300;
+        if (l + 1 < ma && be[j] < 1e-13 * scale) {
+          jb = j;
+          break;
+        }
+      }
+      if (jb < 0) break;
+      // invariant subspace at jb: continue from a random direction orthogonal to V
+      tm(jb - k0, jb - k0 + 1) = tm(jb - k0 + 1, jb - k0) = 0.0;
+      hipLaunchKernelGGL(k_hash_vec, dim3(grid_for(nd)), dim3(kBlock), 0, st, (double*)T.w, nd, rseed++);
+      CK(T.orth(jb + 1, T.w, -1));
+      hipLaunchKernelGGL(k_scale_into<VC>, dim3(g), dim3(kBlock), 0, st, T.w, T.col(T.Vb, jb + 1),
+                         T.beta + m, dim);
+      HIPCK(hipGetLastError());
+      j0 = jb + 1;
+      if (j0 >= m) break;
+    }
+    const double beta = be[m - 1];
+    jacobi_eigh(ma, Tm, theta, Z);
+    // ARPACK-style test: |beta_m * Z(m-1,i)| <= tol * max(eps^(2/3), |theta_i|)
+    const double eps23 = 3.6e-11;
+    conv = 0;
+    for (int i = 0; i < nev; i++)
+      if (fabs(beta * Z[(ma - 1) + (size_t)ma * i]) <= tol * std::max(eps23, fabs(theta[i]))) conv++;
+    if (conv == nev || it == maxit - 1 || m == dim) break;
+    // thick restart: keep nkeep Ritz vectors + the residual direction
+    const int nkeep = std::max(nev, std::min(ma - 2, nev + (ma - nev) / 2));
+    HIPCK(hipMemcpyAsync(T.Y, Z.data(), (size_t)ma * ma * sizeof(double), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_rotate<VC>, dim3(std::min(g, 2048)), dim3(kBlock), (size_t)ma * nkeep * sizeof(double),
+                       st, T.col(T.Vb, k0), ma, T.Y, ma, nkeep, T.Xb, dim);
+    HIPCK(hipMemcpyAsync(T.col(T.Vb, k0), T.Xb, (size_t)nkeep * dim * vs, hipMemcpyDeviceToDevice, st));
+    hipLaunchKernelGGL(k_scale_into<VC>, dim3(g), dim3(kBlock), 0, st, T.w, T.col(T.Vb, k0 + nkeep),
+                       T.beta + (m - 1), dim);
+    HIPCK(hipGetLastError());
+    std::fill(Tm.begin(), Tm.end(), 0.0);
+    for (int i = 0; i < nkeep; i++) {
+      tm(i, i) = theta[i];
+      tm(i, nkeep) = tm(nkeep, i) = beta * Z[(ma - 1) + (size_t)ma * i];
+    }
+    jstart = k0 + nkeep;
+  }
+  *conv_out = conv;
+  return ED_OK;
+}
+
+// sp_eigh replacement.  A single-vector Krylov method (ARPACK as much as this
+// one) sees one direction of each degenerate eigenspace — the other copies
+// only through rounding — so the lowest nev of a degenerate spectrum can come
+// back with copies missing (configs[3] with the flat bath: 77 of 169
+// sectors).  After the solve, the found vectors are locked and the lowest
+// eigenvalue of H on their orthogonal complement is computed from a fresh
+// random start (deflated solve); when it lies below the current nev-th value
+// it is a missed eigenvalue and replaces it; repeated until a deflated solve
+// finds nothing lower (ED_GPU_EIGH_NO_VERIFY=1 skips this, A/B).
 template <bool VC>
 static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, const void* v0,
                      double* evals, void* evecs, int32_t* nconv, int32_t* nhv) {
@@ -1462,11 +1701,14 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
   T.fused = !getenv("ED_GPU_TRLAN_UNFUSED");
   const int64_t dim = s->dim;
   const int m = (int)std::min<int64_t>(ncv, dim);
-  T.m = m;
   if (nev < 1 || nev >= m) return fail(ED_ERR_ARG, "need 1 <= nev < min(ncv, dim)");
+  const bool verify = !getenv("ED_GPU_EIGH_NO_VERIFY") && dim > (int64_t)nev + 2;
+  // deflated solves: nev locked columns + mp active ones
+  const int mp = (int)std::min<int64_t>(std::min(m, 20), dim - nev);
+  const int mcap = verify ? std::max(m, nev + mp) : m;
   const size_t vs = sizeof(V);
-  CK(T.alloc((void**)&T.Vb, (size_t)m * dim * vs));
-  CK(T.alloc((void**)&T.Xb, (size_t)m * dim * vs));
+  CK(T.alloc((void**)&T.Vb, (size_t)mcap * dim * vs));
+  CK(T.alloc((void**)&T.Xb, (size_t)mcap * dim * vs));
   CK(T.alloc((void**)&T.w, dim * vs));
   CK(T.alloc((void**)&T.h, 64 * sizeof(double2)));
   CK(T.alloc((void**)&T.coef, 64 * sizeof(double2)));
@@ -1474,84 +1716,52 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
   CK(T.alloc((void**)&T.npart, (size_t)T.G * sizeof(double)));
   CK(T.alloc((void**)&T.alpha, 72 * sizeof(double)));
   CK(T.alloc((void**)&T.beta, 72 * sizeof(double)));
-  CK(T.alloc((void**)&T.Y, (size_t)m * m * sizeof(double)));
+  CK(T.alloc((void**)&T.Y, (size_t)mcap * mcap * sizeof(double)));
   hipStream_t st = T.st;
   const int g = grid_for(dim);
-  const int64_t nd = dim * (VC ? 2 : 1);
-  // V_0 = v0 / |v0|
-  if (v0) HIPCK(hipMemcpyAsync(T.w, v0, dim * vs, hipMemcpyHostToDevice, st));
-  else hipLaunchKernelGGL(k_default_start, dim3(grid_for(nd)), dim3(kBlock), 0, st, (double*)T.w, nd);
-  CK(T.orth(0, T.w, -1));  // ncol 0: only the norm -> beta[m]
-  double b0 = 0.0;
-  HIPCK(hipMemcpyAsync(&b0, T.beta + m, sizeof(double), hipMemcpyDeviceToHost, st));
-  HIPCK(hipStreamSynchronize(st));
-  if (!(b0 > 0.0)) return fail(ED_ERR_ARG, "zero start vector");
-  hipLaunchKernelGGL(k_scale_into<VC>, dim3(g), dim3(kBlock), 0, st, T.w, T.Vb, T.beta + m, dim);
-
-  std::vector<double> Tm((size_t)m * m, 0.0), theta, Z, al(m), be(m);
-  auto tm = [&](int i, int j) -> double& { return Tm[i + (size_t)m * j]; };
-  int jstart = 0, conv = 0;
-  uint64_t seed = 1;
-  for (int it = 0; it < maxit; it++) {
-    int j0 = jstart;
-    for (;;) {  // expansion j0..m-1, restarted past an invariant subspace
-      CK(T.sweep(j0));
-      HIPCK(hipMemcpyAsync(al.data(), T.alpha, m * sizeof(double), hipMemcpyDeviceToHost, st));
-      HIPCK(hipMemcpyAsync(be.data(), T.beta, m * sizeof(double), hipMemcpyDeviceToHost, st));
-      HIPCK(hipStreamSynchronize(st));
-      int jb = -1;
-      for (int j = j0; j < m; j++) {
-        tm(j, j) = al[j];
-        if (j + 1 < m) tm(j, j + 1) = tm(j + 1, j) = be[j];
-        const double scale = fabs(al[j]) + (j > 0 ? fabs(tm(j - 1, j)) : 0.0) + 1e-300;
-        if (j + 1 < m && be[j] < 1e-13 * scale) {
-          jb = j;
-          break;
-        }
-      }
-      if (jb < 0) break;
-      // invariant subspace at jb: continue from a random direction orthogonal to V
-      tm(jb, jb + 1) = tm(jb + 1, jb) = 0.0;
-      hipLaunchKernelGGL(k_hash_vec, dim3(grid_for(nd)), dim3(kBlock), 0, st, (double*)T.w, nd, seed++);
-      CK(T.orth(jb + 1, T.w, -1));
-      hipLaunchKernelGGL(k_scale_into<VC>, dim3(g), dim3(kBlock), 0, st, T.w, T.col(T.Vb, jb + 1),
-                         T.beta + m, dim);
+  T.m = m;
+  std::vector<double> theta, Z;
+  int conv = 0;
+  CK(trlan_core(T, 0, nev, maxit, tol, v0, 0, theta, Z, &conv));
+  // Ritz vectors -> Xb[0, nev)
+  HIPCK(hipMemcpyAsync(T.Y, Z.data(), (size_t)m * m * sizeof(double), hipMemcpyHostToDevice, st));
+  hipLaunchKernelGGL(k_rotate<VC>, dim3(std::min(g, 2048)), dim3(kBlock), (size_t)m * nev * sizeof(double), st,
+                     T.Vb, m, T.Y, m, nev, T.Xb, dim);
+  HIPCK(hipGetLastError());
+  std::vector<double> ev(theta.begin(), theta.begin() + nev);
+  // the result vectors live in Vb[0, nev) from here on (locked columns of the
+  // deflated solves, which use Xb as scratch)
+  HIPCK(hipMemcpyAsync(T.Vb, T.Xb, (size_t)nev * dim * vs, hipMemcpyDeviceToDevice, st));
+  if (verify && conv == nev) {
+    for (int round = 0; round < nev; round++) {
+      // solve for the lowest eigenvalue on the complement of the nev vectors
+      for (auto& gr : T.graphs) (void)hipGraphExecDestroy(gr.second);
+      T.graphs.clear();  // captured sweeps depend on m
+      T.m = nev + mp;
+      std::vector<double> th2, Z2;
+      int c2 = 0;
+      CK(trlan_core(T, nev, 1, maxit, tol, nullptr, 1000 + round, th2, Z2, &c2));
+      const double mu = th2[0];
+      if (!(c2 == 1 && mu < ev[nev - 1] - 1e-9 * std::max(1.0, fabs(ev[nev - 1])))) break;
+      // a missed eigenvalue: its Ritz vector -> Xb[nev], then insert in order
+      // (drop the current largest)
+      const int ma2 = T.m - nev;
+      HIPCK(hipMemcpyAsync(T.Y, Z2.data(), (size_t)ma2 * sizeof(double), hipMemcpyHostToDevice, st));
+      hipLaunchKernelGGL(k_rotate<VC>, dim3(std::min(g, 2048)), dim3(kBlock), (size_t)ma2 * sizeof(double), st,
+                         T.col(T.Vb, nev), ma2, T.Y, ma2, 1, T.w, dim);
       HIPCK(hipGetLastError());
-      j0 = jb + 1;
-      if (j0 >= m) break;
+      int pos = nev - 1;
+      while (pos > 0 && ev[pos - 1] > mu) pos--;
+      for (int i = nev - 1; i > pos; i--) {
+        ev[i] = ev[i - 1];
+        HIPCK(hipMemcpyAsync(T.col(T.Vb, i), T.col(T.Vb, i - 1), dim * vs, hipMemcpyDeviceToDevice, st));
+      }
+      ev[pos] = mu;
+      HIPCK(hipMemcpyAsync(T.col(T.Vb, pos), T.w, dim * vs, hipMemcpyDeviceToDevice, st));
     }
-    const double beta = be[m - 1];
-    jacobi_eigh(m, Tm, theta, Z);
-    // ARPACK-style test: |beta_m * Z(m-1,i)| <= tol * max(eps^(2/3), |theta_i|)
-    const double eps23 = 3.6e-11;
-    conv = 0;
-    for (int i = 0; i < nev; i++)
-      if (fabs(beta * Z[(m - 1) + (size_t)m * i]) <= tol * std::max(eps23, fabs(theta[i]))) conv++;
-    if (conv == nev || it == maxit - 1 || m == dim) break;
-    // thick restart: keep nkeep Ritz vectors + the residual direction
-    const int nkeep = std::max(nev, std::min(m - 2, nev + (m - nev) / 2));
-    HIPCK(hipMemcpyAsync(T.Y, Z.data(), (size_t)m * m * sizeof(double), hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(k_rotate<VC>, dim3(std::min(g, 2048)), dim3(kBlock), (size_t)m * nkeep * sizeof(double),
-                       st, T.Vb, m, T.Y, m, nkeep, T.Xb, dim);
-    HIPCK(hipMemcpyAsync(T.Vb, T.Xb, (size_t)nkeep * dim * vs, hipMemcpyDeviceToDevice, st));
-    hipLaunchKernelGGL(k_scale_into<VC>, dim3(g), dim3(kBlock), 0, st, T.w, T.col(T.Vb, nkeep),
-                       T.beta + (m - 1), dim);
-    HIPCK(hipGetLastError());
-    std::fill(Tm.begin(), Tm.end(), 0.0);
-    for (int i = 0; i < nkeep; i++) {
-      tm(i, i) = theta[i];
-      tm(i, nkeep) = tm(nkeep, i) = beta * Z[(m - 1) + (size_t)m * i];
-    }
-    jstart = nkeep;
   }
-  for (int i = 0; i < nev; i++) evals[i] = theta[i];
-  if (evecs) {
-    HIPCK(hipMemcpyAsync(T.Y, Z.data(), (size_t)m * m * sizeof(double), hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(k_rotate<VC>, dim3(std::min(g, 2048)), dim3(kBlock), (size_t)m * nev * sizeof(double),
-                       st, T.Vb, m, T.Y, m, nev, T.Xb, dim);
-    HIPCK(hipGetLastError());
-    HIPCK(hipMemcpyAsync(evecs, T.Xb, (size_t)nev * dim * vs, hipMemcpyDeviceToHost, st));
-  }
+  for (int i = 0; i < nev; i++) evals[i] = ev[i];
+  if (evecs) HIPCK(hipMemcpyAsync(evecs, T.Vb, (size_t)nev * dim * vs, hipMemcpyDeviceToHost, st));
   HIPCK(hipStreamSynchronize(st));
   if (nconv) *nconv = conv;
   if (nhv) *nhv = T.nhv;
