@@ -315,7 +315,16 @@ struct EpiStore {
   __device__ __forceinline__ bool skip() const { return false; }
   __device__ __forceinline__ void prepare() {}
   __device__ __forceinline__ double row(int64_t i, V acc, V) {
+#ifdef ED_EPI_NT_STORE
+    if constexpr (VC) {
+      __builtin_nontemporal_store(acc.x, (double*)(hv + i));
+      __builtin_nontemporal_store(acc.y, (double*)(hv + i) + 1);
+    } else {
+      __builtin_nontemporal_store(acc, hv + i);
+    }
+#else
     hv[i] = acc;
+#endif
     return 0.0;
   }
   __device__ __forceinline__ void finish(double) {}
@@ -829,7 +838,7 @@ __global__ void __launch_bounds__(kKronUpBlock) k_kron_up(KronArgs<HC> K, const 
     for (int j = 0; j < CPT; j++) {
       const int iu = t + kKronUpBlock * j;
       const int64_t iw = base + r * G;
-      xr[r][j] = (iw < dd && iu < du) ? x[iw * du + iu] : vzero<V>();
+      xr[r][j] = (iw < dd && iu < du) ? x[(int)iw * du + iu] : vzero<V>();
     }
   int pb = 0;
   for (; base < dd; base += kKronUpRows * G) {
@@ -838,7 +847,13 @@ __global__ void __launch_bounds__(kKronUpBlock) k_kron_up(KronArgs<HC> K, const 
     for (int r = 0; r < kKronUpRows; r++)
 #pragma unroll
       for (int j = 0; j < CPT; j++) xc[r][j] = xr[r][j];
+#ifdef ED_KRON_UP_ONESET
+    // one LDS set (half the LDS: two workgroups per CU), two barriers per step
+    V* buf = bufs;
+    if (base != (int64_t)blockIdx.x) __syncthreads();  // the previous step's reads are done
+#else
     V* buf = bufs + (size_t)pb * kKronUpRows * dup;
+#endif
 #pragma unroll
     for (int j = 0; j < CPT; j++) {
       const int iu = t + kKronUpBlock * j;
@@ -855,7 +870,7 @@ __global__ void __launch_bounds__(kKronUpBlock) k_kron_up(KronArgs<HC> K, const 
       for (int j = 0; j < CPT; j++) {
         const int iu = t + kKronUpBlock * j;
         const int64_t iw = nb + r * G;
-        xr[r][j] = (iw < dd && iu < du) ? x[iw * du + iu] : vzero<V>();
+        xr[r][j] = (iw < dd && iu < du) ? x[(int)iw * du + iu] : vzero<V>();
       }
     H ad[kKronUpRows];
     int imd[kKronUpRows];
@@ -889,16 +904,20 @@ __global__ void __launch_bounds__(kKronUpBlock) k_kron_up(KronArgs<HC> K, const 
               acc[0] = add(acc[0], mul(h, buf[col]));
             }
           }
-        y[base * du + iu] = acc[0];
-        if (second) y[(base + G) * du + iu] = acc[kKronUpRows - 1];
+        y[(int)base * du + iu] = acc[0];
+        if (second) y[(int)(base + G) * du + iu] = acc[kKronUpRows - 1];
       }
     }
     pb ^= 1;
   }
 }
 
+// dwo[iw*DEG + k] = element offset iw'*dimup of the k-th down-hop target row,
+// dwi[iw*DEG + k] = its value's dictionary index (DEG slots per row, padded):
+// one wave-uniform row is one s_load_dwordx8/x16 + one of the index bytes
 template <bool HC, bool VC, int DEG, class Epi>
-__global__ void __launch_bounds__(kBlock) k_kron_dw(KronArgs<HC> K, const uint32_t* __restrict__ dww,
+__global__ void __launch_bounds__(kBlock) k_kron_dw(KronArgs<HC> K, const uint32_t* __restrict__ dwo,
+                                                    const uint8_t* __restrict__ dwi,
                                                     const val_t<HC>* __restrict__ dwdict, int ndict,
                                                     const val_t<VC>* __restrict__ x, const val_t<VC>* ypart,
                                                     Epi epi) {
@@ -909,42 +928,53 @@ __global__ void __launch_bounds__(kBlock) k_kron_dw(KronArgs<HC> K, const uint32
   __shared__ H sdict[kKronDictMax];
   for (int q = threadIdx.x; q < ndict; q += kBlock) sdict[q] = dwdict[q];
   __syncthreads();
+  // 32-bit index arithmetic throughout (dim < 2^31, checked on the host): the
+  // tile walk is scalar code, and 64-bit divisions there made the kernel
+  // SALU-bound (29 M scalar instructions per launch at N28)
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t du = K.dimup, dd = K.dimdw;
+  const int du = (int)K.dimup, dd = (int)K.dimdw;
   const int degdw = K.degdw;
-  const int nchunk = (int)((du + 63) >> 6);
+  const int nchunk = (du + 63) >> 6;
   constexpr int R = kKronRowsPerWave;
   constexpr int kTileRows = (kBlock / 64) * R;
-  const int64_t nrb = (dd + kTileRows - 1) / kTileRows;
+  const int nrb = (dd + kTileRows - 1) / kTileRows;
   // blocks are dealt round-robin to the 8 XCDs: XCD x = blockIdx % 8 takes
   // chunks x, x+8, ...; its blocks walk (chunk, row block) tiles in order
   const int xcd = blockIdx.x & 7;
-  const int64_t jb = blockIdx.x >> 3, g8 = gridDim.x >> 3;
+  const int g8 = gridDim.x >> 3;
   const int mine = nchunk > xcd ? (nchunk - xcd + 7) / 8 : 0;
+  int m = 0, rb = blockIdx.x >> 3;
+  while (rb >= nrb) {
+    rb -= nrb;
+    m++;
+  }
   double part = 0.0;
-  for (int64_t u = jb; u < (int64_t)mine * nrb; u += g8) {
-    const int c = xcd + 8 * (int)(u / nrb);
-    const int64_t rb = u - (u / nrb) * nrb;
-    const int64_t iu = (int64_t)c * 64 + lane;
+  for (; m < mine;) {
+    const int iu = (xcd + 8 * m) * 64 + lane;
     const bool ok = iu < du;
-    const int64_t r0 = rb * kTileRows + wv * R;  // wave-uniform
+    const int r0 = rb * kTileRows + wv * R;  // wave-uniform
     // every load of the wave's R rows in flight before any use
-    uint32_t wd[R][DEG];
+    uint32_t wo[R][DEG];
+    uint8_t wi[R][DEG];
 #pragma unroll
-    for (int r = 0; r < R; r++)
+    for (int r = 0; r < R; r++) {
+      const int rr = r0 + r < dd ? r0 + r : r0;
 #pragma unroll
-      for (int k = 0; k < DEG; k++) wd[r][k] = (r0 + r < dd && k < degdw) ? dww[(int64_t)k * dd + r0 + r] : 0u;
+      for (int k = 0; k < DEG; k++) {
+        wo[r][k] = dwo[rr * DEG + k];
+        wi[r][k] = dwi[rr * DEG + k];
+      }
+    }
     V g[R][DEG], yv[R], xv[R];
 #pragma unroll
     for (int r = 0; r < R; r++) {
-      const int64_t i = (r0 + r) * du + iu;
+      const int i = (r0 + r) * du + iu;
       const bool on = ok && r0 + r < dd;
 #pragma unroll
-      for (int k = 0; k < DEG; k++)
-        g[r][k] = (on && k < degdw) ? x[(int64_t)(wd[r][k] & 0xffffu) * du + iu] : vzero<V>();
+      for (int k = 0; k < DEG; k++) g[r][k] = (on && k < degdw) ? x[(int)wo[r][k] + iu] : vzero<V>();
       xv[r] = on ? x[i] : vzero<V>();
-      yv[r] = on ? ldh<1>(ypart + i) : vzero<V>();  // streamed once: keep the L2 for the V chunk
+      yv[r] = on ? ypart[i] : vzero<V>();
     }
 #pragma unroll
     for (int r = 0; r < R; r++) {
@@ -952,8 +982,13 @@ __global__ void __launch_bounds__(kBlock) k_kron_dw(KronArgs<HC> K, const uint32
       V acc = yv[r];
 #pragma unroll
       for (int k = 0; k < DEG; k++)
-        if (k < degdw) acc = add(acc, mul(sdict[wd[r][k] >> 16], g[r][k]));
-      part += epi.row((r0 + r) * du + iu, acc, xv[r]);
+        if (k < degdw) acc = add(acc, mul(sdict[wi[r][k]], g[r][k]));
+      part += epi.row((int64_t)((r0 + r) * du + iu), acc, xv[r]);
+    }
+    rb += g8;
+    while (rb >= nrb) {
+      rb -= nrb;
+      m++;
     }
   }
   epi.finish(part);

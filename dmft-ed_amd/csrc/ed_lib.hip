@@ -63,7 +63,8 @@ struct KronHost {
   // two-pass form (k_kron_up + k_kron_dw): up-hop words {col:16 | value index:8}
   bool two = false;
   int cpt = 0, degU = 0, degD = 0;  // template values: columns per thread, slot bounds
-  uint32_t *upw = nullptr, *dww = nullptr;
+  uint32_t *upw = nullptr, *dwo = nullptr;
+  uint8_t* dwi = nullptr;
   void *updict = nullptr, *dwdict = nullptr;
   int nupdict = 0, ndwdict = 0;
 };
@@ -177,6 +178,36 @@ static int upload(ed_sector* s, T** p, const std::vector<T>& h) {
   return dcopy(s, *p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice);
 }
 
+// Pinned host staging (Lanczos alpha|beta copies) from a process-wide pool
+// that only grows: hipHostFree / hipHostMalloc synchronise the device, which
+// would stall every other worker thread's stream (and break their graph
+// captures) each time a sector is closed or resized.
+static std::mutex g_pin_mu;
+static std::multimap<size_t, void*> g_pin_free;  // free blocks by size
+static std::map<void*, size_t> g_pin_size;       // every block ever allocated
+static void* pinned_get(size_t n) {
+  {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    auto it = g_pin_free.lower_bound(n);
+    if (it != g_pin_free.end()) {
+      void* p = it->second;
+      g_pin_free.erase(it);
+      return p;
+    }
+  }
+  n = std::max<size_t>(n, 4096);
+  void* p = nullptr;
+  if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  g_pin_size[p] = n;
+  return p;
+}
+static void pinned_put(void* p) {
+  if (!p) return;
+  std::lock_guard<std::mutex> lk(g_pin_mu);
+  g_pin_free.emplace(g_pin_size[p], p);
+}
+
 static void sector_free(ed_sector* s) {
   if (!s) return;
   (void)hipSetDevice(s->device);
@@ -188,7 +219,7 @@ static void sector_free(ed_sector* s) {
     (void)hipStreamSynchronize(s->stream);
     (void)hipStreamDestroy(s->stream);
   }
-  if (s->ws.h_ab) (void)hipHostFree(s->ws.h_ab);
+  pinned_put(s->ws.h_ab);  // after the stream sync above: no copy into it is in flight
   delete s;
 }
 
@@ -362,7 +393,7 @@ static int build_kron_words(ed_sector* s, int sp, const std::vector<int32_t>& co
     const char* env = getenv("ED_GPU_KRON2");
     if (env && env[0] == '0') return ED_OK;
     if (s->dim < kKron2MinDim && !(env && env[0] == '1')) return ED_OK;
-    if (nr > 8192 || deg > 16) return ED_OK;
+    if (nr > 8192 || deg > 16 || s->dim >= ((int64_t)1 << 31)) return ED_OK;  // 32-bit element offsets
     int cpt = 1;
     while (cpt * kKronUpBlock < nr) cpt *= 2;
     K.cpt = cpt;
@@ -398,9 +429,23 @@ static int build_kron_words(ed_sector* s, int sp, const std::vector<int32_t>& co
     }
     words[q] = (uint32_t)cols[q] | (id << 16);
   }
-  uint32_t*& wp = sp == 0 ? K.upw : K.dww;
   void*& dp = sp == 0 ? K.updict : K.dwdict;
-  CK(upload(s, &wp, words));
+  if (sp == 0) {
+    CK(upload(s, &K.upw, words));
+  } else {
+    // pass D layout: [row][DEG slot] target offsets (row * dimup) and indices
+    const int64_t du = K.dimup;
+    std::vector<uint32_t> off((size_t)nr * K.degD, 0u);
+    std::vector<uint8_t> ix((size_t)nr * K.degD, 0);
+    for (int64_t r = 0; r < nr; r++)
+      for (int k = 0; k < deg; k++) {
+        const uint32_t wd = words[(size_t)k * nr + r];
+        off[(size_t)r * K.degD + k] = (uint32_t)((wd & 0xffffu) * du);
+        ix[(size_t)r * K.degD + k] = (uint8_t)(wd >> 16);
+      }
+    CK(upload(s, &K.dwo, off));
+    CK(upload(s, &K.dwi, ix));
+  }
   CK(dalloc(s, &dp, dict.size() * 8));
   CK(dcopy(s, dp, dict.data(), dict.size() * 8, hipMemcpyHostToDevice));
   (sp == 0 ? K.nupdict : K.ndwdict) = (int)(dict.size() / hw);
@@ -529,10 +574,18 @@ static bool xcd_on(const ed_sector* s, int path) {
 }
 // pass D of the two-pass Kronecker H·v: a multiple of 8 blocks (XCD column
 // chunks), 8 resident per CU
-static constexpr int kKronDwGrid = 2048;
+#ifndef ED_KRON_DW_GRID
+#define ED_KRON_DW_GRID 2048
+#endif
+static constexpr int kKronDwGrid = ED_KRON_DW_GRID;
 // pass U LDS: dictionary + two sets of `rows` staged rows
+#ifdef ED_KRON_UP_ONESET
+static constexpr int kKronUpSets = 1;
+#else
+static constexpr int kKronUpSets = 2;
+#endif
 static size_t kron_up_lds(bool hc, bool vc, int64_t du, int rows) {
-  return kKronDictMax * (hc ? 16 : 8) + 2 * rows * (size_t)((du + 1) & ~1) * (vc ? 16 : 8);
+  return kKronDictMax * (hc ? 16 : 8) + kKronUpSets * rows * (size_t)((du + 1) & ~1) * (vc ? 16 : 8);
 }
 static int kron_up_rows(bool hc, bool vc, int64_t du) { return kron_up_lds(hc, vc, du, 2) <= 160 * 1024 ? 2 : 1; }
 static bool kron2_on(const ed_sector* s, int path, int vc) {
@@ -599,10 +652,10 @@ static int launch_kron2(ed_sector* s, const void* x, Epi epi, hipStream_t st) {
   using H = val_t<HC>;
   if (K.degD == 8)
     hipLaunchKernelGGL((k_kron_dw<HC, VC, 8, Epi>), dim3(kKronDwGrid), dim3(kBlock), 0, st, kron_args<HC>(s),
-                       K.dww, (const H*)K.dwdict, K.ndwdict, (const V*)x, (const V*)y, epi);
+                       K.dwo, K.dwi, (const H*)K.dwdict, K.ndwdict, (const V*)x, (const V*)y, epi);
   else
     hipLaunchKernelGGL((k_kron_dw<HC, VC, 16, Epi>), dim3(kKronDwGrid), dim3(kBlock), 0, st, kron_args<HC>(s),
-                       K.dww, (const H*)K.dwdict, K.ndwdict, (const V*)x, (const V*)y, epi);
+                       K.dwo, K.dwi, (const H*)K.dwdict, K.ndwdict, (const V*)x, (const V*)y, epi);
   HIPCK(hipGetLastError());
   return ED_OK;
 }
@@ -711,10 +764,11 @@ sized:
     w.z = blk + 2 * ((size_t)cap + 2);
     if (w.h_ab) {
       HIPCK(hipStreamSynchronize(s->stream));  // no copy into the old staging in flight
-      HIPCK(hipHostFree(w.h_ab));
+      pinned_put(w.h_ab);
       w.h_ab = nullptr;
     }
-    HIPCK(hipHostMalloc((void**)&w.h_ab, 2 * ((size_t)cap + 2) * sizeof(double), hipHostMallocDefault));
+    w.h_ab = (double*)pinned_get(2 * ((size_t)cap + 2) * sizeof(double));
+    if (!w.h_ab) return fail(ED_ERR_OOM, "pinned host staging");
     w.cap = cap;
   }
   if (want_basis && basis_cols > w.basis_cols) {
@@ -1868,7 +1922,7 @@ static int sector_create(const ed_params* p, int32_t q1, int32_t q2, int32_t fla
     row0 = 0;
     nrows = s->dim;
   }
-  if (row0 < 0 || nrows < 1 || row0 + nrows > s->dim) {
+  if (row0 < 0 || nrows < 0 || row0 + nrows > s->dim) {  // nrows == 0: a rank with no rows (dim < MpiSize)
     delete s;
     return fail(ED_ERR_ARG, "row range outside the sector");
   }
@@ -1914,7 +1968,7 @@ static int sector_create(const ed_params* p, int32_t q1, int32_t q2, int32_t fla
   }
   // Kronecker form: normal mode without Jx/Jp terms (no term moves both spins)
   s->kron = (flags & ED_DIRECT) && s->Mh.mode == ED_MODE_NORMAL && !s->Mh.jhflag && nrows == s->dim;
-  if (flags & ED_STORED) TRY(build_stored(s));
+  if ((flags & ED_STORED) && nrows > 0) TRY(build_stored(s));
   if (s->kron) TRY(build_kron(s));
   if (hipStreamSynchronize(s->stream) != hipSuccess) {
     sector_free(s);
@@ -1966,6 +2020,7 @@ int ed_sector_get_info(const ed_sector* s, ed_sector_info* info) {
 
 int ed_sector_hxv_dev_path(ed_sector* s, int32_t path, int32_t vtype, const void* v, void* hv,
                            void* stream) {
+  if (s && s->nrows == 0) return ED_OK;  // no local rows: nothing to write
   if (!s || !v || !hv) return fail(ED_ERR_ARG, "null");
   int pth = resolve_path(s, path);
   if (pth < 0) return fail(ED_ERR_ARG, "H·v path not available for this sector");
@@ -2025,6 +2080,8 @@ int ed_sector_dump_csr(const ed_sector* s, int64_t* rowptr, int32_t* cols, doubl
   if (!(s->flags & ED_STORED)) return fail(ED_ERR_STATE, "sector was built without ED_STORED");
   HIPCK(hipSetDevice(s->device));
   const int64_t dim = s->nrows, ns = s->nslice, slots = s->padded;  // local rows, global columns
+  rowptr[0] = 0;
+  if (dim == 0) return ED_OK;
   const int hw = s->hc ? 2 : 1;
   std::vector<uint16_t> cnt(dim);
   std::vector<int64_t> sptr(ns + 1);
@@ -2531,10 +2588,47 @@ int ed_gpu_build_sector(int32_t q1, int32_t q2, int32_t flags, int64_t* dim) {
 
 int ed_gpu_vecdim(int32_t* vecdim) {
   if (!g_cur || !vecdim) return fail(ED_ERR_STATE, "no current sector");
-  *vecdim = (int32_t)g_cur->dim;  // serial: MpiQ=Dim, MpiR=0 (ED_HAMILTONIAN.f90:141-143)
+  *vecdim = (int32_t)g_cur->nrows;  // MpiQ + MpiR (ED_HAMILTONIAN.f90:126-149); serial: Dim
   return ED_OK;
 }
 
+int ed_gpu_mpi_split(int64_t dim, int32_t rank, int32_t size, int64_t* row0, int64_t* nrows) {
+  if (!row0 || !nrows || size < 1 || rank < 0 || rank >= size || dim < 0) return fail(ED_ERR_ARG, "mpi_split args");
+  const int64_t q = dim / size;                          // MpiQ
+  const int64_t r = rank == size - 1 ? dim % size : 0;   // MpiR (last rank)
+  *row0 = (int64_t)rank * q;                             // MpiIshift
+  *nrows = q + r;                                        // MpiIend - MpiIstart + 1
+  return ED_OK;
+}
+int ed_gpu_build_sector_rows(int32_t q1, int32_t q2, int32_t flags, int64_t row0, int64_t nrows, int64_t* dim) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_have_params) return fail(ED_ERR_STATE, "ed_gpu_init not called");
+  if (g_cur) {
+    sector_free(g_cur);
+    g_cur = nullptr;
+  }
+  CK(ed_sector_create_rows(&g_params, q1, q2, flags, row0, nrows, g_device, nullptr, &g_cur));
+  if (dim) *dim = g_cur->dim;
+  return ED_OK;
+}
+int ed_gpu_hxv_mpi(const int32_t* nloc, const double* vin, double* hv) {
+  if (!g_cur) return fail(ED_ERR_STATE, "ed_gpu_hxv_mpi ERROR: Hsector NOT set");
+  if (!nloc) return fail(ED_ERR_ARG, "null");
+  ed_sector* s = g_cur;
+  if ((int64_t)*nloc != s->nrows) return fail(ED_ERR_ARG, "ed_gpu_hxv_mpi ERROR: Nloc != local rows of the sector");
+  if (s->nrows == 0) return ED_OK;
+  if (!vin || !hv) return fail(ED_ERR_ARG, "null");
+  HIPCK(hipSetDevice(s->device));
+  if (!s->d_x) {
+    CK(dalloc(s, &s->d_x, s->dim * 16));
+    CK(dalloc(s, &s->d_y, s->nrows * 16));
+  }
+  HIPCK(hipMemcpyAsync(s->d_x, vin, s->dim * 16, hipMemcpyHostToDevice, s->stream));
+  CK(ed_sector_hxv_dev(s, 1, s->d_x, s->d_y, s->stream));
+  HIPCK(hipMemcpyAsync(hv, s->d_y, s->nrows * 16, hipMemcpyDeviceToHost, s->stream));
+  HIPCK(hipStreamSynchronize(s->stream));
+  return ED_OK;
+}
 int ed_gpu_hxv(const int32_t* nloc, const double* v, double* hv) {
   if (!g_cur) return fail(ED_ERR_STATE, "ed_gpu_hxv ERROR: Hsector NOT set");
   if (!nloc) return fail(ED_ERR_ARG, "null nloc");

@@ -51,6 +51,9 @@ SIGNATURES = {
     "ed_gpu_build_sector": ([_i32, _i32, _i32, _P], ctypes.c_int),
     "ed_gpu_vecdim": ([_P], ctypes.c_int),
     "ed_gpu_hxv": ([_P, _P, _P], ctypes.c_int),
+    "ed_gpu_build_sector_rows": ([_i32, _i32, _i32, _i64, _i64, _P], ctypes.c_int),
+    "ed_gpu_mpi_split": ([_i64, _i32, _i32, _P, _P], ctypes.c_int),
+    "ed_gpu_hxv_mpi": ([_P, _P, _P], ctypes.c_int),
     "ed_gpu_dump_csr": ([_P, _P, _P], ctypes.c_int),
     "ed_gpu_lanc_eigh": ([_i32, _f64, _i32, _P, _P, _P], ctypes.c_int),
     "ed_gpu_lanc_tridiag": ([_P, _i32, _f64, _P, _P, _P], ctypes.c_int),

@@ -118,11 +118,52 @@ program ed_gpu_driver
   write(*,"(A,F20.12,A,F20.12,A,I0,A,ES10.3)") "EIG1=", eval6(1), " EIG6=", eval6(6), " NCONV=", nconv, &
        " EIGRES=", sqrt(sum(abs(hv - eval6(1)*evec6(:,1))**2))
 
+  ! --- MpiStatus=T row split (ED_HAMILTONIAN.f90:55-62 + spMatVec_mpi_cc):
+  !     emulate P ranks one after the other, each holding its rows and
+  !     applying them to the gathered vector; the assembled product must equal
+  !     the serial one bit for bit (same per-row element order)
+  call gpuMatVec_cc(vecdim, vin, hv)
+  call mpi_rows_check(3, hv)
+  call mpi_rows_check(int(dim8) + 2, hv)   ! more ranks than rows: empty ranks
+
   call ed_gpu_check(ed_gpu_delete_sector(), "delete_Hv_sector")
   call ed_gpu_check(ed_gpu_finalize(), "finalize")
   write(*,"(A)") "DRIVER_OK"
 
 contains
+
+  subroutine mpi_rows_check(nproc, hv_serial)
+    integer, intent(in) :: nproc
+    complex(8), intent(in) :: hv_serial(:)
+    integer(c_int64_t) :: r0, nr, d8
+    integer :: rank, nzero, vd
+    integer(c_int32_t) :: vdim
+    complex(8), allocatable :: hloc(:), hall(:)
+    allocate(hall(size(hv_serial)))
+    hall = (0d0, 0d0)
+    nzero = 0
+    do rank = 0, nproc-1
+       call ed_gpu_check(ed_gpu_mpi_split(dim8, int(rank, c_int32_t), int(nproc, c_int32_t), r0, nr), "mpi_split")
+       call ed_gpu_check(ed_gpu_build_sector_rows(int(nup,c_int32_t), int(ndw,c_int32_t), flags_mpi(), r0, nr, d8), &
+            "build_Hv_sector(MPI)")
+       call ed_gpu_check(ed_gpu_vecdim(vdim), "vecDim_Hv_sector(MPI)")
+       vd = int(vdim)
+       if (vd /= int(nr)) stop "vecDim mismatch"
+       if (vd == 0) nzero = nzero + 1
+       allocate(hloc(max(vd,1)))
+       ! the Allgatherv result is the whole vector vin
+       call ed_gpu_check(ed_gpu_hxv_mpi(vdim, vin, hloc), "spMatVec_mpi_cc")
+       if (vd > 0) hall(int(r0)+1:int(r0)+vd) = hloc(1:vd)
+       deallocate(hloc)
+    enddo
+    write(*,"(A,I0,A,I0,A,L1,A,ES10.3)") "MPI_RANKS=", nproc, " EMPTY_RANKS=", nzero, " MPI_EQUAL=", &
+         all(hall == hv_serial), " MPI_RELDEV=", maxval(abs(hall - hv_serial)) / maxval(abs(hv_serial))
+  end subroutine mpi_rows_check
+
+  integer(c_int32_t) function flags_mpi()
+    flags_mpi = ED_STORED
+    if (direct) flags_mpi = ED_DIRECT
+  end function flags_mpi
 
   subroutine host_lanczos(n, v0, nmax, a, b, nl)
     integer, intent(in) :: n, nmax

@@ -13,8 +13,14 @@
 !-----------------------------------------------------------------------
 module ED_GPU_HXV
   use iso_c_binding
+#ifdef _MPI
+  use mpi
+#endif
   implicit none
   private
+
+  ! communicator of the MPI H·v (the reference's MpiComm, ED_VARS_GLOBAL.f90:228-231)
+  integer, public :: ed_gpu_comm = 0
 
   integer, parameter, public :: ED_MAX_NORB = 3, ED_MAX_NSPIN = 2, ED_MAX_NBATH = 32
   integer, parameter, public :: ED_STORED = 1, ED_DIRECT = 2, ED_REAL = 4
@@ -62,6 +68,27 @@ module ED_GPU_HXV
        complex(c_double_complex), intent(in) :: v(*)
        complex(c_double_complex), intent(out) :: hv(*)
      end function ed_gpu_hxv
+     ! MpiStatus=T: rows [row0, row0+nrows) of the sector on this rank
+     integer(c_int) function ed_gpu_build_sector_rows(q1, q2, flags, row0, nrows, dim) &
+          bind(C, name="ed_gpu_build_sector_rows")
+       import :: c_int, c_int32_t, c_int64_t
+       integer(c_int32_t), value :: q1, q2, flags
+       integer(c_int64_t), value :: row0, nrows
+       integer(c_int64_t), intent(out) :: dim
+     end function ed_gpu_build_sector_rows
+     integer(c_int) function ed_gpu_mpi_split(dim, rank, size, row0, nrows) bind(C, name="ed_gpu_mpi_split")
+       import :: c_int, c_int32_t, c_int64_t
+       integer(c_int64_t), value :: dim
+       integer(c_int32_t), value :: rank, size
+       integer(c_int64_t), intent(out) :: row0, nrows
+     end function ed_gpu_mpi_split
+     ! spMatVec_mpi_cc after the Allgatherv: vin(dim) -> Hv(nloc)
+     integer(c_int) function ed_gpu_hxv_mpi(nloc, vin, hv) bind(C, name="ed_gpu_hxv_mpi")
+       import :: c_int, c_int32_t, c_double_complex
+       integer(c_int32_t), intent(in) :: nloc
+       complex(c_double_complex), intent(in) :: vin(*)
+       complex(c_double_complex), intent(out) :: hv(*)
+     end function ed_gpu_hxv_mpi
      integer(c_int) function ed_gpu_lanc_eigh(nitermax, threshold, ncheck, egs, vect, nlanc) &
           bind(C, name="ed_gpu_lanc_eigh")
        import :: c_int, c_int32_t, c_double, c_double_complex
@@ -108,7 +135,8 @@ module ED_GPU_HXV
 
   public :: ed_gpu_init, ed_gpu_set_device, ed_gpu_build_sector, ed_gpu_vecdim, ed_gpu_hxv
   public :: ed_gpu_lanc_eigh, ed_gpu_lanc_tridiag, ed_gpu_eigh, ed_gpu_delete_sector, ed_gpu_finalize
-  public :: gpuMatVec_cc
+  public :: ed_gpu_build_sector_rows, ed_gpu_mpi_split, ed_gpu_hxv_mpi
+  public :: gpuMatVec_cc, gpuMatVec_mpi_cc
   public :: ed_gpu_check
   public :: ed_gpu_pack_params
 
@@ -123,6 +151,40 @@ contains
     n = int(Nloc, c_int32_t)
     call ed_gpu_check(ed_gpu_hxv(n, v, Hv), "gpuMatVec_cc")
   end subroutine gpuMatVec_cc
+
+  !> Same interface and contract as spMatVec_mpi_cc (STORED_HxV.f90:147-197):
+  !> v and Hv are this rank's Nloc rows; the whole vector is gathered with
+  !> MPI_Allgatherv (counts N/P, the last rank N/P + mod(N,P), as the
+  !> reference), then the GPU applies the rank's rows of H.  A serial build
+  !> (no -D_MPI) is one rank: the gathered vector is v itself.
+  subroutine gpuMatVec_mpi_cc(Nloc, v, Hv)
+    integer                    :: Nloc
+    complex(8),dimension(Nloc) :: v
+    complex(8),dimension(Nloc) :: Hv
+    complex(8),allocatable     :: vin(:)
+    integer                    :: N
+#ifdef _MPI
+    integer                    :: i, ierr, nproc
+    integer,allocatable        :: counts(:), offset(:)
+    call MPI_Comm_size(ed_gpu_comm, nproc, ierr)
+    call MPI_Allreduce(Nloc, N, 1, MPI_INTEGER, MPI_SUM, ed_gpu_comm, ierr)
+    allocate(counts(0:nproc-1), offset(0:nproc-1))
+    counts = N/nproc
+    counts(nproc-1) = N/nproc + mod(N, nproc)
+    offset = 0
+    do i = 1, nproc-1
+       offset(i) = offset(i-1) + counts(i-1)
+    enddo
+    allocate(vin(N))
+    call MPI_Allgatherv(v, Nloc, MPI_DOUBLE_COMPLEX, vin, counts, offset, MPI_DOUBLE_COMPLEX, &
+         ed_gpu_comm, ierr)
+#else
+    N = Nloc
+    allocate(vin(N))
+    vin = v
+#endif
+    call ed_gpu_check(ed_gpu_hxv_mpi(int(Nloc, c_int32_t), vin, Hv), "gpuMatVec_mpi_cc")
+  end subroutine gpuMatVec_mpi_cc
 
   !> Reference error convention: stop with a message (e.g. STORED_HxV.f90:50).
   subroutine ed_gpu_check(rc, where)

@@ -256,6 +256,21 @@ int ed_gpu_build_sector(int32_t q1, int32_t q2, int32_t flags, int64_t* dim);
 int ed_gpu_vecdim(int32_t* vecdim);           /* vecDim_Hv_sector of the current sector */
 /* cc_sparse_HxV(Nloc,v,Hv): Nloc by reference, complex(8) host arrays. */
 int ed_gpu_hxv(const int32_t* nloc, const double* v, double* hv);
+/* MPI variant of the current sector (MpiStatus=T in build_Hv_sector,
+ * ED_HAMILTONIAN.f90:55-62, 85-101): this rank holds rows [row0, row0+nrows)
+ * of H (nrows may be 0 when dim < MpiSize); vecDim_Hv_sector is then nrows. */
+int ed_gpu_build_sector_rows(int32_t q1, int32_t q2, int32_t flags, int64_t row0, int64_t nrows,
+                             int64_t* dim);
+/* The reference's row split (ED_HAMILTONIAN.f90:55-62): MpiQ = dim/size, the
+ * last rank also takes mod(dim,size); row0 = MpiIshift (0-based MpiIstart). */
+int ed_gpu_mpi_split(int64_t dim, int32_t rank, int32_t size, int64_t* row0, int64_t* nrows);
+/* spMatVec_mpi_cc (ED_HAMILTONIAN_STORED_HxV.f90:147-197) after its
+ * MPI_Allgatherv: vin is the whole sector vector (dim, complex(8)), hv the
+ * nloc = nrows local entries.  The Allgatherv itself stays in the caller's MPI
+ * (the Fortran shim's gpuMatVec_mpi_cc).  Summation: every local row in the
+ * reference's serial element order (spMatVec_cc); the reference's MPI kernel
+ * adds the local-column elements first, so the two differ by rounding. */
+int ed_gpu_hxv_mpi(const int32_t* nloc, const double* vin, double* hv);
 int ed_gpu_dump_csr(int64_t* rowptr, int32_t* cols, double* vals);
 int ed_gpu_lanc_eigh(int32_t nitermax, double threshold, int32_t ncheck, double* egs,
                      double* vect, int32_t* nlanc);

@@ -185,3 +185,24 @@ def test_row_split_two_ranks_one_gpu():
         assert p.exitcode == 0
     for rank, exact, da, nl, nr, _ in out:
         assert exact and nl == nr == 30 and da < 1e-10
+
+
+def test_empty_row_range():
+    """A rank with no rows (dim < MpiSize in build_Hv_sector's split): the
+    sector builds, vecDim is 0 and H·v is a no-op (spMatVec_mpi_cc with Nloc=0)."""
+    import torch
+
+    from edgpu.hamiltonian import Sector
+    from edgpu.params import make_config
+
+    cfg = make_config(Norb=1, Nbath=3)
+    for stored in (True, False):
+        with Sector(cfg, 0, 0, stored=stored, direct=not stored, rows=(0, 0)) as S:
+            assert S.nrows == 0 and S.dim == 1
+            x = torch.ones(S.dim, dtype=torch.complex128, device="cuda:0")
+            y = torch.empty(0, dtype=torch.complex128, device="cuda:0")
+            S.hxv_dev(x, y)
+            torch.cuda.synchronize()
+            if stored:
+                rp, cols, vals = S.dump_csr()
+                assert list(rp) == [0] and len(cols) == 0

@@ -13,12 +13,17 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DRIVER = os.path.join(ROOT, "dmft-ed_amd", "fortran", "ed_gpu_driver")
 
 
-def _run(*args):
+def _driver():
     if not os.path.exists(DRIVER):
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "dmft-ed_amd"), "fortran"], check=True)
-    r = subprocess.run([DRIVER, *map(str, args)], capture_output=True, text=True, timeout=300)
+    return DRIVER
+
+
+def _run(*args):
+    r = subprocess.run([_driver(), *map(str, args)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     vals = dict(re.findall(r"(\w+)=\s*(\S+)", r.stdout))
+    vals["_stdout"] = r.stdout
     assert "DRIVER_OK" in r.stdout
     return vals
 
@@ -38,10 +43,23 @@ def test_fortran_driver_c2(mode):
     assert abs(float(v["EIG1"]) - float(v["E0_DEV"])) < 1e-9
     assert float(v["EIG6"]) >= float(v["EIG1"])
     assert float(v["EIGRES"]) < 1e-8
+    # MpiStatus=T: rows split as build_Hv_sector does (3 ranks, and more ranks
+    # than rows so that some hold none), gpuMatVec_mpi_cc's local products
+    # assembled = the serial product: bit for bit for the stored matrix (same
+    # per-row element order); the serial matrix-free product takes the
+    # Kronecker kernel (another summation order) while row sectors take the
+    # generic one, so there the bar is rounding (1e-13)
+    mpi = re.findall(r"MPI_RANKS=(\d+) EMPTY_RANKS=(\d+) MPI_EQUAL=(\w) MPI_RELDEV=\s*(\S+)", v["_stdout"])
+    assert len(mpi) == 2
+    assert mpi[0][:2] == ("3", "0") and int(mpi[1][0]) == 4902 and int(mpi[1][1]) > 0
+    for m in mpi:
+        if mode == "stored":
+            assert m[2] == "T"
+        assert float(m[3]) < 1e-13
 
 
 def test_fortran_driver_error_is_loud():
     """Nonexistent sector (nup > Ns): the shim stops with the library's message."""
-    r = subprocess.run([DRIVER, "1", "3", "9", "0"], capture_output=True, text=True, timeout=120)
+    r = subprocess.run([_driver(), "1", "3", "9", "0"], capture_output=True, text=True, timeout=120)
     assert r.returncode != 0
     assert "ED_GPU ERROR" in r.stdout

@@ -127,3 +127,24 @@ def test_tridiag_poles_host_matches_tql2_and_lapack():
     E, z2 = tridiag_poles(a, b, 4)
     np.testing.assert_allclose(z2.sum(), 1.0, atol=1e-15)
     assert np.count_nonzero(z2 > 1e-30) == 2
+
+
+def test_mpi_split_matches_reference_formula():
+    """ed_gpu_mpi_split = build_Hv_sector's split (ED_HAMILTONIAN.f90:55-62):
+    MpiQ = Dim/MpiSize, the last rank also takes mod(Dim, MpiSize); ranks may
+    hold no rows when Dim < MpiSize.  Pure host arithmetic (no GPU call)."""
+    import ctypes
+
+    from edgpu import _lib
+
+    L = _lib.load()
+    for dim, P in [(4900, 1), (4900, 3), (4900, 8), (5, 8), (0, 2), (853776, 7)]:
+        rows = []
+        for r in range(P):
+            r0, n = ctypes.c_int64(), ctypes.c_int64()
+            assert L.ed_gpu_mpi_split(dim, r, P, ctypes.byref(r0), ctypes.byref(n)) == 0
+            q, rem = dim // P, (dim % P if r == P - 1 else 0)
+            assert (r0.value, n.value) == (r * q, q + rem)
+            rows.append((r0.value, n.value))
+        assert sum(n for _, n in rows) == dim
+        assert all(rows[i][0] + rows[i][1] == rows[i + 1][0] for i in range(P - 1))
