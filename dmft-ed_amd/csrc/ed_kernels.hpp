@@ -513,6 +513,17 @@ template <int NT> __device__ __forceinline__ double2 ldh(const double2* p) { ret
 // +10-14 % over a plain loop on the Nlevels=28 sector), summed in row order.
 constexpr int kChunk = 16;
 
+// Optional XCD-aware slice schedule for stored sectors beyond the Infinity
+// Cache (normal mode): slices sorted by their column window ((64 s) mod dimup
+// / 64), then by down row; XCD x sweeps the contiguous part lo[x] .. lo[x+1]
+// of that list, so at any time its workgroups gather the down-spin entries
+// v[iw'][window] of one window (dimdw x ~128 columns, in the XCD's L2)
+// instead of whole rows from the MALL.  One slice per wavefront.
+struct SliceOrder {
+  const int32_t* ord;  // nullptr: natural order
+  int lo[9];
+};
+
 template <bool HC, bool VC, int NT, class Epi>
 __global__ void __launch_bounds__(kBlock) k_spmv(const val_t<HC>* __restrict__ diag,
                                                  const int64_t* __restrict__ sptr,
@@ -520,16 +531,14 @@ __global__ void __launch_bounds__(kBlock) k_spmv(const val_t<HC>* __restrict__ d
                                                  const val_t<HC>* __restrict__ vals,
                                                  const val_t<VC>* __restrict__ x,
                                                  const val_t<VC>* __restrict__ xr, int64_t dim,
-                                                 int64_t nslice, Epi epi, int xcd) {
+                                                 int64_t nslice, Epi epi, int xcd, SliceOrder so) {
   using V = val_t<VC>;
   using H = val_t<HC>;
   if (epi.skip()) return;
   epi.prepare();
   double part = 0.0;
-  int64_t b = blockIdx.x;
-  if (xcd) b = (b & 7) * (gridDim.x >> 3) + (b >> 3);  // one row range per XCD (see k_spmv_pk)
-  for (int64_t i = b * kBlock + threadIdx.x; i < nslice * 64; i += (int64_t)gridDim.x * kBlock) {
-    if (i < dim) {
+  auto body = [&](int64_t i) {
+    {
       const int64_t s = (int64_t)__builtin_amdgcn_readfirstlane((int)(i >> 6));  // wave-uniform (k_spmv_pk)
       const int64_t s0 = sptr[s];
       const int w = (int)((sptr[s + 1] - s0) >> 6);
@@ -555,6 +564,20 @@ __global__ void __launch_bounds__(kBlock) k_spmv(const val_t<HC>* __restrict__ d
       }
       part += epi.row(i, acc, xi);
     }
+  };
+  if (so.ord) {
+    const int x = blockIdx.x & 7, wv = threadIdx.x >> 6;
+    const int step = (gridDim.x >> 3) * (kBlock / 64);
+    for (int p = so.lo[x] + (int)(blockIdx.x >> 3) * (kBlock / 64) + wv; p < so.lo[x + 1]; p += step) {
+      const int64_t i = (int64_t)so.ord[p] * 64 + (threadIdx.x & 63);
+      if (i < dim) body(i);
+    }
+  } else {
+    // one row range per XCD (see k_spmv_pk)
+    int64_t b = blockIdx.x;
+    if (xcd) b = (b & 7) * (gridDim.x >> 3) + (b >> 3);
+    for (int64_t i = b * kBlock + threadIdx.x; i < nslice * 64; i += (int64_t)gridDim.x * kBlock)
+      if (i < dim) body(i);
   }
   epi.finish(part);
 }
@@ -619,29 +642,87 @@ __global__ void __launch_bounds__(kBlock) k_dict_pack(const int32_t* __restrict_
   }
 }
 
-template <bool VC, int NT, class Epi>
-__global__ void __launch_bounds__(kBlock) k_spmv_pk(const double* __restrict__ diag,
+// Complex H (the reference's complex(8) arithmetic, ED_SPARSE_MATRIX.f90:11-29):
+// the same words over a dictionary of distinct (re, im) pairs.  Keys are a
+// 64-bit mix of the two bit patterns; the inserting thread records the pair,
+// and the pack kernel checks every slot's pair bit for bit against its entry
+// (a hash collision between two pairs flags overflow: the plain arrays serve).
+__device__ __forceinline__ unsigned long long pair_key(double2 v) {
+  unsigned long long a = (unsigned long long)__double_as_longlong(v.x);
+  unsigned long long b = (unsigned long long)__double_as_longlong(v.y);
+  unsigned long long k = a ^ (b * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull + (a << 6) + (a >> 2));
+  return k == kDictEmpty ? 0x7ff8dead00000001ull : k;
+}
+
+__global__ void __launch_bounds__(kBlock) k_dict_insert_c(const double2* __restrict__ vals, int64_t n,
+                                                          unsigned long long* table, double2* reps,
+                                                          unsigned int* overflow) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    const double2 v = vals[i];
+    const unsigned long long key = pair_key(v);
+    uint32_t h = dict_hash(key);
+    bool done = false;
+    for (int probe = 0; probe < kDictTable && !done; probe++) {
+      const unsigned long long cur = ((volatile unsigned long long*)table)[h];
+      if (cur == key) {
+        done = true;
+      } else if (cur == kDictEmpty) {
+        const unsigned long long prev = atomicCAS(table + h, kDictEmpty, key);
+        if (prev == kDictEmpty) {
+          reps[h] = v;  // the inserting thread records the pair
+          done = true;
+        } else if (prev == key) {
+          done = true;
+        } else {
+          h = (h + 1) & (kDictTable - 1);
+        }
+      } else {
+        h = (h + 1) & (kDictTable - 1);
+      }
+    }
+    if (!done) atomicOr(overflow, 1u);
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_dict_pack_c(const int32_t* __restrict__ cols,
+                                                        const double2* __restrict__ vals, int64_t n,
+                                                        const unsigned long long* __restrict__ table,
+                                                        const double2* __restrict__ reps,
+                                                        const uint8_t* __restrict__ tidx,
+                                                        uint32_t* __restrict__ words,
+                                                        unsigned int* overflow) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    const double2 v = vals[i];
+    const unsigned long long key = pair_key(v);
+    uint32_t h = dict_hash(key);
+    while (table[h] != key) h = (h + 1) & (kDictTable - 1);  // present by construction
+    const double2 r = reps[h];
+    if (__double_as_longlong(r.x) != __double_as_longlong(v.x) ||
+        __double_as_longlong(r.y) != __double_as_longlong(v.y))
+      atomicOr(overflow, 1u);
+    words[i] = (uint32_t)cols[i] | ((uint32_t)tidx[h] << kPackShift);
+  }
+}
+
+template <bool HC, bool VC, int NT, class Epi>
+__global__ void __launch_bounds__(kBlock) k_spmv_pk(const val_t<HC>* __restrict__ diag,
                                                     const int64_t* __restrict__ sptr,
                                                     const uint32_t* __restrict__ words,
-                                                    const double* __restrict__ dict,
+                                                    const val_t<HC>* __restrict__ dict,
                                                     const val_t<VC>* __restrict__ x,
                                                     const val_t<VC>* __restrict__ xr, int64_t dim,
-                                                    int64_t nslice, Epi epi, int xcd) {
+                                                    int64_t nslice, Epi epi, int xcd, SliceOrder so) {
   using V = val_t<VC>;
+  using H = val_t<HC>;
   if (epi.skip()) return;
   epi.prepare();
   double part = 0.0;
-  // xcd: blocks are dealt round-robin to the 8 XCDs; remap so that each XCD
-  // sweeps one contiguous range of rows (its L2 then serves the v gathers
-  // shared by neighbouring rows)
-  int64_t b = blockIdx.x;
-  if (xcd) b = (b & 7) * (gridDim.x >> 3) + (b >> 3);
   // dictionary in LDS: its lookups leave the vector-memory pipe to the gathers
-  __shared__ double sdict[256];
+  __shared__ H sdict[256];
   sdict[threadIdx.x] = dict[threadIdx.x];  // kBlock == 256 == dictionary capacity
   __syncthreads();
-  for (int64_t i = b * kBlock + threadIdx.x; i < nslice * 64; i += (int64_t)gridDim.x * kBlock) {
-    if (i < dim) {
+  auto body = [&](int64_t i) {
+    {
       // one slice per wavefront (kBlock is a multiple of 64 and lane 0 holds the
       // slice's first row): slice pointer and width are wave-uniform, so the
       // pointer loads and the k-loop bound live in scalar registers
@@ -650,13 +731,13 @@ __global__ void __launch_bounds__(kBlock) k_spmv_pk(const double* __restrict__ d
       const int w = (int)((sptr[s + 1] - s0) >> 6);
       const uint32_t* wp = words + s0 + (i & 63);
       const V xi = xr[i];
-      V acc = add(vzero<V>(), mul(ldm<NT>(diag + i), xi));
+      V acc = add(vzero<V>(), mul(ldh<NT>(diag + i), xi));
       for (int k0 = 0; k0 < w; k0 += kChunk) {
         uint32_t c[kChunk];
 #pragma unroll
         for (int k = 0; k < kChunk; k++) c[k] = (k0 + k < w) ? ldm<NT>(wp + 64 * (k0 + k)) : (uint32_t)i;
         V g[kChunk];
-        double h[kChunk];
+        H h[kChunk];
 #pragma unroll
         for (int k = 0; k < kChunk; k++) {
           g[k] = x[c[k] & kPackColMask];
@@ -668,6 +749,22 @@ __global__ void __launch_bounds__(kBlock) k_spmv_pk(const double* __restrict__ d
       }
       part += epi.row(i, acc, xi);
     }
+  };
+  if (so.ord) {
+    const int x = blockIdx.x & 7, wv = threadIdx.x >> 6;
+    const int step = (gridDim.x >> 3) * (kBlock / 64);
+    for (int p = so.lo[x] + (int)(blockIdx.x >> 3) * (kBlock / 64) + wv; p < so.lo[x + 1]; p += step) {
+      const int64_t i = (int64_t)so.ord[p] * 64 + (threadIdx.x & 63);
+      if (i < dim) body(i);
+    }
+  } else {
+    // xcd: blocks are dealt round-robin to the 8 XCDs; remap so that each XCD
+    // sweeps one contiguous range of rows (its L2 then serves the v gathers
+    // shared by neighbouring rows)
+    int64_t b = blockIdx.x;
+    if (xcd) b = (b & 7) * (gridDim.x >> 3) + (b >> 3);
+    for (int64_t i = b * kBlock + threadIdx.x; i < nslice * 64; i += (int64_t)gridDim.x * kBlock)
+      if (i < dim) body(i);
   }
   epi.finish(part);
 }

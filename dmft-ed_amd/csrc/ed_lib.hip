@@ -107,8 +107,11 @@ struct ed_sector {
   int64_t nnz = 0, padded = 0;
   // packed stored H (real values, <= 256 distinct): {col:24 | index:8} words
   uint32_t* d_words = nullptr;
-  double* d_pdict = nullptr;
+  void* d_pdict = nullptr;   // real(8) or complex(8) values (hc)
   int npdict = 0;
+  // XCD column-window slice schedule (SliceOrder, stored sectors beyond the MALL)
+  int32_t* d_sorder = nullptr;
+  int sord_lo[9] = {0};
   // matrix-free
   bool kron = false;
   KronHost K;
@@ -229,54 +232,85 @@ static void sector_free(ed_sector* s) {
 static int build_pack(ed_sector* s) {
   const int64_t slots = s->padded;
   if (slots == 0) return ED_OK;
+  const bool hc = s->hc;
+  const int hw = hc ? 2 : 1;
   unsigned long long* table;
   unsigned int* ovf;
   uint8_t* tidx;
+  double2* reps = nullptr;
   HIPCK(hipMallocAsync((void**)&table, kDictTable * 8, s->stream));
   HIPCK(hipMallocAsync((void**)&ovf, 4, s->stream));
   HIPCK(hipMallocAsync((void**)&tidx, kDictTable, s->stream));
+  if (hc) HIPCK(hipMallocAsync((void**)&reps, kDictTable * 16, s->stream));
   auto cleanup = [&]() {
     (void)hipFreeAsync(table, s->stream);
     (void)hipFreeAsync(ovf, s->stream);
     (void)hipFreeAsync(tidx, s->stream);
+    if (reps) (void)hipFreeAsync(reps, s->stream);
   };
   HIPCK(hipMemsetAsync(table, 0xFF, kDictTable * 8, s->stream));
   HIPCK(hipMemsetAsync(ovf, 0, 4, s->stream));
-  hipLaunchKernelGGL(k_dict_insert, dim3(grid_for(slots)), dim3(kBlock), 0, s->stream,
-                     (const double*)s->d_vals, slots, table, ovf);
+  if (hc)
+    hipLaunchKernelGGL(k_dict_insert_c, dim3(grid_for(slots)), dim3(kBlock), 0, s->stream,
+                       (const double2*)s->d_vals, slots, table, reps, ovf);
+  else
+    hipLaunchKernelGGL(k_dict_insert, dim3(grid_for(slots)), dim3(kBlock), 0, s->stream,
+                       (const double*)s->d_vals, slots, table, ovf);
   HIPCK(hipGetLastError());
   std::vector<unsigned long long> ht(kDictTable);
+  std::vector<double> hr(hc ? 2 * kDictTable : 0);
   unsigned int hov = 0;
   HIPCK(hipMemcpyAsync(ht.data(), table, kDictTable * 8, hipMemcpyDeviceToHost, s->stream));
+  if (hc) HIPCK(hipMemcpyAsync(hr.data(), reps, kDictTable * 16, hipMemcpyDeviceToHost, s->stream));
   HIPCK(hipMemcpyAsync(&hov, ovf, 4, hipMemcpyDeviceToHost, s->stream));
   HIPCK(hipStreamSynchronize(s->stream));
   std::vector<uint8_t> ti(kDictTable, 0);
   std::vector<double> dict;
   for (int h = 0; h < kDictTable && !hov; h++) {
     if (ht[h] == kDictEmpty) continue;
-    if (dict.size() == 256) {
+    if (dict.size() == (size_t)256 * hw) {
       hov = 1;
       break;
     }
-    ti[h] = (uint8_t)dict.size();
-    double v;
-    memcpy(&v, &ht[h], 8);
-    dict.push_back(v);
+    ti[h] = (uint8_t)(dict.size() / hw);
+    if (hc) {
+      dict.push_back(hr[2 * h]);
+      dict.push_back(hr[2 * h + 1]);
+    } else {
+      double v;
+      memcpy(&v, &ht[h], 8);
+      dict.push_back(v);
+    }
   }
   if (hov) {
     cleanup();
     return ED_OK;  // too many distinct values: the plain SELL path serves
   }
-  CK(dalloc(s, (void**)&s->d_pdict, 256 * 8));
-  CK(dalloc(s, (void**)&s->d_words, slots * 4));
-  HIPCK(hipMemcpyAsync(s->d_pdict, dict.data(), dict.size() * 8, hipMemcpyHostToDevice, s->stream));
+  uint32_t* words = nullptr;
+  void* pd = nullptr;
+  CK(dalloc(s, &pd, 256 * 8 * hw));
+  CK(dalloc(s, (void**)&words, slots * 4));
+  HIPCK(hipMemsetAsync(pd, 0, 256 * 8 * hw, s->stream));
+  HIPCK(hipMemcpyAsync(pd, dict.data(), dict.size() * 8, hipMemcpyHostToDevice, s->stream));
   HIPCK(hipMemcpyAsync(tidx, ti.data(), kDictTable, hipMemcpyHostToDevice, s->stream));
-  hipLaunchKernelGGL(k_dict_pack, dim3(grid_for(slots)), dim3(kBlock), 0, s->stream, s->d_cols,
-                     (const double*)s->d_vals, slots, table, tidx, s->d_words);
+  if (hc)
+    hipLaunchKernelGGL(k_dict_pack_c, dim3(grid_for(slots)), dim3(kBlock), 0, s->stream, s->d_cols,
+                       (const double2*)s->d_vals, slots, table, reps, tidx, words, ovf);
+  else
+    hipLaunchKernelGGL(k_dict_pack, dim3(grid_for(slots)), dim3(kBlock), 0, s->stream, s->d_cols,
+                       (const double*)s->d_vals, slots, table, tidx, words);
   HIPCK(hipGetLastError());
+  HIPCK(hipMemcpyAsync(&hov, ovf, 4, hipMemcpyDeviceToHost, s->stream));
   HIPCK(hipStreamSynchronize(s->stream));
   cleanup();
-  s->npdict = (int)dict.size();
+  if (hov) {  // a 64-bit key collision between two complex values: keep the plain path
+    dfree(s, &pd, 256 * 8 * hw);
+    dfree(s, (void**)&words, slots * 4);
+    return ED_OK;
+  }
+  s->d_pdict = pd;
+  s->d_words = words;
+  s->npdict = (int)(dict.size() / hw);
   return ED_OK;
 }
 
@@ -285,6 +319,35 @@ static int build_pack(ed_sector* s) {
 static int whole_only(const ed_sector* s) {
   if (s->nrows == s->dim) return ED_OK;
   return fail(ED_ERR_UNSUPPORTED, "row-split sector: only ed_sector_hxv_dev[_path] and ed_sector_dump_csr apply");
+}
+
+// Bytes of the stored matrix stream (the NT threshold: beyond ~192 MB it
+// cannot stay in the 256 MB MALL next to the vectors).
+static int64_t stored_mbytes(const ed_sector* s) {
+  const int64_t hv = s->hc ? 16 : 8;
+  if (s->d_words) return s->padded * 4 + s->nrows * hv;
+  return s->padded * (4 + hv) + s->nrows * hv;
+}
+
+// SliceOrder for normal-mode sectors whose matrix exceeds the MALL: slices
+// sorted by column window (64 s mod dimup) / 64, then row; the list is cut
+// into 8 equal contiguous parts, one per XCD.  Opt-in (ED_GPU_SORDER=1): it
+// moves the down-spin gathers into L2 but scatters the up-spin ones (each row
+// iw is then revisited once per window): N28 packed 0.226 -> 0.255 ms real,
+// 0.361 -> 0.405 ms complex.
+static int build_sorder(ed_sector* s) {
+  const int64_t du = s->T.dimup, ns = s->nslice;
+  if (s->Mh.mode != ED_MODE_NORMAL || du < 64 || s->nrows != s->dim || ns >= ((int64_t)1 << 31) ||
+      stored_mbytes(s) <= ((int64_t)192 << 20) || !getenv("ED_GPU_SORDER"))
+    return ED_OK;
+  const int64_t nw = (du + 63) / 64;
+  std::vector<int32_t> cnt(nw + 1, 0), ord(ns);
+  for (int64_t q = 0; q < ns; q++) cnt[((64 * q) % du) / 64 + 1]++;
+  for (int64_t c = 0; c < nw; c++) cnt[c + 1] += cnt[c];
+  for (int64_t q = 0; q < ns; q++) ord[cnt[((64 * q) % du) / 64]++] = (int32_t)q;
+  CK(upload(s, &s->d_sorder, ord));
+  for (int x = 0; x <= 8; x++) s->sord_lo[x] = (int)(ns * x / 8);
+  return ED_OK;
 }
 
 static int build_stored(ed_sector* s) {
@@ -339,7 +402,8 @@ static int build_stored(ed_sector* s) {
   int64_t nnz = dim;
   for (int64_t i = 0; i < dim; i++) nnz += hc[i];
   s->nnz = nnz;
-  if (!s->hc && s->dim <= (int64_t)kPackColMask + 1 && !getenv("ED_GPU_NO_PACK")) CK(build_pack(s));
+  if (s->dim <= (int64_t)kPackColMask + 1 && !getenv("ED_GPU_NO_PACK")) CK(build_pack(s));
+  CK(build_sorder(s));
   return ED_OK;
 }
 
@@ -570,7 +634,7 @@ static int xcd_remap() {
 // Only the packed kernel on grids of >= 1024 blocks gains (plain SELL n28:
 // 0.421 -> 0.443 ms with the remap; small grids lose blocks to the rounding).
 static bool xcd_on(const ed_sector* s, int path) {
-  return path == 0 && !s->hc && s->d_words && xcd_remap() && grid_for(s->nslice * 64) >= 1024;
+  return path == 0 && s->d_words && xcd_remap() && grid_for(s->nslice * 64) >= 1024;
 }
 // pass D of the two-pass Kronecker H·v: a multiple of 8 blocks (XCD column
 // chunks), 8 resident per CU
@@ -592,10 +656,19 @@ static bool kron2_on(const ed_sector* s, int path, int vc) {
   if (path != 2 || !s->K.two) return false;
   return kron_up_lds(s->hc, vc, s->K.dimup, 1) <= 160 * 1024;
 }
+static bool sorder_on(const ed_sector* s, int path) { return path == 0 && s->d_sorder; }
+static SliceOrder slice_order(const ed_sector* s, int path) {
+  SliceOrder so{};
+  if (sorder_on(s, path)) {
+    so.ord = s->d_sorder;
+    for (int x = 0; x <= 8; x++) so.lo[x] = s->sord_lo[x];
+  }
+  return so;
+}
 static int hxv_blocks(const ed_sector* s, int path, int vc = 0) {
   if (kron2_on(s, path, vc)) return kKronDwGrid;
   const int g = grid_for(s->nslice * 64);
-  return xcd_on(s, path) ? (g & ~7) : g;
+  return (xcd_on(s, path) || sorder_on(s, path)) ? (g & ~7) : g;
 }
 
 template <bool HC, bool VC, int CPT, int DEGU, int RU>
@@ -667,26 +740,27 @@ static int launch_hxv_t(ed_sector* s, int path, const void* x, Epi epi, hipStrea
   const int g = grid_for(ns * 64);
   const int gx = hxv_blocks(s, path);
   const int xr = xcd_on(s, path) ? 1 : 0;
+  const SliceOrder so = slice_order(s, path);
   const V* xo = (const V*)x + s->row0;  // the rows' own entries
-  if (path == 0 && !HC && s->d_words) {
-    const int64_t mbytes = s->padded * 4 + dim * 8;
-    if (mbytes > (int64_t)192 << 20)
-      hipLaunchKernelGGL((k_spmv_pk<VC, 1, Epi>), dim3(gx), dim3(kBlock), 0, st, (const double*)s->d_diag,
-                         s->d_sptr, s->d_words, s->d_pdict, (const V*)x, xo, dim, ns, epi, xr);
+  // non-temporal matrix loads once the matrix cannot stay in the 256 MB MALL
+  const bool nt = stored_mbytes(s) > ((int64_t)192 << 20);
+  if (path == 0 && s->d_words) {
+    using H = val_t<HC>;
+    if (nt)
+      hipLaunchKernelGGL((k_spmv_pk<HC, VC, 1, Epi>), dim3(gx), dim3(kBlock), 0, st, (const H*)s->d_diag,
+                         s->d_sptr, s->d_words, (const H*)s->d_pdict, (const V*)x, xo, dim, ns, epi, xr, so);
     else
-      hipLaunchKernelGGL((k_spmv_pk<VC, 0, Epi>), dim3(gx), dim3(kBlock), 0, st, (const double*)s->d_diag,
-                         s->d_sptr, s->d_words, s->d_pdict, (const V*)x, xo, dim, ns, epi, xr);
+      hipLaunchKernelGGL((k_spmv_pk<HC, VC, 0, Epi>), dim3(gx), dim3(kBlock), 0, st, (const H*)s->d_diag,
+                         s->d_sptr, s->d_words, (const H*)s->d_pdict, (const V*)x, xo, dim, ns, epi, xr, so);
   } else if (path == 0) {
-    // non-temporal matrix loads once the matrix cannot stay in the 256 MB MALL
-    const int64_t mbytes = s->padded * (4 + (HC ? 16 : 8)) + dim * (HC ? 16 : 8);
-    if (mbytes > (int64_t)192 << 20)
+    if (nt)
       hipLaunchKernelGGL((k_spmv<HC, VC, 1, Epi>), dim3(gx), dim3(kBlock), 0, st,
                          (const val_t<HC>*)s->d_diag, s->d_sptr, s->d_cols,
-                         (const val_t<HC>*)s->d_vals, (const V*)x, xo, dim, ns, epi, xr);
+                         (const val_t<HC>*)s->d_vals, (const V*)x, xo, dim, ns, epi, xr, so);
     else
       hipLaunchKernelGGL((k_spmv<HC, VC, 0, Epi>), dim3(gx), dim3(kBlock), 0, st,
                          (const val_t<HC>*)s->d_diag, s->d_sptr, s->d_cols,
-                         (const val_t<HC>*)s->d_vals, (const V*)x, xo, dim, ns, epi, xr);
+                         (const val_t<HC>*)s->d_vals, (const V*)x, xo, dim, ns, epi, xr, so);
   } else if (path == 1) {
     DevIndex idx{s->d_off, s->d_rank, s->T.ns, s->T.nst - 1};
     hipLaunchKernelGGL((k_direct<HC, VC, Epi>), dim3(g), dim3(kBlock), 0, st, s->Md, s->d_map + s->row0,
@@ -1244,7 +1318,7 @@ static int64_t persist_lds(const ed_sector* s, int vc, int mode) {
 }
 
 template <bool HC, bool VC, int MODE, int RPT, int E = 1>
-static int persist_launch_t(ed_sector* s, const PersistRun<HC>& run, int64_t lds, hipStream_t st) {
+static int persist_launch_t(ed_sector* s, const PersistRun<HC>& run, int64_t lds, hipStream_t st, int nb) {
   if constexpr ((MODE == 2 || MODE == 3) && RPT * E > preg_cap(HC, VC)) {
     return fail(ED_ERR_UNSUPPORTED, "register-resident ELL exceeds the spill-free budget");
   } else if constexpr (MODE == 4 && (HC || VC || !pkr_fits(E, RPT))) {
@@ -1253,59 +1327,71 @@ static int persist_launch_t(ed_sector* s, const PersistRun<HC>& run, int64_t lds
   constexpr int NT = MODE >= 2 ? kPRegBlock : kPBlock;
   auto fn = k_lanc_persist<HC, VC, MODE, RPT, E, NT>;
   HIPCK(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(fn, dim3(1), dim3(NT), (size_t)lds, st, run);
+  hipLaunchKernelGGL(fn, dim3(nb), dim3(NT), (size_t)lds, st, run);
   HIPCK(hipGetLastError());
   return ED_OK;
   }
 }
 
 template <bool HC, bool VC, int MODE, int W>
-static int persist_launch_e(ed_sector* s, const PersistRun<HC>& run, int64_t lds, hipStream_t st) {
+static int persist_launch_e(ed_sector* s, const PersistRun<HC>& run, int64_t lds, hipStream_t st, int nb) {
   switch (MODE == 2 ? s->preg_rpt : MODE == 3 ? s->kreg_rpt : s->pkr_rpt) {
-    case 2: return persist_launch_t<HC, VC, MODE, 2, W>(s, run, lds, st);
-    case 4: return persist_launch_t<HC, VC, MODE, 4, W>(s, run, lds, st);
-    case 6: return persist_launch_t<HC, VC, MODE, 6, W>(s, run, lds, st);
-    case 8: return persist_launch_t<HC, VC, MODE, 8, W>(s, run, lds, st);
-    default: return persist_launch_t<HC, VC, MODE, 10, W>(s, run, lds, st);
+    case 2: return persist_launch_t<HC, VC, MODE, 2, W>(s, run, lds, st, nb);
+    case 4: return persist_launch_t<HC, VC, MODE, 4, W>(s, run, lds, st, nb);
+    case 6: return persist_launch_t<HC, VC, MODE, 6, W>(s, run, lds, st, nb);
+    case 8: return persist_launch_t<HC, VC, MODE, 8, W>(s, run, lds, st, nb);
+    default: return persist_launch_t<HC, VC, MODE, 10, W>(s, run, lds, st, nb);
   }
 }
 
 template <bool HC, bool VC, int MODE>
-static int persist_launch_m(ed_sector* s, const PersistRun<HC>& run, int64_t lds, hipStream_t st) {
+static int persist_launch_m(ed_sector* s, const PersistRun<HC>& run, int64_t lds, hipStream_t st, int nb = 1) {
   if constexpr (MODE == 4) {
     if constexpr (HC || VC) {
       return fail(ED_ERR_UNSUPPORTED, "MODE 4 needs real H and vectors");
     } else {
-      return s->pkr_E == 4 ? persist_launch_e<HC, VC, 4, 4>(s, run, lds, st)
-                           : persist_launch_e<HC, VC, 4, 8>(s, run, lds, st);
+      return s->pkr_E == 4 ? persist_launch_e<HC, VC, 4, 4>(s, run, lds, st, nb)
+                           : persist_launch_e<HC, VC, 4, 8>(s, run, lds, st, nb);
     }
   } else if constexpr (MODE >= 2) {
     switch (MODE == 2 ? s->preg_E : s->kreg_W) {
-      case 8: return persist_launch_e<HC, VC, MODE, 8>(s, run, lds, st);
-      case 12: return persist_launch_e<HC, VC, MODE, 12>(s, run, lds, st);
-      case 14: return persist_launch_e<HC, VC, MODE, 14>(s, run, lds, st);
-      default: return persist_launch_e<HC, VC, MODE, 16>(s, run, lds, st);
+      case 8: return persist_launch_e<HC, VC, MODE, 8>(s, run, lds, st, nb);
+      case 12: return persist_launch_e<HC, VC, MODE, 12>(s, run, lds, st, nb);
+      case 14: return persist_launch_e<HC, VC, MODE, 14>(s, run, lds, st, nb);
+      default: return persist_launch_e<HC, VC, MODE, 16>(s, run, lds, st, nb);
     }
   } else {
   switch (persist_rpt01(s->dim)) {
-    case 1: return persist_launch_t<HC, VC, MODE, 1>(s, run, lds, st);
-    case 2: return persist_launch_t<HC, VC, MODE, 2>(s, run, lds, st);
-    case 3: return persist_launch_t<HC, VC, MODE, 3>(s, run, lds, st);
-    case 4: return persist_launch_t<HC, VC, MODE, 4>(s, run, lds, st);
-    case 5: return persist_launch_t<HC, VC, MODE, 5>(s, run, lds, st);
-    case 6: return persist_launch_t<HC, VC, MODE, 6>(s, run, lds, st);
-    case 8: return persist_launch_t<HC, VC, MODE, 8>(s, run, lds, st);
-    case 10: return persist_launch_t<HC, VC, MODE, 10>(s, run, lds, st);
-    case 12: return persist_launch_t<HC, VC, MODE, 12>(s, run, lds, st);
-    default: return persist_launch_t<HC, VC, MODE, 16>(s, run, lds, st);
+    case 1: return persist_launch_t<HC, VC, MODE, 1>(s, run, lds, st, nb);
+    case 2: return persist_launch_t<HC, VC, MODE, 2>(s, run, lds, st, nb);
+    case 3: return persist_launch_t<HC, VC, MODE, 3>(s, run, lds, st, nb);
+    case 4: return persist_launch_t<HC, VC, MODE, 4>(s, run, lds, st, nb);
+    case 5: return persist_launch_t<HC, VC, MODE, 5>(s, run, lds, st, nb);
+    case 6: return persist_launch_t<HC, VC, MODE, 6>(s, run, lds, st, nb);
+    case 8: return persist_launch_t<HC, VC, MODE, 8>(s, run, lds, st, nb);
+    case 10: return persist_launch_t<HC, VC, MODE, 10>(s, run, lds, st, nb);
+    case 12: return persist_launch_t<HC, VC, MODE, 12>(s, run, lds, st, nb);
+    default: return persist_launch_t<HC, VC, MODE, 16>(s, run, lds, st, nb);
   }
   }
 }
 
+// Workspace of a batched persistent launch: nb runs on the same H, run b at
+// R + b*ldr, P + b*ldp, st + b, alpha/beta + b*ldab.
+struct PersistBatch {
+  int nb;
+  void *R, *P;
+  LancState* st;
+  double *alpha, *beta;
+  int64_t ldr, ldp, ldab;
+};
+
 // Launch `niter` persistent iterations.  first=1 starts from the vector in R.
 template <bool VC>
-static int persist_iters(ed_sector* s, int mode, bool basis, int niter, int first, hipStream_t st) {
+static int persist_iters(ed_sector* s, int mode, bool basis, int niter, int first, hipStream_t st,
+                         const PersistBatch* bt = nullptr) {
   LancWS& w = s->ws;
+  const int nb = bt ? bt->nb : 1;
   auto fill = [&](auto& r) {
     using RT = std::remove_reference_t<decltype(r)>;
     using HT = std::remove_const_t<std::remove_pointer_t<decltype(r.diag)>>;
@@ -1336,6 +1422,17 @@ static int persist_iters(ed_sector* s, int mode, bool basis, int niter, int firs
     r.kdd = s->pkr_dd;
     r.kdegu = s->pkr_degu;
     r.kdegd = s->pkr_degd;
+    if (bt) {
+      r.R = bt->R;
+      r.P = bt->P;
+      r.st = bt->st;
+      r.alpha = bt->alpha;
+      r.beta = bt->beta;
+      r.basis = nullptr;
+      r.ldr = bt->ldr;
+      r.ldp = bt->ldp;
+      r.ldab = bt->ldab;
+    }
   };
   const int64_t lds = persist_lds(s, VC, mode);
   if (s->hc) {
@@ -1345,20 +1442,20 @@ static int persist_iters(ed_sector* s, int mode, bool basis, int niter, int firs
       fill(r);
       if (mode == 1 || mode == 3) r.K = kron_args<true>(s);
       if (mode == 4) return fail(ED_ERR_UNSUPPORTED, "MODE 4 needs real H");
-      return mode == 0 ? persist_launch_m<true, true, 0>(s, r, lds, st)
-             : mode == 1 ? persist_launch_m<true, true, 1>(s, r, lds, st)
-             : mode == 2 ? persist_launch_m<true, true, 2>(s, r, lds, st)
-                         : persist_launch_m<true, true, 3>(s, r, lds, st);
+      return mode == 0 ? persist_launch_m<true, true, 0>(s, r, lds, st, nb)
+             : mode == 1 ? persist_launch_m<true, true, 1>(s, r, lds, st, nb)
+             : mode == 2 ? persist_launch_m<true, true, 2>(s, r, lds, st, nb)
+                         : persist_launch_m<true, true, 3>(s, r, lds, st, nb);
     }
   }
   PersistRun<false> r;
   fill(r);
   if (mode == 1 || mode == 3 || (mode == 4 && s->kron)) r.K = kron_args<false>(s);
-  return mode == 0 ? persist_launch_m<false, VC, 0>(s, r, lds, st)
-         : mode == 1 ? persist_launch_m<false, VC, 1>(s, r, lds, st)
-         : mode == 2 ? persist_launch_m<false, VC, 2>(s, r, lds, st)
-         : mode == 3 ? persist_launch_m<false, VC, 3>(s, r, lds, st)
-                     : persist_launch_m<false, VC, 4>(s, r, lds, st);
+  return mode == 0 ? persist_launch_m<false, VC, 0>(s, r, lds, st, nb)
+         : mode == 1 ? persist_launch_m<false, VC, 1>(s, r, lds, st, nb)
+         : mode == 2 ? persist_launch_m<false, VC, 2>(s, r, lds, st, nb)
+         : mode == 3 ? persist_launch_m<false, VC, 3>(s, r, lds, st, nb)
+                     : persist_launch_m<false, VC, 4>(s, r, lds, st, nb);
 }
 
 static int persist_set_thresh(ed_sector* s, double thresh, hipStream_t st) {
@@ -1794,9 +1891,18 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
       T.m = nev + mp;
       std::vector<double> th2, Z2;
       int c2 = 0;
-      CK(trlan_core(T, nev, 1, maxit, tol, nullptr, 1000 + round, th2, Z2, &c2));
+      // the decision needs only a loose tolerance (a missed eigenvalue lies
+      // below ev[nev-1]; Ritz values approach the lowest from above); a
+      // found one is then re-solved to the full tolerance
+      const double tprobe = std::max(tol, 1e-7);
+      const double cut = ev[nev - 1] - 1e-9 * std::max(1.0, fabs(ev[nev - 1]));
+      CK(trlan_core(T, nev, 1, maxit, tprobe, nullptr, 1000 + round, th2, Z2, &c2));
+      if (!(c2 == 1 && th2[0] < cut)) break;
+      if (tprobe > tol) {
+        CK(trlan_core(T, nev, 1, maxit, tol, nullptr, 5000 + round, th2, Z2, &c2));
+        if (!(c2 == 1 && th2[0] < cut)) break;
+      }
       const double mu = th2[0];
-      if (!(c2 == 1 && mu < ev[nev - 1] - 1e-9 * std::max(1.0, fabs(ev[nev - 1])))) break;
       // a missed eigenvalue: its Ritz vector -> Xb[nev], then insert in order
       // (drop the current largest)
       const int ma2 = T.m - nev;
@@ -2228,6 +2334,95 @@ int ed_sector_lanc_tridiag(ed_sector* s, int32_t vtype, const void* v0, int32_t 
   }
   beta[0] = 0.0;
   if (nlanc) *nlanc = n;
+  return ED_OK;
+}
+
+// sp_lanc_tridiag for nseed start vectors on one sector (GF seeds of one
+// target sector: ED_GF_NORMAL.f90:180-193, ED_GF_NONSU2.f90:343-886).  When
+// the sector runs the persistent one-workgroup recurrence, all seeds go in
+// ONE launch, one workgroup each (same per-workgroup code as a single run:
+// identical alpha/beta); otherwise the seeds run one after the other.
+int ed_sector_lanc_tridiag_batch(ed_sector* s, int32_t vtype, int32_t nseed, const void* v0_dev,
+                                 int32_t nitermax, double threshold, double* alfa, double* beta,
+                                 int32_t* nlanc) {
+  if (!s || !v0_dev || !alfa || !beta || nitermax < 1 || nseed < 1) return fail(ED_ERR_ARG, "bad args");
+  HIPCK(hipSetDevice(s->device));
+  LancDriver d;
+  CK(make_driver(s, vtype, false, &d));
+  const size_t vs = d.vc ? 16 : 8;
+  auto unpack = [&](int k, const double* a, const double* b, int n) {
+    double* al = alfa + (size_t)k * nitermax;
+    double* be = beta + (size_t)k * nitermax;
+    for (int q = 0; q < nitermax; q++) {
+      al[q] = q < n ? a[q] : 0.0;
+      be[q] = (q >= 1 && q <= n) ? b[q] : 0.0;
+    }
+    be[0] = 0.0;
+    if (nlanc) nlanc[k] = n;
+  };
+  if (d.pm < 0 || getenv("ED_GPU_NO_BATCH")) {
+    CK(lanc_prepare(s, d.vc, nitermax, false, 0));
+    for (int k = 0; k < nseed; k++) {
+      CK(lanc_load_start(s, d.vc, (const unsigned char*)v0_dev + (size_t)k * s->dim * vs, true));
+      CK(d.start(threshold));
+      CK(d.iters(nitermax, true));
+      std::vector<double> a(nitermax + 1), b(nitermax + 2);
+      LancState hs;
+      HIPCK(hipMemcpyAsync(a.data(), s->ws.alpha, nitermax * 8, hipMemcpyDeviceToHost, d.st));
+      HIPCK(hipMemcpyAsync(b.data(), s->ws.beta, (nitermax + 1) * 8, hipMemcpyDeviceToHost, d.st));
+      HIPCK(hipMemcpyAsync(&hs, s->ws.st, sizeof(hs), hipMemcpyDeviceToHost, d.st));
+      HIPCK(hipStreamSynchronize(d.st));
+      unpack(k, a.data(), b.data(), hs.iter);
+    }
+    return ED_OK;
+  }
+  CK(lanc_prepare(s, d.vc, nitermax, false, 0));  // register tables / dictionaries of the persistent mode
+  PersistBatch bt;
+  bt.nb = nseed;
+  bt.ldr = s->dim;
+  bt.ldp = (int64_t)p_rows(s);
+  bt.ldab = 2 * ((int64_t)nitermax + 2);
+  hipStream_t st = d.st;
+  void *R = nullptr, *P = nullptr, *ab = nullptr, *sts = nullptr;
+  HIPCK(hipMallocAsync(&R, (size_t)nseed * bt.ldr * vs, st));
+  HIPCK(hipMallocAsync(&P, (size_t)nseed * bt.ldp * vs, st));
+  HIPCK(hipMallocAsync(&ab, (size_t)nseed * bt.ldab * 8, st));
+  HIPCK(hipMallocAsync(&sts, (size_t)nseed * sizeof(LancState), st));
+  auto release = [&]() {
+    (void)hipFreeAsync(R, st);
+    (void)hipFreeAsync(P, st);
+    (void)hipFreeAsync(ab, st);
+    (void)hipFreeAsync(sts, st);
+  };
+  bt.R = R;
+  bt.P = P;
+  bt.st = (LancState*)sts;
+  bt.alpha = (double*)ab;
+  bt.beta = (double*)ab + nitermax + 2;
+  s->pthresh = threshold;
+  int rc = ED_OK;
+  if (hipMemcpyAsync(R, v0_dev, (size_t)nseed * s->dim * vs, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+      hipMemsetAsync(P, 0, (size_t)nseed * bt.ldp * vs, st) != hipSuccess ||
+      hipMemsetAsync(ab, 0, (size_t)nseed * bt.ldab * 8, st) != hipSuccess ||
+      hipMemsetAsync(sts, 0, (size_t)nseed * sizeof(LancState), st) != hipSuccess)
+    rc = fail(ED_ERR_HIP, "batch workspace");
+  if (rc == ED_OK)
+    rc = d.vc ? persist_iters<true>(s, d.pm, false, nitermax, 1, st, &bt)
+              : persist_iters<false>(s, d.pm, false, nitermax, 1, st, &bt);
+  std::vector<double> hab((size_t)nseed * bt.ldab);
+  std::vector<LancState> hst(nseed);
+  if (rc == ED_OK) {
+    HIPCK(hipMemcpyAsync(hab.data(), ab, hab.size() * 8, hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(hst.data(), sts, nseed * sizeof(LancState), hipMemcpyDeviceToHost, st));
+  }
+  release();
+  HIPCK(hipStreamSynchronize(st));
+  CK(rc);
+  for (int k = 0; k < nseed; k++) {
+    // a run that never broke down ends with st->iter = nitermax
+    const double* a = hab.data() + (size_t)k * bt.ldab;
+    unpack(k, a, a + nitermax + 2, hst[k].iter);
+  }
   return ED_OK;
 }
 

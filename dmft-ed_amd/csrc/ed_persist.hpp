@@ -62,6 +62,10 @@ struct PersistRun {
   double thresh;     // breakdown threshold (|b| < thresh stops)
   int niter;         // iterations in this launch
   int first;         // 1: R holds the unnormalised start vector
+  // batched launches (one workgroup per run, same H): run b = blockIdx.x uses
+  // R + b*ldr, P + b*ldp, st + b, alpha/beta + b*ldab (0: single run)
+  int64_t ldr, ldp;
+  int64_t ldab;
 };
 
 // Wave sum on DPP row operations (no LDS traffic, ~6 dependent VALU steps
@@ -154,9 +158,10 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
   V* vl = (V*)smem;                // MODE 2/3 move it behind the dictionary
   const int64_t dim = a.dim;
   const int tid = threadIdx.x;
-  V* Rg = (V*)a.R;
-  V* Pg = (V*)a.P;
-  LancState* st = a.st;
+  const int run = blockIdx.x;  // batched launches: one independent run per workgroup
+  V* Rg = (V*)a.R + run * a.ldr;
+  V* Pg = (V*)a.P + run * a.ldp;
+  LancState* st = a.st + run;
   PRows q = persist_rows<MODE, RPT, NT>(tid, dim, a.kdu, a.kdd);
 #define PROW(r) (q.row0 + (r) * q.stride)
 
@@ -356,9 +361,9 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
   }
   if (st->done && !a.first) return;
   const double thresh = a.thresh;
-  double* const alpha_out = a.alpha;
-  double* const beta_out = a.beta;
-  V* const basis = (V*)a.basis;
+  double* const alpha_out = a.alpha + run * a.ldab;
+  double* const beta_out = a.beta + run * a.ldab;
+  V* const basis = run == 0 ? (V*)a.basis : nullptr;
 
   for (int k = 0; k < a.niter; k++) {
     const int it = it0 + k;

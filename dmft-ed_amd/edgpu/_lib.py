@@ -45,6 +45,7 @@ SIGNATURES = {
     "ed_sector_apply_op": ([_P, _P, _i32, _i32, _i32, _P, _P, _P], ctypes.c_int),
     "ed_sector_apply_op_acc": ([_P, _P, _i32, _i32, _f64, _f64, _i32, _P, _P, _P], ctypes.c_int),
     "ed_sector_lanc_tridiag_dev": ([_P, _i32, _P, _i32, _f64, _P, _P, _P], ctypes.c_int),
+    "ed_sector_lanc_tridiag_batch": ([_P, _i32, _i32, _P, _i32, _f64, _P, _P, _P], ctypes.c_int),
     "ed_tridiag_poles": ([_i32, _P, _P, _P, _P], ctypes.c_int),
     "ed_gpu_init": ([_P], ctypes.c_int),
     "ed_gpu_set_device": ([_i32], ctypes.c_int),

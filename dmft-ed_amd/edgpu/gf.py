@@ -51,6 +51,10 @@ class GFOptions:
     # device sectors); contributions are added to G in job order, so the
     # result is bit-identical to the serial loop
     workers: int = 4
+    # seeds grouped by target sector: one sector build and one batched
+    # persistent Lanczos launch per group (one workgroup per seed,
+    # ed_sector_lanc_tridiag_batch); bit-identical to the per-seed runs
+    batch: bool = True
 
 
 def matsubara(beta: float, L: int) -> np.ndarray:
@@ -244,6 +248,75 @@ def _run_job(cfg, states, gopt, job, cache, wm, wr, G_m, G_r, record, zeta):
     add_poles(G_m, G_r, weight * norm2 / zeta, e_i, E, z2, isign, wm, wr, gopt.eps)
 
 
+def _tridiag_batch(S: Sector, seeds, nlanc: int, real: bool, threshold: float):
+    """sp_lanc_tridiag of every seed (rows of the contiguous `seeds` tensor) on S."""
+    k = seeds.shape[0]
+    a = np.zeros((k, nlanc))
+    b = np.zeros((k, nlanc))
+    n = np.zeros(k, dtype=np.int32)
+    check(_lib.load().ed_sector_lanc_tridiag_batch(S.handle, 0 if real else 1, k,
+                                                   ctypes.c_void_p(seeds.data_ptr()), nlanc, threshold,
+                                                   a.ctypes.data_as(ctypes.c_void_p),
+                                                   b.ctypes.data_as(ctypes.c_void_p),
+                                                   n.ctypes.data_as(ctypes.c_void_p)),
+          "ed_sector_lanc_tridiag_batch")
+    return a, b, n
+
+
+def _run_jobs_batched(cfg, states, gopt, jobs, todo, device, wm, wr, Gm, Gr, zeta, record=None):
+    """The seed loop grouped by (target sector, vector type): each group's
+    seeds are built on the device, tridiagonalised in one batched launch, and
+    their pole sums computed per job exactly as _run_job; contributions are
+    added to G in job order (the serial loop's sequence of additions)."""
+    import torch
+
+    torch.cuda.set_device(device)
+    cache = _SectorCache(cfg, gopt, device)
+    groups = {}
+    for n in todo:
+        comp, tag, k, (op, isign, ispin, terms, weight), sec, jsec = jobs[n]
+        vec = states.vectors[k]
+        if vec is None:
+            raise ValueError("the Green's function needs the state vectors (keep_vectors=True)")
+        cplx = (not cfg.is_real()) or np.iscomplexobj(vec) or any(np.imag(c) != 0 for _, c in terms)
+        groups.setdefault((jsec.q1, jsec.q2, cplx), []).append(n)
+    contrib = {}
+    try:
+        for (_, _, cplx), members in groups.items():
+            live, seeds, norms = [], [], []
+            for n in members:
+                comp, tag, k, (op, isign, ispin, terms, weight), sec, jsec = jobs[n]
+                HI, HJ = cache.get(sec, False), cache.get(jsec, True)
+                seed, norm2 = _seed(HI, HJ, op, terms, states.vectors[k], cplx)
+                if norm2 == 0.0:
+                    continue
+                live.append(n)
+                seeds.append(seed)
+                norms.append(norm2)
+            if not live:
+                continue
+            HJ = cache.get(jobs[live[0]][5], True)
+            nlanc = min(HJ.dim, gopt.lanc_nGFiter)
+            a, b, nl = _tridiag_batch(HJ, torch.stack(seeds).contiguous(), nlanc, not cplx, gopt.threshold)
+            for q, n in enumerate(live):
+                comp, tag, k, (op, isign, ispin, terms, weight), sec, jsec = jobs[n]
+                E, z2 = tridiag_poles(a[q], b[q], nlanc)
+                if record is not None:
+                    record.append((n, dict(channel=tag, isector=states.sectors[k], op=op, norm2=norms[q],
+                                           alfa=a[q], beta=b[q], nlanc=int(nl[q]))))
+                c_m = np.zeros(gopt.Lmats, dtype=np.complex128)
+                c_r = np.zeros(gopt.Lreal, dtype=np.complex128)
+                add_poles(c_m, c_r, weight * norms[q] / zeta, states.energies[k], E, z2, isign, wm, wr, gopt.eps)
+                contrib[n] = (c_m, c_r)
+    finally:
+        cache.close()
+    for n in todo:
+        if n in contrib:
+            ispin, jspin, iorb = jobs[n][0]
+            Gm[ispin, jspin, iorb, iorb] += contrib[n][0]
+            Gr[ispin, jspin, iorb, iorb] += contrib[n][1]
+
+
 def _run_jobs_threaded(cfg, states, gopt, jobs, todo, device, wm, wr, Gm, Gr, zeta):
     """The seed loop on `gopt.workers` host threads (one sector cache per
     thread); each job's pole sum goes into its own zero arrays, which are then
@@ -341,7 +414,12 @@ def build_gf(cfg: EDConfig, states: StateList, gopt: Optional[GFOptions] = None,
         mine = set(range(len(jobs)))
     zeta = float(states.size)       # T=0: zeta_function = state_list%size (ED_DIAG.f90:411)
     todo = [n for n in range(len(jobs)) if n in mine]
-    if runner is None and record is None and gopt.workers > 1 and len(todo) > 1:
+    if runner is None and gopt.batch:
+        rec = [] if record is not None else None
+        _run_jobs_batched(cfg, states, gopt, jobs, todo, device, wm, wr, Gm, Gr, zeta, rec)
+        if record is not None:
+            record.extend(r for _, r in sorted(rec, key=lambda t: t[0]))
+    elif runner is None and record is None and gopt.workers > 1 and len(todo) > 1:
         _run_jobs_threaded(cfg, states, gopt, jobs, todo, device, wm, wr, Gm, Gr, zeta)
     else:
         cache = _SectorCache(cfg, gopt, device)

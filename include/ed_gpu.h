@@ -242,6 +242,15 @@ int ed_sector_apply_op_acc(const ed_sector* src, const ed_sector* dst, int32_t o
 /* v0_dev must be complete on entry (synchronise the stream that wrote it). */
 int ed_sector_lanc_tridiag_dev(ed_sector* s, int32_t vtype, const void* v0_dev, int32_t nitermax,
                                double threshold, double* alfa, double* beta, int32_t* nlanc);
+/* sp_lanc_tridiag for nseed device start vectors (v0_dev: nseed x dim,
+ * contiguous, not modified) on the same sector — the Green's-function seeds
+ * of one target sector (ED_GF_NORMAL.f90:180-193, ED_GF_NONSU2.f90:343-886).
+ * Sectors that run the persistent one-workgroup recurrence take all seeds in
+ * one launch, one workgroup per seed; alfa/beta/nlanc: nseed x nitermax /
+ * nseed, each as ed_sector_lanc_tridiag. */
+int ed_sector_lanc_tridiag_batch(ed_sector* s, int32_t vtype, int32_t nseed, const void* v0_dev,
+                                 int32_t nitermax, double threshold, double* alfa, double* beta,
+                                 int32_t* nlanc);
 /* GF poles of one continued fraction (host, O(n^2)): E[n] ascending eigenvalues
  * of tridiag(alfa[0:n], beta[1:n]) and z2[n] the squared first components of
  * their eigenvectors.  Replaces tql2 in add_to_lanczos_gf_nonsu2

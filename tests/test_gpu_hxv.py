@@ -166,24 +166,51 @@ def test_full_size_roofline_sectors(pin):
 @pytest.mark.parametrize("name,factory,sectors", CASES, ids=[c[0] for c in CASES])
 def test_packed_matches_plain_sell(name, factory, sectors, monkeypatch):
     """Packed stored H ({col|value index} words over the distinct values) gives
-    bit-identical H·v to the plain SELL arrays, real and complex vectors."""
+    bit-identical H·v to the plain SELL arrays: real(8) H with real and complex
+    vectors, and complex(8) H (the reference's arithmetic, dictionary of
+    (re, im) pairs) with complex vectors."""
     from edgpu.hamiltonian import Sector
 
     cfg = factory()
-    if not cfg.is_real():
-        pytest.skip("packing applies to real Hamiltonians")
     q1, q2 = sectors[0]
-    with Sector(cfg, q1, q2, stored=True, real=True) as S:
-        monkeypatch.setenv("ED_GPU_NO_PACK", "1")
-        with Sector(cfg, q1, q2, stored=True, real=True) as P:
-            assert P.info.packed == 0
-            assert S.info.packed == 1 and 1 <= S.info.npdict <= 256
-            i = np.arange(1, S.dim + 1, dtype=np.float64)
-            for x in (np.sin(i), np.sin(i) + 1j * np.cos(3 * i)):
-                xd = _dev(x)
-                y1 = torch.empty_like(xd)
-                y2 = torch.empty_like(xd)
-                S.hxv_dev(xd, y1, path=0)
-                P.hxv_dev(xd, y2, path=0)
-                torch.cuda.synchronize()
-                assert torch.equal(y1, y2)
+    for real in ((True, False) if cfg.is_real() else (False,)):
+        monkeypatch.delenv("ED_GPU_NO_PACK", raising=False)
+        with Sector(cfg, q1, q2, stored=True, real=real) as S:
+            monkeypatch.setenv("ED_GPU_NO_PACK", "1")
+            with Sector(cfg, q1, q2, stored=True, real=real) as P:
+                assert P.info.packed == 0
+                assert S.info.packed == 1 and 1 <= S.info.npdict <= 256
+                i = np.arange(1, S.dim + 1, dtype=np.float64)
+                xs = (np.sin(i), np.sin(i) + 1j * np.cos(3 * i)) if real else (np.sin(i) + 1j * np.cos(3 * i),)
+                for x in xs:
+                    xd = _dev(x)
+                    y1 = torch.empty_like(xd)
+                    y2 = torch.empty_like(xd)
+                    S.hxv_dev(xd, y1, path=0)
+                    P.hxv_dev(xd, y2, path=0)
+                    torch.cuda.synchronize()
+                    assert torch.equal(y1, y2)
+
+
+@pytest.mark.parametrize("cplx", [False, True])
+def test_slice_order_schedule_bit_identical(cplx, monkeypatch):
+    """Nlevels=28 sector (matrix beyond the MALL): the XCD column-window slice
+    schedule visits every slice once with the same per-row arithmetic —
+    identical H·v to the natural order, packed real and packed complex H."""
+    from edgpu.hamiltonian import Sector
+    from edgpu.params import make_config
+
+    cfg = make_config(Norb=1, Nbath=13, bath="random", seed=3)
+    g = torch.Generator(device="cuda:0").manual_seed(1)
+    monkeypatch.setenv("ED_GPU_SORDER", "1")
+    with Sector(cfg, 7, 7, stored=True, real=not cplx) as S:
+        monkeypatch.delenv("ED_GPU_SORDER")
+        with Sector(cfg, 7, 7, stored=True, real=not cplx) as P:
+            assert S.info.packed == 1 and P.info.packed == 1
+            dt = torch.complex128 if cplx else torch.float64
+            x = torch.rand(S.dim, dtype=dt, device="cuda:0", generator=g)
+            y1, y2 = torch.empty_like(x), torch.empty_like(x)
+            S.hxv_dev(x, y1, path=0)
+            P.hxv_dev(x, y2, path=0)
+            torch.cuda.synchronize()
+            assert torch.equal(y1, y2)

@@ -9,7 +9,9 @@ from edgpu.diag import DiagOptions, lanczos_params, _start_vector
 from edgpu.sectors import setup_pointers
 from edgpu.hamiltonian import Sector
 
-cfg = make_config(Norb=2, Nbath=5, bath="random", seed=20251015)
+sys.path.insert(0, os.path.join(os.getcwd(), "tests"))
+from golden.golden_configs import c4_config
+cfg = c4_config("random")
 opt = DiagOptions()
 tot = {"build": 0.0, "eigh": 0.0, "dense_build": 0.0, "dense_dump": 0.0, "dense_eigh": 0.0, "close": 0.0}
 rows = []

@@ -9,7 +9,9 @@ from edgpu.farm import farm_diag  # noqa: E402
 from edgpu.gf import GFOptions, build_gf  # noqa: E402
 from edgpu.params import make_config  # noqa: E402
 
-cfg = make_config(Norb=1, Nbath=6, Nspin=2, ed_mode="nonsu2", bath="random", seed=20251015)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+from golden.golden_configs import c5_config
+cfg = c5_config("random")
 res = farm_diag(cfg, DiagOptions(), device=0)
 g = GFOptions()
 build_gf(cfg, res.states, g, device=0)
