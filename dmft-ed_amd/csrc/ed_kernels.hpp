@@ -890,7 +890,15 @@ __global__ void __launch_bounds__(kBlock) k_kron(KronArgs<HC> K, const val_t<VC>
 // pass U writes into the epilogue's scratch (its output buffer).
 constexpr int kKronUpBlock = 1024;
 constexpr int kKronDictMax = 256;
-constexpr int kKronRowsPerWave = 4;   // pass D tile: 4 waves x 4 rows x 64 columns
+#ifndef ED_KRON_DW_R
+#define ED_KRON_DW_R 4
+#endif
+constexpr int kKronRowsPerWave = ED_KRON_DW_R;   // pass D tile: 4 waves x 4 rows x 64 columns
+constexpr int kKronUimpMax = 64;      // U[imp][imp] table entries (Norb <= 3)
+#ifndef ED_KRON_UP_PF
+#define ED_KRON_UP_PF 1
+#endif
+constexpr int kKronUpPF = ED_KRON_UP_PF;
 
 template <bool HC, bool VC, int CPT, int DEG, int kKronUpRows>
 __global__ void __launch_bounds__(kKronUpBlock) k_kron_up(KronArgs<HC> K, const uint32_t* __restrict__ upw,
@@ -900,13 +908,18 @@ __global__ void __launch_bounds__(kKronUpBlock) k_kron_up(KronArgs<HC> K, const 
   using H = val_t<HC>;
   extern __shared__ __align__(16) unsigned char smem[];
   H* sdict = (H*)smem;
+  // the impurity interaction table U[imp(iu)][imp(iw)] (<= 8 x 8) in LDS: a
+  // global load there sat in every step's dependency chain (L2 round trip
+  // between the barrier and the first FMA, exposed at one workgroup per CU)
+  double* suimp = (double*)(smem + kKronDictMax * sizeof(H));
   const int du = (int)K.dimup;
   const int64_t dd = K.dimdw;
   const int dup = (du + 1) & ~1;
-  V* bufs = (V*)(smem + kKronDictMax * sizeof(H));  // 2 sets x kKronUpRows rows
+  V* bufs = (V*)(smem + kKronDictMax * sizeof(H) + kKronUimpMax * sizeof(double));  // 2 sets x kKronUpRows rows
   const int t = threadIdx.x;
   const int64_t G = gridDim.x;
   for (int q = t; q < ndict; q += kKronUpBlock) sdict[q] = updict[q];
+  for (int q = t; q < K.nimp * K.nimp; q += kKronUpBlock) suimp[q] = K.uimp[q];
   const int degup = K.degup;
   uint32_t w[CPT][DEG];
   H au[CPT];
@@ -927,23 +940,37 @@ __global__ void __launch_bounds__(kKronUpBlock) k_kron_up(KronArgs<HC> K, const 
   struct Pair {
     V a, b;
   };
-  V xr[kKronUpRows][CPT];
+  // PF steps of rows in flight in registers (ED_KRON_UP_PF, default 2: one
+  // step's 2 rows are 55 KB per CU, too few bytes in flight to cover the
+  // loaded HBM latency at one workgroup per CU)
+  V xr[kKronUpPF][kKronUpRows][CPT];
   int64_t base = blockIdx.x;
 #pragma unroll
-  for (int r = 0; r < kKronUpRows; r++)
-#pragma unroll
-    for (int j = 0; j < CPT; j++) {
-      const int iu = t + kKronUpBlock * j;
-      const int64_t iw = base + r * G;
-      xr[r][j] = (iw < dd && iu < du) ? x[(int)iw * du + iu] : vzero<V>();
-    }
-  int pb = 0;
-  for (; base < dd; base += kKronUpRows * G) {
-    V xc[kKronUpRows][CPT];
+  for (int f = 0; f < kKronUpPF; f++)
 #pragma unroll
     for (int r = 0; r < kKronUpRows; r++)
 #pragma unroll
-      for (int j = 0; j < CPT; j++) xc[r][j] = xr[r][j];
+      for (int j = 0; j < CPT; j++) {
+        const int iu = t + kKronUpBlock * j;
+        const int64_t iw = base + (f * kKronUpRows + r) * G;
+        xr[f][r][j] = (iw < dd && iu < du) ? x[(int)iw * du + iu] : vzero<V>();
+      }
+  // down-spin diagonal factors of the rows in flight (wave-uniform), loaded
+  // with them
+  H adn[kKronUpPF][kKronUpRows];
+  int imdn[kKronUpPF][kKronUpRows];
+#pragma unroll
+  for (int f = 0; f < kKronUpPF; f++)
+#pragma unroll
+    for (int r = 0; r < kKronUpRows; r++) {
+      const int64_t iw = base + (f * kKronUpRows + r) * G;
+      const int64_t iwc = iw < dd ? iw : 0;
+      adn[f][r] = K.adw[iwc];
+      imdn[f][r] = K.impd[iwc];
+    }
+  int pb = 0;
+  for (; base < dd; base += kKronUpRows * G) {
+
 #ifdef ED_KRON_UP_ONESET
     // one LDS set (half the LDS: two workgroups per CU), two barriers per step
     V* buf = bufs;
@@ -955,38 +982,60 @@ __global__ void __launch_bounds__(kKronUpBlock) k_kron_up(KronArgs<HC> K, const 
     for (int j = 0; j < CPT; j++) {
       const int iu = t + kKronUpBlock * j;
       if (iu < du) {
-        if constexpr (kKronUpRows == 2) ((Pair*)buf)[iu] = Pair{xr[0][j], xr[1][j]};
-        else buf[iu] = xr[0][j];
+        if constexpr (kKronUpRows == 2) ((Pair*)buf)[iu] = Pair{xr[0][0][j], xr[0][1][j]};
+        else buf[iu] = xr[0][0][j];
       }
     }
     __syncthreads();  // rows staged; (two sets: the reads of the step before last are done)
-    const int64_t nb = base + kKronUpRows * G;
-#pragma unroll
-    for (int r = 0; r < kKronUpRows; r++)
-#pragma unroll
-      for (int j = 0; j < CPT; j++) {
-        const int iu = t + kKronUpBlock * j;
-        const int64_t iw = nb + r * G;
-        xr[r][j] = (iw < dd && iu < du) ? x[(int)iw * du + iu] : vzero<V>();
-      }
     H ad[kKronUpRows];
     int imd[kKronUpRows];
 #pragma unroll
     for (int r = 0; r < kKronUpRows; r++) {
-      const int64_t iw = base + r * G < dd ? base + r * G : base;
-      ad[r] = K.adw[iw];
-      imd[r] = K.impd[iw];
+      ad[r] = adn[0][r];
+      imd[r] = imdn[0][r];
+    }
+#pragma unroll
+    for (int f = 0; f + 1 < kKronUpPF; f++)
+#pragma unroll
+      for (int r = 0; r < kKronUpRows; r++) {
+        adn[f][r] = adn[f + 1][r];
+        imdn[f][r] = imdn[f + 1][r];
+#pragma unroll
+        for (int j = 0; j < CPT; j++) xr[f][r][j] = xr[f + 1][r][j];
+      }
+    const int64_t nb = base + kKronUpPF * kKronUpRows * G;
+#pragma unroll
+    for (int r = 0; r < kKronUpRows; r++) {
+      const int64_t iw = nb + r * G;
+      const int64_t iwc = iw < dd ? iw : 0;
+      adn[kKronUpPF - 1][r] = K.adw[iwc];
+      imdn[kKronUpPF - 1][r] = K.impd[iwc];
+#pragma unroll
+      for (int j = 0; j < CPT; j++) {
+        const int iu = t + kKronUpBlock * j;
+        xr[kKronUpPF - 1][r][j] = (iw < dd && iu < du) ? x[(int)iw * du + iu] : vzero<V>();
+      }
     }
     const bool second = kKronUpRows == 2 && base + G < dd;
 #pragma unroll
     for (int j = 0; j < CPT; j++) {
       const int iu = t + kKronUpBlock * j;
       if (iu < du) {
+        // the element's own value for the diagonal term is read back from the
+        // staged row (no register copy: the prefetch ring needs the VGPRs)
+        V xo[kKronUpRows];
+        if constexpr (kKronUpRows == 2) {
+          const Pair p = ((const Pair*)buf)[iu];
+          xo[0] = p.a;
+          xo[kKronUpRows - 1] = p.b;
+        } else {
+          xo[0] = buf[iu];
+        }
         V acc[kKronUpRows];
 #pragma unroll
         for (int r = 0; r < kKronUpRows; r++) {
-          const auto d = add(add(au[j], ad[r]), mk<HC>(K.uimp[imu[j] * K.nimp + imd[r]], 0.0));
-          acc[r] = mul(d, xc[r][j]);
+          const auto d = add(add(au[j], ad[r]), mk<HC>(suimp[imu[j] * K.nimp + imd[r]], 0.0));
+          acc[r] = mul(d, xo[r]);
         }
 #pragma unroll
         for (int k = 0; k < DEG; k++)
@@ -1071,7 +1120,12 @@ __global__ void __launch_bounds__(kBlock) k_kron_dw(KronArgs<HC> K, const uint32
 #pragma unroll
       for (int k = 0; k < DEG; k++) g[r][k] = (on && k < degdw) ? x[(int)wo[r][k] + iu] : vzero<V>();
       xv[r] = on ? x[i] : vzero<V>();
+#ifdef ED_KRON_DW_NT
+      // y is read once: keep it from evicting the XCD's V chunk from L2
+      yv[r] = on ? ldh<1>(ypart + i) : vzero<V>();
+#else
       yv[r] = on ? ypart[i] : vzero<V>();
+#endif
     }
 #pragma unroll
     for (int r = 0; r < R; r++) {

@@ -458,6 +458,7 @@ static int build_kron_words(ed_sector* s, int sp, const std::vector<int32_t>& co
     if (env && env[0] == '0') return ED_OK;
     if (s->dim < kKron2MinDim && !(env && env[0] == '1')) return ED_OK;
     if (nr > 8192 || deg > 16 || s->dim >= ((int64_t)1 << 31)) return ED_OK;  // 32-bit element offsets
+    if (K.nimp * K.nimp > kKronUimpMax) return ED_OK;                          // U table in LDS
     int cpt = 1;
     while (cpt * kKronUpBlock < nr) cpt *= 2;
     K.cpt = cpt;
@@ -649,7 +650,7 @@ static constexpr int kKronUpSets = 1;
 static constexpr int kKronUpSets = 2;
 #endif
 static size_t kron_up_lds(bool hc, bool vc, int64_t du, int rows) {
-  return kKronDictMax * (hc ? 16 : 8) + kKronUpSets * rows * (size_t)((du + 1) & ~1) * (vc ? 16 : 8);
+  return kKronDictMax * (hc ? 16 : 8) + kKronUimpMax * 8 + kKronUpSets * rows * (size_t)((du + 1) & ~1) * (vc ? 16 : 8);
 }
 static int kron_up_rows(bool hc, bool vc, int64_t du) { return kron_up_lds(hc, vc, du, 2) <= 160 * 1024 ? 2 : 1; }
 static bool kron2_on(const ed_sector* s, int path, int vc) {
@@ -1921,7 +1922,9 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
     }
   }
   for (int i = 0; i < nev; i++) evals[i] = ev[i];
-  if (evecs) HIPCK(hipMemcpyAsync(evecs, T.Vb, (size_t)nev * dim * vs, hipMemcpyDeviceToHost, st));
+  // host or device destination (unified addressing): a farm keeps the
+  // sector eigenvectors in HBM and copies back only the kept states
+  if (evecs) HIPCK(hipMemcpyAsync(evecs, T.Vb, (size_t)nev * dim * vs, hipMemcpyDefault, st));
   HIPCK(hipStreamSynchronize(st));
   if (nconv) *nconv = conv;
   if (nhv) *nhv = T.nhv;
@@ -2716,7 +2719,7 @@ int ed_sector_lanc_eigh(ed_sector* s, int32_t vtype, const void* v0, int32_t nit
       hipLaunchKernelGGL(k_scale_tmp<false>, dim3(grid_for(s->dim)), dim3(kBlock), 0, s->stream,
                          (double*)w.Y, s->dim, w.st);
     HIPCK(hipGetLastError());
-    HIPCK(hipMemcpyAsync(vect, w.Y, s->dim * vs, hipMemcpyDeviceToHost, s->stream));
+    HIPCK(hipMemcpyAsync(vect, w.Y, s->dim * vs, hipMemcpyDefault, s->stream));
     HIPCK(hipStreamSynchronize(s->stream));
   }
   return ED_OK;

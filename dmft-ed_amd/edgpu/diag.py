@@ -41,6 +41,10 @@ class DiagOptions:
     gs_threshold: float = 1e-9
     mpi_size: int = 1
     keep_vectors: bool = True
+    # Lanczos / thick-restart eigenvectors stay in HBM (torch tensors on the
+    # sector's GPU); only the states the T=0 list keeps are retained, and
+    # nothing crosses PCIe unless a caller asks for host copies (to_host)
+    device_vectors: bool = True
     # sectors solved concurrently on one GPU (host threads, one HIP stream per
     # sector; ctypes releases the GIL): small sectors are launch-latency bound
     workers: int = 8
@@ -86,6 +90,21 @@ def lanczos_params(dim: int, opt: DiagOptions) -> Tuple[int, int, int]:
     return neigen, nitermax, nblock
 
 
+def to_host(vec):
+    """A state vector as a host numpy array (device tensors are copied back)."""
+    if vec is None or isinstance(vec, np.ndarray):
+        return vec
+    return vec.detach().cpu().numpy()
+
+
+def is_complex_vector(vec) -> bool:
+    if vec is None:
+        return False
+    if isinstance(vec, np.ndarray):
+        return np.iscomplexobj(vec)
+    return bool(vec.is_complex())
+
+
 def _start_vector(dim: int, cplx: bool) -> np.ndarray:
     i = np.arange(1, dim + 1, dtype=np.float64)
     return (np.sin(i) + 1j * np.cos(3.0 * i)) if cplx else np.sin(i)
@@ -111,7 +130,8 @@ def solve_sector(cfg: EDConfig, sec: SectorId, opt: DiagOptions, device: int = 0
     with Sector(cfg, sec.q1, sec.q2, stored=True, real=real, device=device) as S:
         if opt.lanc_method == "lanczos":
             e0, vec, _ = S.lanc_eigh(nitermax=nitermax, threshold=opt.lanc_tolerance,
-                                     v0=_start_vector(dim, not real), vector=opt.keep_vectors)
+                                     v0=_start_vector(dim, not real), vector=opt.keep_vectors,
+                                     on_device=opt.device_vectors)
             vecs = vec[:, None] if vec is not None else None
             return SectorResult(sec.isector, q, dim, np.array([e0]), 1, vecs, "lanczos")
         if neigen >= dim:
@@ -119,10 +139,11 @@ def solve_sector(cfg: EDConfig, sec: SectorId, opt: DiagOptions, device: int = 0
         ncv = min(max(nblock, neigen + 1), 64, dim)   # device basis limit (ed_gpu.h)
         w, v, _, _ = S.eigh(neigen=neigen, ncv=ncv, maxit=max(nitermax, 10),
                             tol=opt.lanc_tolerance, v0=_start_vector(dim, not real),
-                            vectors=opt.keep_vectors)
+                            vectors=opt.keep_vectors, on_device=opt.device_vectors)
         order = np.argsort(w)
-        w = w[order]
-        v = v[:, order] if v is not None else None
+        if np.any(order != np.arange(len(w))):      # (the device solver returns them ascending)
+            w = w[order]
+            v = v[:, order] if v is not None else None
         return SectorResult(sec.isector, q, dim, w, neigen, v if opt.keep_vectors else None, "arpack")
 
 
@@ -142,6 +163,18 @@ def state_list(results: Iterable[SectorResult], opt: DiagOptions) -> StateList:
                 oldzero = min(oldzero, enemin)
                 sl.energies.append(enemin); sl.sectors.append(r.isector); sl.vectors.append(vec)
     return sl
+
+
+def retain_state_vectors(sl: StateList, results: Iterable[SectorResult]) -> StateList:
+    """Keep only the state list's vectors (ED_DIAG.f90:220-236 stores just
+    those): each kept device vector is cloned out of its sector's (neigen, dim)
+    block and every sector result drops its block, so the HBM held after the
+    diagonalisation is the kept states alone."""
+    vecs = [v.clone() if (v is not None and not isinstance(v, np.ndarray)) else v for v in sl.vectors]
+    for r in results:
+        if r.vectors is not None and not isinstance(r.vectors, np.ndarray):
+            r.vectors = None
+    return StateList(list(sl.energies), list(sl.sectors), vecs)
 
 
 def solve_many(cfg: EDConfig, secs: List[SectorId], opt: DiagOptions, device: int = 0,
@@ -171,7 +204,7 @@ def ed_diag(cfg: EDConfig, opt: Optional[DiagOptions] = None,
     pick = set(sectors) if sectors is not None else None
     todo = [sec for sec in secs if pick is None or sec.isector in pick]
     results = solve_many(cfg, todo, opt, device)
-    return results, state_list(results, opt)
+    return results, retain_state_vectors(state_list(results, opt), results)
 
 
 def eigenvalues_table(results: Iterable[SectorResult]) -> Dict[int, np.ndarray]:

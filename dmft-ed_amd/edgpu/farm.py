@@ -24,7 +24,7 @@ from typing import Callable, Dict, List, Optional, Sequence
 
 import numpy as np
 
-from .diag import DiagOptions, SectorResult, StateList, lanczos_params, state_list
+from .diag import DiagOptions, SectorResult, StateList, lanczos_params, retain_state_vectors, state_list
 from .params import EDConfig
 from .sectors import Sector as SectorId
 from .sectors import diag_sectors
@@ -110,16 +110,17 @@ def farm_diag(cfg: EDConfig, opt: Optional[DiagOptions] = None, *, device: int =
     for k, (q, dim, neigen, ev) in merged.items():
         loc = local.get(k)
         shadows.append(SectorResult(k, q, dim, ev, neigen, loc.vectors if loc is not None else None))
-    states = state_list(shadows, opt)
+    states = retain_state_vectors(state_list(shadows, opt), list(local.values()))
     owners = [owner_of[s] for s in states.sectors]
     tables = {k: v[3] for k, v in merged.items()}
     return FarmResult(states, owners, tables, local, assignment)
 
 
-def broadcast_vector(vec: Optional[np.ndarray], owner: int, dim: int, cplx: bool,
-                     device: Optional[int] = None) -> np.ndarray:
-    """Ship one eigenvector from its owner to every rank (RCCL broadcast on GPU
-    tensors when the backend is nccl; host tensors for gloo)."""
+def broadcast_vector(vec, owner: int, dim: int, cplx: bool, device: Optional[int] = None):
+    """Ship one eigenvector from its owner to every rank.  nccl (RCCL over
+    xGMI): the device tensor is broadcast in place and stays in HBM on every
+    rank (a host array on the owner is uploaded first).  gloo (CPU tests):
+    host tensors, returned as numpy."""
     dist = _dist()
     if dist is None:
         return vec
@@ -130,8 +131,12 @@ def broadcast_vector(vec: Optional[np.ndarray], owner: int, dim: int, cplx: bool
     dev = torch.device("cuda", device if device is not None else torch.cuda.current_device()) if on_gpu \
         else torch.device("cpu")
     if dist.get_rank() == owner:
-        t = torch.from_numpy(np.ascontiguousarray(vec).astype(np.complex128 if cplx else np.float64)).to(dev)
+        if isinstance(vec, np.ndarray):
+            t = torch.from_numpy(np.ascontiguousarray(vec).astype(np.complex128 if cplx else np.float64))
+        else:
+            t = vec
+        t = t.to(device=dev, dtype=dt).contiguous()
     else:
         t = torch.empty(dim, dtype=dt, device=dev)
     dist.broadcast(t, src=owner)
-    return t.cpu().numpy()
+    return t if on_gpu else t.numpy()

@@ -28,7 +28,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import check
-from .diag import StateList
+from .diag import StateList, is_complex_vector
 from .hamiltonian import Sector
 from .params import EDConfig
 from .sectors import c_sector, cdg_sector, setup_pointers
@@ -108,7 +108,10 @@ def _seed(src: Sector, dst: Sector, op: int, terms, vec: np.ndarray, cplx: bool)
     real = not cplx
     dt = torch.float64 if real else torch.complex128
     dev = f"cuda:{src.device}"
-    x = torch.from_numpy(np.ascontiguousarray(vec.astype(np.float64 if real else np.complex128))).to(dev)
+    if isinstance(vec, np.ndarray):
+        x = torch.from_numpy(np.ascontiguousarray(vec.astype(np.float64 if real else np.complex128))).to(dev)
+    else:                                   # state vector kept in HBM by the farm
+        x = vec.to(device=dev, dtype=dt).contiguous()
     y = torch.empty(dst.dim, dtype=dt, device=dev)
     st = torch.cuda.current_stream(x.device)
     L = _lib.load()
@@ -233,7 +236,7 @@ def _run_job(cfg, states, gopt, job, cache, wm, wr, G_m, G_r, record, zeta):
     e_i, vec = states.energies[k], states.vectors[k]
     if vec is None:
         raise ValueError("the Green's function needs the state vectors (keep_vectors=True)")
-    cplx = (not cfg.is_real()) or np.iscomplexobj(vec) or any(np.imag(c) != 0 for _, c in terms)
+    cplx = (not cfg.is_real()) or is_complex_vector(vec) or any(np.imag(c) != 0 for _, c in terms)
     HI, HJ = cache.get(sec, False), cache.get(jsec, True)
     seed, norm2 = _seed(HI, HJ, op, terms, vec, cplx)
     if norm2 == 0.0:
@@ -278,7 +281,7 @@ def _run_jobs_batched(cfg, states, gopt, jobs, todo, device, wm, wr, Gm, Gr, zet
         vec = states.vectors[k]
         if vec is None:
             raise ValueError("the Green's function needs the state vectors (keep_vectors=True)")
-        cplx = (not cfg.is_real()) or np.iscomplexobj(vec) or any(np.imag(c) != 0 for _, c in terms)
+        cplx = (not cfg.is_real()) or is_complex_vector(vec) or any(np.imag(c) != 0 for _, c in terms)
         groups.setdefault((jsec.q1, jsec.q2, cplx), []).append(n)
     contrib = {}
     try:
@@ -399,7 +402,7 @@ def build_gf(cfg: EDConfig, states: StateList, gopt: Optional[GFOptions] = None,
         vecs = list(states.vectors)
         for k, isec in enumerate(states.sectors):
             dim = setup_pointers(cfg)[isec - 1].dim
-            cplx = not cfg.is_real() or (vecs[k] is not None and np.iscomplexobj(vecs[k]))
+            cplx = not cfg.is_real() or is_complex_vector(vecs[k])
             flag = [cplx]
             dist.broadcast_object_list(flag, src=owners[k])
             vecs[k] = broadcast_vector(vecs[k], owners[k], dim, flag[0], device)

@@ -33,6 +33,11 @@ def _tptr(t):
     return ctypes.c_void_p(t.data_ptr())
 
 
+def _aptr(a):
+    """Pointer of a host numpy array or a (contiguous) torch device tensor."""
+    return _ptr(a) if isinstance(a, np.ndarray) else _tptr(a)
+
+
 def _stream_ptr(stream):
     if stream is None:
         return None
@@ -153,16 +158,18 @@ class Sector:
 
     def lanc_eigh(self, nitermax: int = 512, threshold: float = 1e-12, ncheck: int = 10,
                   v0: Optional[np.ndarray] = None, vector: bool = True,
-                  real: Optional[bool] = None):
-        """sp_lanc_eigh: ground-state energy (and Ritz vector) by plain Lanczos."""
+                  real: Optional[bool] = None, on_device: bool = False):
+        """sp_lanc_eigh: ground-state energy (and Ritz vector) by plain Lanczos.
+        on_device: the Ritz vector stays in HBM (a torch tensor on this
+        sector's GPU) instead of being copied to the host."""
         vt, buf = self._vec_arg(v0, real)
         egs = np.zeros(1)
         n = ctypes.c_int32()
         out = None
         if vector:
-            out = np.zeros(self.dim, dtype=np.complex128 if vt else np.float64)
+            out = self._out_array((self.dim,), vt, on_device)
         check(_lib.load().ed_sector_lanc_eigh(self._h, vt, buf, nitermax, threshold, ncheck,
-                                              _ptr(egs), None if out is None else _ptr(out),
+                                              _ptr(egs), None if out is None else _aptr(out),
                                               ctypes.byref(n)), "lanc_eigh")
         return float(egs[0]), out, int(n.value)
 
@@ -186,21 +193,32 @@ class Sector:
         return int(_lib.load().ed_sector_lanc_mode(self._h, vt, path))
 
     def eigh(self, neigen: int = 6, ncv: int = 23, maxit: int = 512, tol: float = 1e-12,
-             v0: Optional[np.ndarray] = None, vectors: bool = True, real: Optional[bool] = None):
+             v0: Optional[np.ndarray] = None, vectors: bool = True, real: Optional[bool] = None,
+             on_device: bool = False):
         """sp_eigh (ARPACK, which="SR") replacement: thick-restart Lanczos with
         the Krylov basis in HBM.  Returns (eigenvalues, vectors (dim, neigen) or
-        None, nconv, number of H·v products)."""
+        None, nconv, number of H·v products).  on_device: the eigenvectors stay
+        in HBM (a (dim, neigen) view of a row-major (neigen, dim) torch tensor,
+        so column i is contiguous) instead of being copied to the host."""
         vt, buf = self._vec_arg(v0, real)
         ev = np.zeros(neigen)
         out = None
         if vectors:
-            out = np.zeros((neigen, self.dim), dtype=np.complex128 if vt else np.float64)
+            out = self._out_array((neigen, self.dim), vt, on_device)
         nconv = ctypes.c_int32()
         nhv = ctypes.c_int32()
         check(_lib.load().ed_sector_eigh(self._h, vt, neigen, ncv, maxit, tol, buf, _ptr(ev),
-                                         None if out is None else _ptr(out), ctypes.byref(nconv),
+                                         None if out is None else _aptr(out), ctypes.byref(nconv),
                                          ctypes.byref(nhv)), "ed_sector_eigh")
         return ev, (out.T if out is not None else None), int(nconv.value), int(nhv.value)
+
+    def _out_array(self, shape, vt, on_device):
+        if not on_device:
+            return np.zeros(shape, dtype=np.complex128 if vt else np.float64)
+        import torch
+
+        return torch.empty(shape, dtype=torch.complex128 if vt else torch.float64,
+                           device=torch.device("cuda", self.device))
 
     def _vec_arg(self, v0, real):
         use_real = self.real if real is None else real

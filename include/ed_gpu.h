@@ -183,7 +183,8 @@ int ed_sector_sell_view(const ed_sector* s, ed_sell_view* view);
 int ed_sector_lanc_tridiag(ed_sector* s, int32_t vtype, const void* v0, int32_t nitermax,
                            double threshold, double* alfa, double* beta, int32_t* nlanc);
 /* Ground state: returns egs (lowest Ritz value) and, if vect != NULL, the
- * normalised Ritz vector (host, vtype).  ncheck as lanczos_plain_c. */
+ * normalised Ritz vector (host or device pointer, vtype).  ncheck as
+ * lanczos_plain_c. */
 int ed_sector_lanc_eigh(ed_sector* s, int32_t vtype, const void* v0, int32_t nitermax,
                         double threshold, int32_t ncheck, double* egs, void* vect,
                         int32_t* nlanc);
@@ -197,7 +198,8 @@ int ed_sector_lanc_mode(ed_sector* s, int32_t vtype, int32_t path);
  * device replacement of SciFortran's ARPACK sp_eigh (ED_DIAG.f90:145-167,
  * which="SR", Nblock=ncv, Nitermax=maxit restarts, tol as ARPACK:
  * |r_i| <= tol*max(eps^(2/3),|theta_i|)).  v0: host start vector or NULL.
- * evals[nev] ascending; evecs (host, dim x nev column-major, vtype) or NULL.
+ * evals[nev] ascending; evecs (host or device pointer, dim x nev
+ * column-major, vtype) or NULL.
  * nconv: converged pairs; nhv: H·v products used.  ncv <= 64. */
 int ed_sector_eigh(ed_sector* s, int32_t vtype, int32_t nev, int32_t ncv, int32_t maxit, double tol,
                    const void* v0, double* evals, void* evecs, int32_t* nconv, int32_t* nhv);

@@ -4,6 +4,7 @@ target H%map), tridiagonalisation by the oracle's lanczos_plain_tridiag_c,
 poles as add_to_lanczos_gf_normal (:580-632)."""
 import numpy as np
 
+from edgpu.diag import to_host
 from edgpu.gf import matsubara, realaxis
 from edgpu.sectors import c_sector, cdg_sector, setup_pointers
 from oracle.oracle import Oracle, lanc_tridiag
@@ -55,7 +56,7 @@ def build_gf_normal_oracle(cfg, states, gopt):
     for ispin in range(Nsp):
         for iorb in range(No):
             isite = iorb + ispin * Ns
-            for e_i, isec, vec in zip(states.energies, states.sectors, states.vectors):
+            for e_i, isec, vec in zip(states.energies, states.sectors, map(to_host, states.vectors)):
                 sec = secs[isec - 1]
                 hmap_i = orc.build_sector(sec.q1, sec.q2)
                 for op, isign, jsec in ((1, 1, cdg_sector(cfg, sec, ispin)), (0, -1, c_sector(cfg, sec, ispin))):
@@ -105,7 +106,7 @@ def build_gf_oracle(cfg, states, gopt):
     site = lambda o, s: o + s * Ns
 
     def channel(idx, specs):
-        for e_i, isec, vec in zip(states.energies, states.sectors, states.vectors):
+        for e_i, isec, vec in zip(states.energies, states.sectors, map(to_host, states.vectors)):
             sec = secs[isec - 1]
             hmap_i = orc.build_sector(sec.q1, sec.q2)
             for op, isign, ispin, terms, weight in specs:
@@ -159,7 +160,7 @@ def oracle_job_runner(cfg, states, gopt, job, wm, wr, G_m, G_r, zeta):
     comp, tag, k, (op, isign, ispin, terms, weight), sec, jsec = job
     orc = Oracle(cfg)
     hmap_i = orc.build_sector(sec.q1, sec.q2)
-    hmap_j, v = seed_combo(orc, hmap_i, jsec, op, terms, np.asarray(states.vectors[k]).astype(np.complex128))
+    hmap_j, v = seed_combo(orc, hmap_i, jsec, op, terms, np.asarray(to_host(states.vectors[k])).astype(np.complex128))
     norm2 = float(np.vdot(v, v).real)
     if norm2 == 0.0:
         return

@@ -3,7 +3,7 @@ the oracle-backed CPU pipeline (same algorithms, oracle pieces)."""
 import numpy as np
 import pytest
 
-from edgpu.diag import DiagOptions, ed_diag
+from edgpu.diag import DiagOptions, ed_diag, to_host
 from edgpu.farm import farm_diag
 from edgpu.params import make_config
 from oracle_solver import solve_sector_oracle
@@ -27,7 +27,7 @@ def test_ed_diag_matches_oracle(cfg_kw, method):
     np.testing.assert_allclose(sl.energies, ref.energies, rtol=1e-10, atol=1e-10)
     for v, r in zip(sl.vectors, ref.vectors):       # same eigenvector up to a phase
         if v is not None and len(sl.vectors) == 1:
-            assert abs(abs(np.vdot(v, r)) - 1.0) < 1e-8
+            assert abs(abs(np.vdot(to_host(v), r)) - 1.0) < 1e-8
 
 
 def test_gf_normal_matches_oracle():
