@@ -75,13 +75,21 @@ def time_kernel(fn, iters, stream):
     return e0.elapsed_time(e1) / iters
 
 
-def measure_hxv(Sector, cfg, q, iters, path=0, warm=5, info=None):
+def spmv_bytes_packed_complex(padded, dim):
+    """Bytes of k_spmv_pk on complex(8) H and vectors: 4-B words per slot,
+    slice pointers, complex(8) diagonal, read v, write Hv (16 B each)."""
+    nslice = (dim + 63) // 64
+    return 4 * padded + 8 * (nslice + 1) + 16 * dim + 32 * dim
+
+
+def measure_hxv(Sector, cfg, q, iters, path=0, warm=5, info=None, cplx=False):
     stored = path == 0
-    with Sector(cfg, q[0], q[1], stored=stored, direct=not stored, real=True) as S:
+    with Sector(cfg, q[0], q[1], stored=stored, direct=not stored, real=not cplx) as S:
         dim, nnz = S.dim, S.nnz
         if info is not None:
             info.update(packed=int(S.info.packed), padded=int(S.info.padded), npdict=int(S.info.npdict))
-        x = torch.sin(torch.arange(1, dim + 1, dtype=torch.float64, device="cuda")).contiguous()
+        i = torch.arange(1, dim + 1, dtype=torch.float64, device="cuda")
+        x = (torch.complex(torch.sin(i), torch.cos(3 * i)) if cplx else torch.sin(i)).contiguous()
         y = torch.empty_like(x)
         st = torch.cuda.current_stream()
         for _ in range(warm):
@@ -403,8 +411,32 @@ def main():
                     "achieved_gbs": round(Bk / (msk * 1e-3) / 1e9, 1),
                     "frac": round(Bk / (msk * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                     "traffic": tk, "traffic_source": tksrc,
-                    "basis": "SURVEY §8(d) direct: 16*dim real (read v, write Hv)",
+                    "physical_gbs": round(tk / (msk * 1e-3) / 1e9, 1) if tk else None,
+                    "two_pass_bytes": 40 * dimk,
+                    "two_pass_gbs": round(40 * dimk / (msk * 1e-3) / 1e9, 1),
+                    "basis": "SURVEY §8(d) direct: 16*dim real (read v, write Hv); two_pass_bytes = 40*dim, "
+                             "the least a two-pass form moves (pass U reads V, writes y; pass D reads V and "
+                             "y, writes Hv)",
                     "kernel": "k_kron_up + k_kron_dw (two-pass matrix-free Kronecker H·v)"}
+            # generic matrix-free (any ed_mode) and complex(8) stored H·v on the same sector
+            _, _, msd = measure_hxv(Sector, cfg28, (7, 7), 20, path=1)
+            td, tdsrc = _traffic("direct_n28_traffic.json")
+            kron["direct_generic"] = {"ms_per_hxv": round(msd, 4), "kernel": "k_direct (row regenerated per H·v)",
+                                      "frac_16dim": round(Bk / (msd * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                      "traffic": td, "traffic_source": tdsrc}
+            infc = {}
+            _, _, msc = measure_hxv(Sector, cfg28, (7, 7), 20, path=0, info=infc, cplx=True)
+            Bc = spmv_bytes_packed_complex(infc["padded"], dim28)
+            tc, tcsrc = _traffic("spmv_cplx_n28_traffic.json")
+            roof["complex"] = {"ms_per_launch": round(msc, 4), "bytes_per_launch": Bc,
+                               "achieved": round(Bc / (msc * 1e-3) / 1e9, 1),
+                               "frac": round(Bc / (msc * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                               "csr_equivalent_gbs": round((20 * nnz28 + 8 * (dim28 + 1) + 32 * dim28)
+                                                           / (msc * 1e-3) / 1e9, 1),
+                               "traffic": tc, "traffic_source": tcsrc,
+                               "kernel": f"k_spmv_pk<complex> ({infc['npdict']}-value dictionary of (re, im) "
+                                         "pairs; the reference's complex(8) arithmetic)",
+                               "achieved_basis": "4*padded + 8*(nslice+1) + 16*dim (diagonal) + 32*dim (v, Hv)"}
         cpu = None if args.no_cpu else cpu_baseline()
         out = {
             "metric": "Lanczos SpMV GB/s + ground-state iters/s, Ns=16 half-filled sector, 1/2/4/8 GPU",

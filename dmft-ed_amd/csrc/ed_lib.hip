@@ -1856,7 +1856,8 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
   if (nev < 1 || nev >= m) return fail(ED_ERR_ARG, "need 1 <= nev < min(ncv, dim)");
   const bool verify = !getenv("ED_GPU_EIGH_NO_VERIFY") && dim > (int64_t)nev + 2;
   // deflated solves: nev locked columns + mp active ones
-  const int mp = (int)std::min<int64_t>(std::min(m, 20), dim - nev);
+  static const int kmp = getenv("ED_GPU_EIGH_PROBE_NCV") ? atoi(getenv("ED_GPU_EIGH_PROBE_NCV")) : 20;
+  const int mp = (int)std::min<int64_t>(std::min(m, std::max(kmp, 4)), dim - nev);
   const int mcap = verify ? std::max(m, nev + mp) : m;
   const size_t vs = sizeof(V);
   CK(T.alloc((void**)&T.Vb, (size_t)mcap * dim * vs));
@@ -1895,7 +1896,8 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
       // the decision needs only a loose tolerance (a missed eigenvalue lies
       // below ev[nev-1]; Ritz values approach the lowest from above); a
       // found one is then re-solved to the full tolerance
-      const double tprobe = std::max(tol, 1e-7);
+      static const double kprobe = getenv("ED_GPU_EIGH_PROBE_TOL") ? atof(getenv("ED_GPU_EIGH_PROBE_TOL")) : 1e-5;
+      const double tprobe = std::max(tol, kprobe);
       const double cut = ev[nev - 1] - 1e-9 * std::max(1.0, fabs(ev[nev - 1]));
       CK(trlan_core(T, nev, 1, maxit, tprobe, nullptr, 1000 + round, th2, Z2, &c2));
       if (!(c2 == 1 && th2[0] < cut)) break;
