@@ -313,7 +313,10 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
   constexpr bool PG = REG && VC;
   // real vectors keep their own rows of r_k in registers; complex ones
   // re-read them from LDS (register budget of the ELL words)
-  constexpr bool UREG = !VC && (REG || KR);
+  // (MODE 4 at 10 rows per thread reads them from LDS with the gathers: the
+  // software-pipelined gathers need the 20 VGPRs)
+  constexpr bool PIPE = KR && !VC && RPT * E <= 40;  // software-pipelined MODE 4 gathers (spill-free)
+  constexpr bool UREG = !VC && (REG || (KR && (!PIPE || RPT * E < 40)));
   V u[UREG ? RPT : 1];  // own rows of r_k (the LDS vector)
   V p[PG ? 1 : RPT];
   uint32_t rix[RPT];    // Kronecker row index packed (iw << 16) | iu  (DimUp, DimDw < 2^16)
@@ -383,6 +386,50 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
     // ---- w = (H r_k)/b_k - b_k p ; alpha partial
     V w[RPT];
     double ap = 0.0;
+    if constexpr (PIPE) {
+      // MODE 4: software-pipelined gathers — row r+1's 2E LDS reads are in
+      // flight while row r is summed (issued per hop group of 4 and waited
+      // at once, one wave had <= 4 reads outstanding: the LDS latency was
+      // exposed ~20 times per step at 2 waves per SIMD)
+      double gu[E], gd[E], go;
+      auto gather = [&](int r, double* hu, double* hd, double& ho) {
+        const unsigned char* rb = (const unsigned char*)(vl + (PROW(r) - q.iu));  // row iw of V
+#pragma unroll
+        for (int e = 0; e < E; e++) hu[e] = *(const double*)(rb + ucol[e]);
+#pragma unroll
+        for (int e = 0; e < E; e++) hd[e] = *(const double*)((const unsigned char*)vl + dcol[r * E + e]);
+        if constexpr (UREG) ho = u[r];
+        else ho = vl[PROW(r)];
+      };
+      gather(0, gu, gd, go);
+#pragma unroll
+      for (int r = 0; r < RPT; r++) {
+        double nu[E], nd[E], no = 0.0;
+        if (r + 1 < RPT) gather(r + 1, nu, nd, no);
+        const double ur = go;
+        double acc = ur * dgr[r];
+#ifndef ED_P4_NOGATHER  // timing probe: the step without its gathers
+#pragma unroll
+        for (int e = 0; e < E; e++) acc = fma(uval[e], gu[e], acc);
+#pragma unroll
+        for (int e = 0; e < E; e++) acc = fma(dval[r * E + e], gd[e], acc);
+#endif
+        // contracted recurrence (MODE 4 already fuses its gathers; the
+        // Lanczos bar is 1e-10, not bit-exactness): f64 VALU issue is a
+        // large part of the step at 2 waves per SIMD
+        const double x = s * ur;
+        w[r] = fma(s, acc, -(b * p[r]));
+        ap = fma(x, w[r], ap);
+        if (r + 1 < RPT) {
+#pragma unroll
+          for (int e = 0; e < E; e++) {
+            gu[e] = nu[e];
+            gd[e] = nd[e];
+          }
+          go = no;
+        }
+      }
+    } else {
 #pragma unroll
     for (int r = 0; r < RPT; r++) {
       const int i = PROW(r);
@@ -452,18 +499,33 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
       w[r] = sub(scl(s, acc), scl(b, pr));
       ap += redot(x, w[r]);
     }
+    }
     // alpha barrier: every gather of r_k in LDS is done -> r_k's slots may
     // be overwritten by w below
+#ifdef ED_P4_NOALPHA  // timing probe: the step without the alpha reduction (a bare barrier)
+    __syncthreads();
+    const double alpha = ap * 1e-300;
+#else
     const double alpha = pblock_sum<NT, false>(ap, ws);
+#endif
     // ---- w -= alpha v ; beta ; p <- v_k ; publish w (= r_{k+1}) in LDS
     double bp = 0.0;
+    if (basis) {  // uniform: no per-row EXEC masking when no basis is kept
+#pragma unroll
+      for (int r = 0; r < RPT; r++)
+        if (r < q.nvalid) basis[(int64_t)it * dim + PROW(r)] = scl(s, UREG ? u[r] : vl[PROW(r)]);  // column k = v_k
+    }
 #pragma unroll
     for (int r = 0; r < RPT; r++) {
       const int i = PROW(r);
       const V x = scl(s, UREG ? u[r] : vl[i]);
-      w[r] = sub(w[r], scl(alpha, x));
-      bp += redot(w[r], w[r]);
-      if (basis && r < q.nvalid) basis[(int64_t)it * dim + i] = x;  // column k = v_k
+      if constexpr (PIPE) {
+        w[r] = fma(-alpha, x, w[r]);
+        bp = fma(w[r], w[r], bp);
+      } else {
+        w[r] = sub(w[r], scl(alpha, x));
+        bp += redot(w[r], w[r]);
+      }
       if constexpr (PG) {
         Pg[i] = x;
       } else {
@@ -473,7 +535,12 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
       vl[i] = w[r];
     }
     // beta barrier: also publishes r_{k+1}
+#ifdef ED_P4_NOBETA  // timing probe: the step without the beta reduction (a bare barrier)
+    __syncthreads();
+    const double bn = 1.0 + bp * 1e-300;
+#else
     const double bn = sqrt(pblock_sum<NT, false>(bp, ws2));
+#endif
     if (tid == 0) {
       alpha_out[it] = alpha;
       beta_out[it + 1] = bn;
