@@ -437,7 +437,8 @@ def main():
                                "kernel": f"k_spmv_pk<complex> ({infc['npdict']}-value dictionary of (re, im) "
                                          "pairs; the reference's complex(8) arithmetic)",
                                "achieved_basis": "4*padded + 8*(nslice+1) + 16*dim (diagonal) + 32*dim (v, Hv)"}
-        cpu = None if args.no_cpu else cpu_baseline()
+        # the CPU baseline is a rank-0, N=1 measurement (task contract)
+        cpu = None if (args.no_cpu or world > 1) else cpu_baseline()
         out = {
             "metric": "Lanczos SpMV GB/s + ground-state iters/s, Ns=16 half-filled sector, 1/2/4/8 GPU",
             "value": round(value, 1),

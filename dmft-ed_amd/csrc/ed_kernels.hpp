@@ -602,11 +602,34 @@ __device__ __forceinline__ uint32_t dict_hash(unsigned long long k) {
 
 // Insert every value's bit pattern; plain reads first so that the few
 // distinct keys cost one CAS each, not one per slot.
+// Wave-level deduplication before the table: the lanes of a wavefront read 64
+// consecutive SELL slots, which hold only a few distinct values (hoppings);
+// one leader per distinct key goes to the table.  Without it every slot did a
+// read (and the first ones a CAS) of the same few table lines: all of the
+// device's requests on one L2 channel (N28: 1.05 ms; c4 farm: 0.75 ms per
+// sector, 0.125 s of the serial configs[3] farm).
+__device__ __forceinline__ bool wave_key_leader(unsigned long long key) {
+  const int lane = threadIdx.x & 63;
+  unsigned long long pending = __ballot(1);
+  bool lead = false;
+  while (pending) {
+    const int l = __ffsll((long long)pending) - 1;
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)key, l);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(key >> 32), l);
+    const unsigned long long kl = ((unsigned long long)hi << 32) | lo;
+    const unsigned long long same = __ballot(key == kl);
+    lead |= lane == l;
+    pending &= ~same;
+  }
+  return lead;
+}
+
 __global__ void __launch_bounds__(kBlock) k_dict_insert(const double* __restrict__ vals, int64_t n,
                                                         unsigned long long* table,
                                                         unsigned int* overflow) {
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
     const unsigned long long key = (unsigned long long)__double_as_longlong(vals[i]);
+    if (!wave_key_leader(key)) continue;
     if (key == kDictEmpty) {
       atomicOr(overflow, 1u);
       continue;
@@ -660,6 +683,7 @@ __global__ void __launch_bounds__(kBlock) k_dict_insert_c(const double2* __restr
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
     const double2 v = vals[i];
     const unsigned long long key = pair_key(v);
+    if (!wave_key_leader(key)) continue;  // (pairs with equal keys are checked at pack time)
     uint32_t h = dict_hash(key);
     bool done = false;
     for (int probe = 0; probe < kDictTable && !done; probe++) {

@@ -1639,7 +1639,10 @@ struct Trlan {
   int G = 1, m = 0;
   bool fused = true;  // ED_GPU_TRLAN_UNFUSED=1: the four-sweep CGS2 (A/B)
   V *Vb = nullptr, *Xb = nullptr, *w = nullptr;
-  double2 *h = nullptr, *coef = nullptr, *part = nullptr;
+  double2 *h = nullptr, *coef = nullptr, *part = nullptr, *part2 = nullptr;
+  // grids up to this fold the coefficient reduction into the next CGS pass
+  // (every block re-reads G x ncol partials; ED_GPU_TRLAN_NOFOLD=1: A/B)
+  const int kFinFoldG = getenv("ED_GPU_TRLAN_NOFOLD") ? 0 : 128;
   double *Y = nullptr, *npart = nullptr, *alpha = nullptr, *beta = nullptr;
   std::vector<void*> mine;
   std::vector<std::pair<int, hipGraphExec_t>> graphs;
@@ -1657,10 +1660,12 @@ struct Trlan {
   // x -= V[:, :ncol] V[:, :ncol]^H x, twice; coef = summed coefficients;
   // with jn >= 0: alpha[jn], beta[jn] = ||x|| afterwards
   // one fused sweep (k_cgs) with the column group rounded up to 8/16/24/32
-  bool cgs(int ncol, const double2* hin, V* x, double2* pt, double* np) {
+  bool cgs(int ncol, const double2* hin, V* x, double2* pt, double* np, const double2* pin = nullptr,
+           int add = 0) {
     const int nc = (ncol + 7) / 8 * 8;
 #define ED_CGS(NCV) \
-  hipLaunchKernelGGL((k_cgs<VC, NCV>), dim3(G), dim3(kBlock), 0, st, Vb, ncol, hin, x, dim, pt, np)
+  hipLaunchKernelGGL((k_cgs<VC, NCV>), dim3(G), dim3(kBlock), 0, st, Vb, ncol, hin, x, dim, pt, np, pin, G, \
+                     coef, add)
     if (nc <= 8) ED_CGS(8);
     else if (nc <= 16) ED_CGS(16);
     else if (nc <= 24) ED_CGS(24);
@@ -1672,10 +1677,17 @@ struct Trlan {
   int orth(int ncol, V* x, int jn, V* out = nullptr) {
     // fused CGS2: dots | x -= V h1, dots | x -= V h2, |x|^2  (V streamed 3x)
     if (fused && ncol > 0 && cgs(ncol, nullptr, x, part, nullptr)) {
-      hipLaunchKernelGGL(k_vdot_fin<VC>, dim3(ncol), dim3(kBlock), 0, st, part, G, h, coef, 0);
-      cgs(ncol, h, x, part, nullptr);
-      hipLaunchKernelGGL(k_vdot_fin<VC>, dim3(ncol), dim3(kBlock), 0, st, part, G, h, coef, 1);
-      cgs(ncol, h, x, nullptr, npart);
+      if (G <= kFinFoldG) {
+        // small grids: each pass forms the previous pass's coefficients from
+        // its partials (k_vdot_fin folded in: 5 launches per step, not 7)
+        cgs(ncol, nullptr, x, part2, nullptr, part, 0);
+        cgs(ncol, nullptr, x, nullptr, npart, part2, 1);
+      } else {
+        hipLaunchKernelGGL(k_vdot_fin<VC>, dim3(ncol), dim3(kBlock), 0, st, part, G, h, coef, 0);
+        cgs(ncol, h, x, part, nullptr);
+        hipLaunchKernelGGL(k_vdot_fin<VC>, dim3(ncol), dim3(kBlock), 0, st, part, G, h, coef, 1);
+        cgs(ncol, h, x, nullptr, npart);
+      }
       if (out && jn >= 0)  // + V_{j+1} = x / beta_j in the same launch
         hipLaunchKernelGGL(k_coef_scale<VC>, dim3(G), dim3(kBlock), 0, st, npart, G, coef, jn, alpha, beta,
                            x, out, dim);
@@ -1866,6 +1878,7 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
   CK(T.alloc((void**)&T.h, 64 * sizeof(double2)));
   CK(T.alloc((void**)&T.coef, 64 * sizeof(double2)));
   CK(T.alloc((void**)&T.part, (size_t)64 * T.G * sizeof(double2)));
+  CK(T.alloc((void**)&T.part2, (size_t)64 * T.G * sizeof(double2)));
   CK(T.alloc((void**)&T.npart, (size_t)T.G * sizeof(double)));
   CK(T.alloc((void**)&T.alpha, 72 * sizeof(double)));
   CK(T.alloc((void**)&T.beta, 72 * sizeof(double)));

@@ -191,15 +191,38 @@ template <bool VC, int NC>
 __global__ void __launch_bounds__(kBlock) k_cgs(const val_t<VC>* __restrict__ V, int ncol,
                                                 const double2* __restrict__ hin,
                                                 val_t<VC>* __restrict__ x, int64_t dim,
-                                                double2* __restrict__ part, double* __restrict__ npart) {
+                                                double2* __restrict__ part, double* __restrict__ npart,
+                                                const double2* __restrict__ pin = nullptr, int gin = 0,
+                                                double2* __restrict__ coef = nullptr, int add = 0) {
   constexpr int NW = kBlock / 64;
   constexpr int NR = (VC ? 2 * NC : NC) + 1;  // partial slots per wave
   __shared__ double2 hs[NC];
   __shared__ double red[NW][NR];
-  if (hin) {
+  if (pin) {
+    // the previous pass's coefficients from its block partials (k_vdot_fin
+    // folded in: small sectors, gin x ncol partials): every block forms the
+    // same sums in the same order (wave c mod NW, lanes strided, DPP sum);
+    // block 0 also records them (coef = h, or coef += h)
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int c = wv; c < ncol; c += NW) {  // wave-uniform
+      double re = 0.0, im = 0.0;
+      for (int b = lane; b < gin; b += 64) {
+        re += pin[(int64_t)c * gin + b].x;
+        if constexpr (VC) im += pin[(int64_t)c * gin + b].y;
+      }
+      re = wave_sum_dpp(re);
+      if constexpr (VC) im = wave_sum_dpp(im);
+      if (lane == 63) {
+        hs[c] = make_double2(re, im);
+        if (coef && blockIdx.x == 0) coef[c] = add ? make_double2(coef[c].x + re, coef[c].y + im) : make_double2(re, im);
+      }
+    }
+    __syncthreads();
+  } else if (hin) {
     for (int c = threadIdx.x; c < ncol; c += kBlock) hs[c] = hin[c];
     __syncthreads();
   }
+  const bool upd = hin || pin;
   double are[NC], aim[VC ? NC : 1];
 #pragma unroll
   for (int c = 0; c < NC; c++) {
@@ -212,7 +235,7 @@ __global__ void __launch_bounds__(kBlock) k_cgs(const val_t<VC>* __restrict__ V,
 #pragma unroll
     for (int c = 0; c < NC; c++) v[c] = c < ncol ? V[(int64_t)c * dim + i] : vzero<val_t<VC>>();
     auto xi = x[i];
-    if (hin) {
+    if (upd) {
 #pragma unroll
       for (int c = 0; c < NC; c++) {
         if (c >= ncol) continue;  // uniform
