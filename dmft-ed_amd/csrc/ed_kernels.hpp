@@ -1082,7 +1082,9 @@ __global__ void __launch_bounds__(kKronUpBlock) k_kron_up(KronArgs<HC> K, const 
   }
 }
 
-// dwo[iw*DEG + k] = element offset iw'*dimup of the k-th down-hop target row,
+// dwo[iw*DEG + k] = row index iw' of the k-th down-hop target row (its
+// element offset is iw' * ld: ld = DimUp for the whole sector, nu for the
+// DimDw x nu column strip of the within-sector split),
 // dwi[iw*DEG + k] = its value's dictionary index (DEG slots per row, padded):
 // one wave-uniform row is one s_load_dwordx8/x16 + one of the index bytes
 template <bool HC, bool VC, int DEG, class Epi>
@@ -1090,7 +1092,7 @@ __global__ void __launch_bounds__(kBlock) k_kron_dw(KronArgs<HC> K, const uint32
                                                     const uint8_t* __restrict__ dwi,
                                                     const val_t<HC>* __restrict__ dwdict, int ndict,
                                                     const val_t<VC>* __restrict__ x, const val_t<VC>* ypart,
-                                                    Epi epi) {
+                                                    Epi epi, int ld, int ncols) {
   using V = val_t<VC>;
   using H = val_t<HC>;
   if (epi.skip()) return;
@@ -1103,9 +1105,12 @@ __global__ void __launch_bounds__(kBlock) k_kron_dw(KronArgs<HC> K, const uint32
   // SALU-bound (29 M scalar instructions per launch at N28)
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int du = (int)K.dimup, dd = (int)K.dimdw;
+  // rows of length ld, columns [0, ncols): the whole DimDw x DimUp view
+  // (ld = ncols = DimUp) or a column strip; ypart == nullptr: no first-pass
+  // part (the strip's down-hop sum alone)
+  const int du = ld, dd = (int)K.dimdw;
   const int degdw = K.degdw;
-  const int nchunk = (du + 63) >> 6;
+  const int nchunk = (ncols + 63) >> 6;
   constexpr int R = kKronRowsPerWave;
   constexpr int kTileRows = (kBlock / 64) * R;
   const int nrb = (dd + kTileRows - 1) / kTileRows;
@@ -1122,7 +1127,7 @@ __global__ void __launch_bounds__(kBlock) k_kron_dw(KronArgs<HC> K, const uint32
   double part = 0.0;
   for (; m < mine;) {
     const int iu = (xcd + 8 * m) * 64 + lane;
-    const bool ok = iu < du;
+    const bool ok = iu < ncols;
     const int r0 = rb * kTileRows + wv * R;  // wave-uniform
     // every load of the wave's R rows in flight before any use
     uint32_t wo[R][DEG];
@@ -1132,7 +1137,7 @@ __global__ void __launch_bounds__(kBlock) k_kron_dw(KronArgs<HC> K, const uint32
       const int rr = r0 + r < dd ? r0 + r : r0;
 #pragma unroll
       for (int k = 0; k < DEG; k++) {
-        wo[r][k] = dwo[rr * DEG + k];
+        wo[r][k] = dwo[rr * DEG + k] * (uint32_t)du;
         wi[r][k] = dwi[rr * DEG + k];
       }
     }
@@ -1148,7 +1153,7 @@ __global__ void __launch_bounds__(kBlock) k_kron_dw(KronArgs<HC> K, const uint32
       // y is read once: keep it from evicting the XCD's V chunk from L2
       yv[r] = on ? ldh<1>(ypart + i) : vzero<V>();
 #else
-      yv[r] = on ? ypart[i] : vzero<V>();
+      yv[r] = (on && ypart) ? ypart[i] : vzero<V>();
 #endif
     }
 #pragma unroll

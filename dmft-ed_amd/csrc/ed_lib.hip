@@ -498,14 +498,14 @@ static int build_kron_words(ed_sector* s, int sp, const std::vector<int32_t>& co
   if (sp == 0) {
     CK(upload(s, &K.upw, words));
   } else {
-    // pass D layout: [row][DEG slot] target offsets (row * dimup) and indices
-    const int64_t du = K.dimup;
+    // pass D layout: [row][DEG slot] target rows (the kernel scales them by
+    // its row length) and value indices
     std::vector<uint32_t> off((size_t)nr * K.degD, 0u);
     std::vector<uint8_t> ix((size_t)nr * K.degD, 0);
     for (int64_t r = 0; r < nr; r++)
       for (int k = 0; k < deg; k++) {
         const uint32_t wd = words[(size_t)k * nr + r];
-        off[(size_t)r * K.degD + k] = (uint32_t)((wd & 0xffffu) * du);
+        off[(size_t)r * K.degD + k] = wd & 0xffffu;
         ix[(size_t)r * K.degD + k] = (uint8_t)(wd >> 16);
       }
     CK(upload(s, &K.dwo, off));
@@ -673,7 +673,7 @@ static int hxv_blocks(const ed_sector* s, int path, int vc = 0) {
 }
 
 template <bool HC, bool VC, int CPT, int DEGU, int RU>
-static int launch_kron_up_t(ed_sector* s, const void* x, void* y, hipStream_t st) {
+static int launch_kron_up_t(ed_sector* s, const void* x, void* y, hipStream_t st, int64_t w0, int64_t nw) {
   using V = val_t<VC>;
   using H = val_t<HC>;
   KronHost& K = s->K;
@@ -694,44 +694,61 @@ static int launch_kron_up_t(ed_sector* s, const void* x, void* y, hipStream_t st
     HIPCK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)fn, kKronUpBlock, lds));
     up_grid = std::max(per, 1) * ncu;
   }
-  hipLaunchKernelGGL(fn, dim3((int)std::min<int64_t>(K.dimdw, up_grid)), dim3(kKronUpBlock), lds, st, kron_args<HC>(s), K.upw,
+  // down rows [w0, w0+nw) (the whole sector, or a rank's row block: x, y
+  // are then that block)
+  KronArgs<HC> ka = kron_args<HC>(s);
+  ka.adw += w0;
+  ka.impd += w0;
+  ka.dimdw = nw;
+  hipLaunchKernelGGL(fn, dim3((int)std::min<int64_t>(nw, up_grid)), dim3(kKronUpBlock), lds, st, ka, K.upw,
                      (const H*)K.updict, K.nupdict, (const V*)x, (V*)y);
   HIPCK(hipGetLastError());
   return ED_OK;
 }
 
 template <bool HC, bool VC, int CPT, int DEGU>
-static int launch_kron_up(ed_sector* s, const void* x, void* y, hipStream_t st) {
-  if (kron_up_rows(HC, VC, s->K.dimup) == 2) return launch_kron_up_t<HC, VC, CPT, DEGU, 2>(s, x, y, st);
-  return launch_kron_up_t<HC, VC, CPT, DEGU, 1>(s, x, y, st);
+static int launch_kron_up(ed_sector* s, const void* x, void* y, hipStream_t st, int64_t w0, int64_t nw) {
+  if (kron_up_rows(HC, VC, s->K.dimup) == 2) return launch_kron_up_t<HC, VC, CPT, DEGU, 2>(s, x, y, st, w0, nw);
+  return launch_kron_up_t<HC, VC, CPT, DEGU, 1>(s, x, y, st, w0, nw);
+}
+
+// pass U over down rows [w0, w0+nw)
+template <bool HC, bool VC>
+static int launch_kron_up_any(ed_sector* s, const void* x, void* y, hipStream_t st, int64_t w0, int64_t nw) {
+  switch (s->K.cpt * 100 + s->K.degU) {
+    case 108: return launch_kron_up<HC, VC, 1, 8>(s, x, y, st, w0, nw);
+    case 116: return launch_kron_up<HC, VC, 1, 16>(s, x, y, st, w0, nw);
+    case 208: return launch_kron_up<HC, VC, 2, 8>(s, x, y, st, w0, nw);
+    case 216: return launch_kron_up<HC, VC, 2, 16>(s, x, y, st, w0, nw);
+    case 408: return launch_kron_up<HC, VC, 4, 8>(s, x, y, st, w0, nw);
+    case 416: return launch_kron_up<HC, VC, 4, 16>(s, x, y, st, w0, nw);
+    case 808: return launch_kron_up<HC, VC, 8, 8>(s, x, y, st, w0, nw);
+    default: return fail(ED_ERR_STATE, "kron2: no instantiation for this geometry");
+  }
+}
+
+// pass D with rows of length ld over columns [0, ncols); ypart may be null
+template <bool HC, bool VC, class Epi>
+static int launch_kron_dw(ed_sector* s, const void* x, const void* ypart, Epi epi, hipStream_t st, int ld,
+                          int ncols) {
+  using V = val_t<VC>;
+  using H = val_t<HC>;
+  KronHost& K = s->K;
+  if (K.degD == 8)
+    hipLaunchKernelGGL((k_kron_dw<HC, VC, 8, Epi>), dim3(kKronDwGrid), dim3(kBlock), 0, st, kron_args<HC>(s),
+                       K.dwo, K.dwi, (const H*)K.dwdict, K.ndwdict, (const V*)x, (const V*)ypart, epi, ld, ncols);
+  else
+    hipLaunchKernelGGL((k_kron_dw<HC, VC, 16, Epi>), dim3(kKronDwGrid), dim3(kBlock), 0, st, kron_args<HC>(s),
+                       K.dwo, K.dwi, (const H*)K.dwdict, K.ndwdict, (const V*)x, (const V*)ypart, epi, ld, ncols);
+  HIPCK(hipGetLastError());
+  return ED_OK;
 }
 
 template <bool HC, bool VC, class Epi>
 static int launch_kron2(ed_sector* s, const void* x, Epi epi, hipStream_t st) {
-  using V = val_t<VC>;
-  KronHost& K = s->K;
   void* y = (void*)epi.scratch();
-  int rc;
-  switch (K.cpt * 100 + K.degU) {
-    case 108: rc = launch_kron_up<HC, VC, 1, 8>(s, x, y, st); break;
-    case 116: rc = launch_kron_up<HC, VC, 1, 16>(s, x, y, st); break;
-    case 208: rc = launch_kron_up<HC, VC, 2, 8>(s, x, y, st); break;
-    case 216: rc = launch_kron_up<HC, VC, 2, 16>(s, x, y, st); break;
-    case 408: rc = launch_kron_up<HC, VC, 4, 8>(s, x, y, st); break;
-    case 416: rc = launch_kron_up<HC, VC, 4, 16>(s, x, y, st); break;
-    case 808: rc = launch_kron_up<HC, VC, 8, 8>(s, x, y, st); break;
-    default: return fail(ED_ERR_STATE, "kron2: no instantiation for this geometry");
-  }
-  CK(rc);
-  using H = val_t<HC>;
-  if (K.degD == 8)
-    hipLaunchKernelGGL((k_kron_dw<HC, VC, 8, Epi>), dim3(kKronDwGrid), dim3(kBlock), 0, st, kron_args<HC>(s),
-                       K.dwo, K.dwi, (const H*)K.dwdict, K.ndwdict, (const V*)x, (const V*)y, epi);
-  else
-    hipLaunchKernelGGL((k_kron_dw<HC, VC, 16, Epi>), dim3(kKronDwGrid), dim3(kBlock), 0, st, kron_args<HC>(s),
-                       K.dwo, K.dwi, (const H*)K.dwdict, K.ndwdict, (const V*)x, (const V*)y, epi);
-  HIPCK(hipGetLastError());
-  return ED_OK;
+  CK((launch_kron_up_any<HC, VC>(s, x, y, st, 0, s->K.dimdw)));
+  return launch_kron_dw<HC, VC>(s, x, y, epi, st, (int)s->K.dimup, (int)s->K.dimup);
 }
 
 template <bool HC, bool VC, class Epi>
@@ -1952,6 +1969,14 @@ static int kron_split_launch(ed_sector* s, int part, int64_t o, int64_t n, const
   using V = val_t<VC>;
   const int64_t cnt = n * (part == 0 ? s->K.dimup : s->K.dimdw);
   if (cnt == 0) return ED_OK;
+  // the two-pass kernels serve the split too (pass U on the row block, pass D
+  // on the column strip, ld = nu): same products, same order as
+  // k_kron_rows / k_kron_cols
+  if (kron2_on(s, 2, VC) && !getenv("ED_GPU_SPLIT_SIMPLE")) {
+    if (part == 0) return launch_kron_up_any<HC, VC>(s, x, y, st, o, n);
+    EpiStore<VC> e{(V*)y};
+    return launch_kron_dw<HC, VC>(s, x, acc ? y : nullptr, e, st, (int)n, (int)n);
+  }
   if (part == 0)
     hipLaunchKernelGGL((k_kron_rows<HC, VC>), dim3(grid_for(cnt)), dim3(kBlock), 0, st, kron_args<HC>(s), o, n,
                        (const V*)x, (V*)y);

@@ -67,6 +67,8 @@ def split(n: int, parts: int) -> Tuple[List[int], List[int]]:
 class DeviceKronOps:
     """The two factor products on the GPU (ed_sector_kron_rows / _cols)."""
 
+    accumulates = True   # cols(..., into=y) adds in place
+
     def __init__(self, S):
         self.S = S
         self.dimup = int(S.info.dimup)
@@ -87,13 +89,15 @@ class DeviceKronOps:
         check(_lib.load().ed_sector_kron_rows(self.S.handle, vt, w0, nw, xp, yp, sp), "ed_sector_kron_rows")
         return y
 
-    def cols(self, u0: int, nu: int, xt):
+    def cols(self, u0: int, nu: int, xt, into=None):
+        """Hdw on the strip; into: add to this tensor in place (same layout)."""
         import torch
 
-        yt = torch.empty_like(xt)
+        yt = torch.empty_like(xt) if into is None else into
         xp, yp, sp = self._args(xt, yt)
         vt = 1 if xt.is_complex() else 0
-        check(_lib.load().ed_sector_kron_cols(self.S.handle, vt, u0, nu, xp, yp, 0, sp), "ed_sector_kron_cols")
+        check(_lib.load().ed_sector_kron_cols(self.S.handle, vt, u0, nu, xp, yp, 0 if into is None else 1, sp),
+              "ed_sector_kron_cols")
         return yt
 
 
@@ -216,6 +220,10 @@ class DistKronSector:
         """H·v on the split vector (spMatVec_mpi_cc semantics)."""
         r = self.rank
         y = self.ops.rows(self.w0[r], self.nw[r], x)
+        if self.world == 1 and getattr(self.ops, "accumulates", False):
+            # one rank: the strip is the whole view, so the down-spin sum goes
+            # straight into y (no exchange, no separate add)
+            return self.ops.cols(0, self.du, x, into=y)
         yt = self.ops.cols(self.u0[r], self.nu[r], self.to_cols(x))
         return y + self.to_rows(yt)
 
