@@ -6,12 +6,17 @@ set -eo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/${1:-r2c}
 mkdir -p "$OUT"
-STEPS=${STEPS:-tests,pmc,bench}
+STEPS=${STEPS:-tests,phase,pmc,bench}
 has() { [[ ",$STEPS," == *",$1,"* ]]; }
 if has tests; then
   (cd "$R" && timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread) \
     > "$OUT/gpu_tests.log" 2>&1 || { tail -30 "$OUT/gpu_tests.log"; exit 1; }
   tail -2 "$OUT/gpu_tests.log"
+fi
+if has phase; then
+  (cd "$R" && timeout -k 10 300 python -u tools/farm_phase.py) > "$OUT/farm_phase.log" 2>&1
+  cp "$R/gpurun_out/farm_c4_phases.json" "$OUT/"
+  echo "phase ok"
 fi
 cd /tmp && export TMPDIR=/tmp
 mkdir -p "$R/profiles/r2"
