@@ -275,6 +275,50 @@ def _traffic(name):
     return tj.get("traffic_bytes_per_launch"), f"profiles/r2/{name}"
 
 
+def roofline_sweep(Sector, make_config):
+    """The rest of SURVEY §8(d)'s roofline sweep beside the headline N28 line:
+    the Norb=2 Nbath=6 (7,7) sector (Nlevels=28, Norb=2 hopping structure)
+    and the configs[3] half-filled (6,6) sector (dim 853,776; matrix + vectors
+    ~ the 256 MB Infinity Cache), stored packed real(8) H·v and the two-pass
+    matrix-free H·v; average of 50 launches after 5 warm-ups, HIP events on the
+    launch stream.  `frac` on the bytes each kernel moves; traffic from the
+    committed PMC summaries where present."""
+    from golden.golden_configs import SEED
+
+    out = {}
+    for name, kw, q, tname in (("n28b", dict(Norb=2, Nbath=6), (7, 7), "n28b"),
+                               ("c4_66", None, (6, 6), "c4")):
+        if kw is None:
+            from golden.golden_configs import c4_config
+            cfg = c4_config("random")
+        else:
+            cfg = make_config(bath="random", seed=SEED, **kw)
+        inf = {}
+        dim, nnz, ms = measure_hxv(Sector, cfg, q, 50, path=0, info=inf)
+        Bown = spmv_bytes_packed(inf["padded"], dim) if inf["packed"] else spmv_bytes_real(nnz, dim)
+        tr, tsrc = _traffic(f"spmv_{tname}_traffic.json")
+        row = {"dim": dim, "nnz": nnz, "ms_per_launch": round(ms, 4), "bytes_per_launch": Bown,
+               "achieved": round(Bown / (ms * 1e-3) / 1e9, 1),
+               "frac": round(Bown / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+               "csr_equivalent_gbs": round(spmv_bytes_real(nnz, dim) / (ms * 1e-3) / 1e9, 1),
+               "traffic": tr, "traffic_source": tsrc,
+               "physical_gbs": round(tr / (ms * 1e-3) / 1e9, 1) if tr else None,
+               "kernel": "k_spmv_pk<real>" if inf["packed"] else "k_spmv<real,real>"}
+        _, _, msk = measure_hxv(Sector, cfg, q, 50, path=2)
+        tk, tksrc = _traffic(f"kron_{tname}_traffic.json")
+        two = dim >= (1 << 20)   # the library's two-pass threshold
+        row["matrix_free"] = {"ms_per_hxv": round(msk, 4),
+                              "frac_16dim": round(16 * dim / (msk * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                              "kernel": "k_kron_up + k_kron_dw (two-pass)" if two else "k_kron (one pass)",
+                              "traffic": tk, "traffic_source": tksrc}
+        if two:
+            row["matrix_free"]["two_pass_gbs"] = round(40 * dim / (msk * 1e-3) / 1e9, 1)
+        out[name] = row
+    out["workloads"] = {"n28b": "Norb=2 Nbath=6 (Nlevels=28) (7,7) sector, random bath, real(8)",
+                        "c4_66": "configs[3] Norb=2 Nbath=5 half-filled (6,6) sector, random bath, real(8)"}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -437,6 +481,7 @@ def main():
                                "kernel": f"k_spmv_pk<complex> ({infc['npdict']}-value dictionary of (re, im) "
                                          "pairs; the reference's complex(8) arithmetic)",
                                "achieved_basis": "4*padded + 8*(nslice+1) + 16*dim (diagonal) + 32*dim (v, Hv)"}
+            roof["sweep"] = roofline_sweep(Sector, make_config)
         # the CPU baseline is a rank-0, N=1 measurement (task contract)
         cpu = None if (args.no_cpu or world > 1) else cpu_baseline()
         out = {

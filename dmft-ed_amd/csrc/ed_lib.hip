@@ -341,6 +341,27 @@ static int build_sorder(ed_sector* s) {
       stored_mbytes(s) <= ((int64_t)192 << 20) || !getenv("ED_GPU_SORDER"))
     return ED_OK;
   const int64_t nw = (du + 63) / 64;
+  if (getenv("ED_GPU_SORDER")[0] == '2') {
+    // ED_GPU_SORDER=2: XCD x owns the column windows [x nw / 8, (x+1) nw / 8)
+    // (every down-spin hop stays inside its columns) and sweeps them row by
+    // row (iw outer, window inner: the up-spin hops of a row segment stay hot)
+    std::vector<int64_t> key(ns);
+    std::vector<int32_t> ord(ns);
+    for (int64_t q = 0; q < ns; q++) {
+      const int64_t r = 64 * q, win = (r % du) / 64, x = win * 8 / nw;
+      key[q] = (x << 40) | ((r / du) << 12) | win;
+      ord[q] = (int32_t)q;
+    }
+    std::stable_sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) { return key[a] < key[b]; });
+    CK(upload(s, &s->d_sorder, ord));
+    s->sord_lo[0] = 0;
+    int64_t p = 0;
+    for (int x = 0; x < 8; x++) {
+      while (p < ns && (key[ord[p]] >> 40) <= x) p++;
+      s->sord_lo[x + 1] = (int)p;
+    }
+    return ED_OK;
+  }
   std::vector<int32_t> cnt(nw + 1, 0), ord(ns);
   for (int64_t q = 0; q < ns; q++) cnt[((64 * q) % du) / 64 + 1]++;
   for (int64_t c = 0; c < nw; c++) cnt[c + 1] += cnt[c];

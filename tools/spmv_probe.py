@@ -1,6 +1,6 @@
 """Launch one H·v kernel repeatedly on a chosen sector (for rocprofv3 runs).
 
-usage: python tools/spmv_probe.py [--sector n28|n28b|c4|c2] [--path 0|1|2] [--complex] [--iters N]
+usage: python tools/spmv_probe.py [--sector n28|n28b|c4|c4r|c2] [--path 0|1|2] [--complex] [--iters N]
 Prints the HIP-event average per launch on the launch stream.
 """
 import argparse
@@ -9,6 +9,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "dmft-ed_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
 import torch  # noqa: E402
 
 from edgpu.hamiltonian import Sector  # noqa: E402
@@ -28,8 +29,12 @@ ap.add_argument("--complex", action="store_true", help="complex(8) H values (and
 ap.add_argument("--cvec", action="store_true", help="real H, complex vectors")
 ap.add_argument("--iters", type=int, default=20)
 a = ap.parse_args()
-kw, q = SECTORS[a.sector]
-cfg = make_config(bath="random", seed=20251015, **kw)
+if a.sector == "c4r":   # bench.py's configs[3] parameters (Uloc=(2,2,0), Ust=1, Jh=0.5), (6,6)
+    from golden.golden_configs import c4_config
+    cfg, q = c4_config("random"), (6, 6)
+else:
+    kw, q = SECTORS[a.sector]
+    cfg = make_config(bath="random", seed=20251015, **kw)
 real = not a.complex
 with Sector(cfg, q[0], q[1], stored=(a.path == 0), direct=(a.path != 0), real=real) as S:
     dt = torch.float64 if (real and not a.cvec) else torch.complex128
