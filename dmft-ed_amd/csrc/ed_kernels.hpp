@@ -1109,9 +1109,10 @@ __global__ void __launch_bounds__(kBlock) k_kron_dw(KronArgs<HC> K, const uint32
   // (ld = ncols = DimUp) or a column strip; ypart == nullptr: no first-pass
   // part (the strip's down-hop sum alone)
   const int du = ld, dd = (int)K.dimdw;
-  const int degdw = K.degdw;
   const int nchunk = (ncols + 63) >> 6;
-  constexpr int R = kKronRowsPerWave;
+  // rows per wave: 4 at <= 8 slots; 2 above (the R x DEG gathered values sit
+  // in VGPRs: 4 x 16 doubles held 149 VGPRs, 3 waves/SIMD, scalar spills)
+  constexpr int R = DEG <= 8 ? kKronRowsPerWave : 2;
   constexpr int kTileRows = (kBlock / 64) * R;
   const int nrb = (dd + kTileRows - 1) / kTileRows;
   // blocks are dealt round-robin to the 8 XCDs: XCD x = blockIdx % 8 takes
@@ -1132,12 +1133,15 @@ __global__ void __launch_bounds__(kBlock) k_kron_dw(KronArgs<HC> K, const uint32
     // every load of the wave's R rows in flight before any use
     uint32_t wo[R][DEG];
     uint8_t wi[R][DEG];
+    int nk[R];  // the row's hop count (slot 0's top byte; trailing slots are padding)
 #pragma unroll
     for (int r = 0; r < R; r++) {
       const int rr = r0 + r < dd ? r0 + r : r0;
 #pragma unroll
       for (int k = 0; k < DEG; k++) {
-        wo[r][k] = dwo[rr * DEG + k] * (uint32_t)du;
+        const uint32_t wd = dwo[rr * DEG + k];
+        if (k == 0) nk[r] = r0 + r < dd ? (int)(wd >> 24) : 0;
+        wo[r][k] = (wd & 0xffffffu) * (uint32_t)du;
         wi[r][k] = dwi[rr * DEG + k];
       }
     }
@@ -1147,7 +1151,11 @@ __global__ void __launch_bounds__(kBlock) k_kron_dw(KronArgs<HC> K, const uint32
       const int i = (r0 + r) * du + iu;
       const bool on = ok && r0 + r < dd;
 #pragma unroll
-      for (int k = 0; k < DEG; k++) g[r][k] = (on && k < degdw) ? x[(int)wo[r][k] + iu] : vzero<V>();
+      for (int k = 0; k < DEG; k++) {
+        g[r][k] = vzero<V>();
+        if (k < nk[r])  // wave-uniform: padding slots issue no gather
+          g[r][k] = on ? x[(int)wo[r][k] + iu] : vzero<V>();
+      }
       xv[r] = on ? x[i] : vzero<V>();
 #ifdef ED_KRON_DW_NT
       // y is read once: keep it from evicting the XCD's V chunk from L2
@@ -1162,7 +1170,7 @@ __global__ void __launch_bounds__(kBlock) k_kron_dw(KronArgs<HC> K, const uint32
       V acc = yv[r];
 #pragma unroll
       for (int k = 0; k < DEG; k++)
-        if (k < degdw) acc = add(acc, mul(sdict[wi[r][k]], g[r][k]));
+        if (k < nk[r]) acc = add(acc, mul(sdict[wi[r][k]], g[r][k]));
       part += epi.row((int64_t)((r0 + r) * du + iu), acc, xv[r]);
     }
     rb += g8;

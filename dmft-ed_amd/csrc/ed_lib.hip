@@ -470,8 +470,12 @@ static void spin_diag(const EdModel& M, int sp, uint32_t x, double* re, double* 
 // patterns: exact).  Only for large sectors (dim >= 2^20; the small ones run
 // in the persistent kernels) whose up rows fit the register and LDS budget.
 static constexpr int64_t kKron2MinDim = (int64_t)1 << 20;
+// Slot bound of a template instantiation (8, 12 or 16 hops per row).
+static int kron_slot_bound(int deg) { return deg <= 8 ? 8 : deg <= 12 ? 12 : 16; }
+
 static int build_kron_words(ed_sector* s, int sp, const std::vector<int32_t>& cols,
-                            const std::vector<double>& vals, int64_t nr, int deg) {
+                            const std::vector<double>& vals, int64_t nr, int deg,
+                            const std::vector<uint8_t>& nhop) {
   KronHost& K = s->K;
   if (sp == 0) {
     K.two = false;
@@ -483,14 +487,16 @@ static int build_kron_words(ed_sector* s, int sp, const std::vector<int32_t>& co
     int cpt = 1;
     while (cpt * kKronUpBlock < nr) cpt *= 2;
     K.cpt = cpt;
-    K.degU = deg <= 8 ? 8 : 16;
-    if (cpt * K.degU > 64) return ED_OK;
+    K.degU = kron_slot_bound(deg);
+    // the thread's up-hop words live in VGPRs: cpt x DEG of them (4 x 16 at
+    // DimUp > 2048 spilled to scratch: 3x slower pass U)
+    if (cpt * K.degU > (K.degU == 8 ? 64 : 48)) return ED_OK;
     K.two = true;
   } else {
     if (!K.two) return ED_OK;
     K.two = false;
     if (nr > 65535 || deg > 16) return ED_OK;
-    K.degD = deg <= 8 ? 8 : 16;
+    K.degD = kron_slot_bound(deg);
   }
   const int hw = s->hc ? 2 : 1;
   std::map<std::pair<uint64_t, uint64_t>, uint32_t> idx;
@@ -521,14 +527,19 @@ static int build_kron_words(ed_sector* s, int sp, const std::vector<int32_t>& co
   } else {
     // pass D layout: [row][DEG slot] target rows (the kernel scales them by
     // its row length) and value indices
+    // Slot 0's word also carries the row's hop count in bits 24..31: the
+    // padding slots (own row, zero value) trail the hops, and pass D skips
+    // them with a wave-uniform branch (Norb=2 rows hold 0..12 hops in 12 slots)
     std::vector<uint32_t> off((size_t)nr * K.degD, 0u);
     std::vector<uint8_t> ix((size_t)nr * K.degD, 0);
-    for (int64_t r = 0; r < nr; r++)
+    for (int64_t r = 0; r < nr; r++) {
       for (int k = 0; k < deg; k++) {
         const uint32_t wd = words[(size_t)k * nr + r];
         off[(size_t)r * K.degD + k] = wd & 0xffffu;
         ix[(size_t)r * K.degD + k] = (uint8_t)(wd >> 16);
       }
+      off[(size_t)r * K.degD] |= (uint32_t)nhop[r] << 24;
+    }
     CK(upload(s, &K.dwo, off));
     CK(upload(s, &K.dwi, ix));
   }
@@ -561,6 +572,8 @@ static int build_kron(ed_sector* s) {
       gen_row(M, m, rows[r]);
       deg = std::max<int>(deg, (int)rows[r].tgt.size());
     }
+    std::vector<uint8_t> nhop(nr);
+    for (int64_t r = 0; r < nr; r++) nhop[r] = (uint8_t)rows[r].tgt.size();
     std::vector<int32_t> cols((size_t)deg * nr);
     std::vector<double> vals((size_t)deg * nr * (s->hc ? 2 : 1), 0.0);
     for (int64_t r = 0; r < nr; r++)
@@ -605,7 +618,7 @@ static int build_kron(ed_sector* s) {
     CK(dalloc(s, &da, a.size() * 8));
     CK(dcopy(s, da, a.data(), a.size() * 8, hipMemcpyHostToDevice));
     CK(upload(s, &di, imp));
-    CK(build_kron_words(s, sp, cols, vals, nr, deg));
+    CK(build_kron_words(s, sp, cols, vals, nr, deg, nhop));
     if (sp == 0) {
       K.degup = deg; K.upc = dc; K.upv = dv; K.aup = da; K.impu = di;
     } else {
@@ -729,7 +742,12 @@ static int launch_kron_up_t(ed_sector* s, const void* x, void* y, hipStream_t st
 
 template <bool HC, bool VC, int CPT, int DEGU>
 static int launch_kron_up(ed_sector* s, const void* x, void* y, hipStream_t st, int64_t w0, int64_t nw) {
-  if (kron_up_rows(HC, VC, s->K.dimup) == 2) return launch_kron_up_t<HC, VC, CPT, DEGU, 2>(s, x, y, st, w0, nw);
+  // two staged rows per step when LDS allows, except at 4 columns x > 8 slots
+  // per thread, where the second row's registers spill (n28b pass U: 97 us
+  // with 2 rows, 67 us with 1); ED_KRON_UP_RU=1 forces one row (A/B knob)
+  static const bool one_row = getenv("ED_KRON_UP_RU") && getenv("ED_KRON_UP_RU")[0] == '1';
+  if (!one_row && !(CPT >= 4 && DEGU > 8) && kron_up_rows(HC, VC, s->K.dimup) == 2)
+    return launch_kron_up_t<HC, VC, CPT, DEGU, 2>(s, x, y, st, w0, nw);
   return launch_kron_up_t<HC, VC, CPT, DEGU, 1>(s, x, y, st, w0, nw);
 }
 
@@ -740,9 +758,11 @@ static int launch_kron_up_any(ed_sector* s, const void* x, void* y, hipStream_t 
     case 108: return launch_kron_up<HC, VC, 1, 8>(s, x, y, st, w0, nw);
     case 116: return launch_kron_up<HC, VC, 1, 16>(s, x, y, st, w0, nw);
     case 208: return launch_kron_up<HC, VC, 2, 8>(s, x, y, st, w0, nw);
+    case 112: return launch_kron_up<HC, VC, 1, 12>(s, x, y, st, w0, nw);
+    case 212: return launch_kron_up<HC, VC, 2, 12>(s, x, y, st, w0, nw);
     case 216: return launch_kron_up<HC, VC, 2, 16>(s, x, y, st, w0, nw);
     case 408: return launch_kron_up<HC, VC, 4, 8>(s, x, y, st, w0, nw);
-    case 416: return launch_kron_up<HC, VC, 4, 16>(s, x, y, st, w0, nw);
+    case 412: return launch_kron_up<HC, VC, 4, 12>(s, x, y, st, w0, nw);
     case 808: return launch_kron_up<HC, VC, 8, 8>(s, x, y, st, w0, nw);
     default: return fail(ED_ERR_STATE, "kron2: no instantiation for this geometry");
   }
@@ -757,6 +777,9 @@ static int launch_kron_dw(ed_sector* s, const void* x, const void* ypart, Epi ep
   KronHost& K = s->K;
   if (K.degD == 8)
     hipLaunchKernelGGL((k_kron_dw<HC, VC, 8, Epi>), dim3(kKronDwGrid), dim3(kBlock), 0, st, kron_args<HC>(s),
+                       K.dwo, K.dwi, (const H*)K.dwdict, K.ndwdict, (const V*)x, (const V*)ypart, epi, ld, ncols);
+  else if (K.degD == 12)
+    hipLaunchKernelGGL((k_kron_dw<HC, VC, 12, Epi>), dim3(kKronDwGrid), dim3(kBlock), 0, st, kron_args<HC>(s),
                        K.dwo, K.dwi, (const H*)K.dwdict, K.ndwdict, (const V*)x, (const V*)ypart, epi, ld, ncols);
   else
     hipLaunchKernelGGL((k_kron_dw<HC, VC, 16, Epi>), dim3(kKronDwGrid), dim3(kBlock), 0, st, kron_args<HC>(s),
