@@ -467,9 +467,11 @@ static void spin_diag(const EdModel& M, int sp, uint32_t x, double* re, double* 
 
 // Two-pass Kronecker tables (k_kron_up): the up-hop ELL slots as 32-bit words
 // {column:16 | index:8} over a dictionary of the distinct values (bit
-// patterns: exact).  Only for large sectors (dim >= 2^20; the small ones run
+// patterns: exact).  Only for large sectors (dim >= 2^19; the small ones run
 // in the persistent kernels) whose up rows fit the register and LDS budget.
-static constexpr int64_t kKron2MinDim = (int64_t)1 << 20;
+// crossover with the one-pass k_kron on configs[3] sectors: dim 392,040 0.0108
+// vs 0.0111 ms, 627,264 0.0223 vs 0.0155 ms (tools/kron2_threshold.py)
+static constexpr int64_t kKron2MinDim = (int64_t)1 << 19;
 // Slot bound of a template instantiation (8, 12 or 16 hops per row).
 static int kron_slot_bound(int deg) { return deg <= 8 ? 8 : deg <= 12 ? 12 : 16; }
 

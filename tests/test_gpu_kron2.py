@@ -5,7 +5,7 @@ The two-pass form keeps k_kron's term order per element (diagonal, up hops,
 down hops, each in slot order), so its H·v is bit-identical to k_kron's; the
 Lanczos epilogue reduces over a different grid, so alpha/beta agree to
 rounding (1e-12 relative).  ED_GPU_KRON2=1 forces the two-pass form on small
-sectors (by default it serves sectors of dim >= 2^20), =0 disables it.
+sectors (by default it serves sectors of dim >= 2^19), =0 disables it.
 """
 import numpy as np
 import pytest
