@@ -1111,8 +1111,9 @@ __global__ void __launch_bounds__(kBlock) k_kron_dw(KronArgs<HC> K, const uint32
   const int du = ld, dd = (int)K.dimdw;
   const int nchunk = (ncols + 63) >> 6;
   // rows per wave: 4 at <= 8 slots; 2 above (the R x DEG gathered values sit
-  // in VGPRs: 4 x 16 doubles held 149 VGPRs, 3 waves/SIMD, scalar spills)
-  constexpr int R = DEG <= 8 ? kKronRowsPerWave : 2;
+  // in VGPRs: 4 x 16 doubles held 149 VGPRs, 3 waves/SIMD, scalar spills);
+  // half that for complex vectors (4 x 8 complex: 157 VGPRs, 3 waves/SIMD)
+  constexpr int R = VC ? (DEG <= 8 ? 2 : 1) : (DEG <= 8 ? kKronRowsPerWave : 2);
   constexpr int kTileRows = (kBlock / 64) * R;
   const int nrb = (dd + kTileRows - 1) / kTileRows;
   // blocks are dealt round-robin to the 8 XCDs: XCD x = blockIdx % 8 takes

@@ -702,8 +702,16 @@ static SliceOrder slice_order(const ed_sector* s, int path) {
   }
   return so;
 }
+// pass D grid: kKronDwGrid blocks (a multiple of 8: XCD column chunks);
+// ED_KRON_DW_GRID overrides it for A/B runs.  Every per-block reduction of a
+// pass-D epilogue is sized by this (through hxv_blocks).
+static int kron_dw_grid(bool vc) {
+  (void)vc;
+  static const int env = getenv("ED_KRON_DW_GRID") ? (atoi(getenv("ED_KRON_DW_GRID")) & ~7) : 0;
+  return env > 0 ? env : kKronDwGrid;
+}
 static int hxv_blocks(const ed_sector* s, int path, int vc = 0) {
-  if (kron2_on(s, path, vc)) return kKronDwGrid;
+  if (kron2_on(s, path, vc)) return kron_dw_grid(vc);
   const int g = grid_for(s->nslice * 64);
   return (xcd_on(s, path) || sorder_on(s, path)) ? (g & ~7) : g;
 }
@@ -777,14 +785,15 @@ static int launch_kron_dw(ed_sector* s, const void* x, const void* ypart, Epi ep
   using V = val_t<VC>;
   using H = val_t<HC>;
   KronHost& K = s->K;
+  const int grid = kron_dw_grid(VC);
   if (K.degD == 8)
-    hipLaunchKernelGGL((k_kron_dw<HC, VC, 8, Epi>), dim3(kKronDwGrid), dim3(kBlock), 0, st, kron_args<HC>(s),
+    hipLaunchKernelGGL((k_kron_dw<HC, VC, 8, Epi>), dim3(grid), dim3(kBlock), 0, st, kron_args<HC>(s),
                        K.dwo, K.dwi, (const H*)K.dwdict, K.ndwdict, (const V*)x, (const V*)ypart, epi, ld, ncols);
   else if (K.degD == 12)
-    hipLaunchKernelGGL((k_kron_dw<HC, VC, 12, Epi>), dim3(kKronDwGrid), dim3(kBlock), 0, st, kron_args<HC>(s),
+    hipLaunchKernelGGL((k_kron_dw<HC, VC, 12, Epi>), dim3(grid), dim3(kBlock), 0, st, kron_args<HC>(s),
                        K.dwo, K.dwi, (const H*)K.dwdict, K.ndwdict, (const V*)x, (const V*)ypart, epi, ld, ncols);
   else
-    hipLaunchKernelGGL((k_kron_dw<HC, VC, 16, Epi>), dim3(kKronDwGrid), dim3(kBlock), 0, st, kron_args<HC>(s),
+    hipLaunchKernelGGL((k_kron_dw<HC, VC, 16, Epi>), dim3(grid), dim3(kBlock), 0, st, kron_args<HC>(s),
                        K.dwo, K.dwi, (const H*)K.dwdict, K.ndwdict, (const V*)x, (const V*)ypart, epi, ld, ncols);
   HIPCK(hipGetLastError());
   return ED_OK;
