@@ -42,14 +42,19 @@ def _dist():
 
 
 def sector_cost(cfg: EDConfig, sec: SectorId, opt: DiagOptions) -> float:
-    """Work model: dense sectors ~ dim^3 (LAPACK), Lanczos sectors ~
-    Nitermax x dim x (1 + elements per row); elements/row ~ 1 + 2*Norb*Nbath
-    hops (normal bath) — only the ranking matters for LPT."""
+    """Work model in seconds of one MI355X: a fixed cost per sector (build,
+    launches, host syncs) plus a part proportional to the H·v work.
+    Dense sectors: 2 ms + dim^3 x 1e-10 (LAPACK); Lanczos sectors: 11.2 ms +
+    1.34e-11 x Nitermax x dim x (1 + elements per row), elements/row ~ 1 +
+    Norb*Nbath.  Fitted to the 169 solo sector times of configs[3]
+    (profiles/r2/farm_scale_solo.json): small Lanczos sectors are dominated by
+    the fixed part (dim 256-2,000: 8.8 ms each), which a purely proportional
+    model gave to the ranks holding many of them.  Only ratios matter (LPT)."""
     neigen, nitermax, _ = lanczos_params(sec.dim, opt)
     if neigen == sec.dim or sec.dim <= max(opt.lanc_dim_threshold, opt.mpi_size):
-        return float(sec.dim) ** 3 / 1e3
+        return 2e-3 + float(sec.dim) ** 3 * 1e-10
     per_row = 1.0 + cfg.Norb * cfg.Nbath
-    return float(nitermax) * sec.dim * per_row
+    return 11.2e-3 + 1.336e-11 * float(nitermax) * sec.dim * per_row
 
 
 def lpt_partition(costs: Sequence[float], nranks: int) -> List[List[int]]:

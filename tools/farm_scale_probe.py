@@ -82,6 +82,8 @@ for n in [int(x) for x in args.ranks.split(",")]:
     print(f"N={n}: wall {wall:.4f}s parts {[round(t, 3) for t in times]} speedup {base / wall:.2f}", flush=True)
 
 # largest sectors: cost model vs measured
+res["solo"] = [{"sector": [s.q1, s.q2], "dim": s.dim, "solo_s": round(solo[i], 5), "cost_model": costs[i]}
+               for i, s in enumerate(secs)]
 top = sorted(range(len(secs)), key=lambda i: -solo[i])[:12]
 res["largest"] = [{"sector": [secs[i].q1, secs[i].q2], "dim": secs[i].dim, "solo_s": round(solo[i], 4),
                    "cost_model": costs[i]} for i in top]
