@@ -246,20 +246,16 @@ def bench_split(dist, world, dev, iters=10):
                         "kernels + 2 all_to_all exchanges per H·v (RCCL; strip layout, no transposes)"}
 
 
-def _lanc_rate(S, niter, v0, reps=5, env=None):
-    """Best-of device time of `reps` niter-step runs -> iters/s (and the last α, β)."""
-    old = {k: os.environ.get(k) for k in (env or {})}
-    os.environ.update(env or {})
+def _lanc_rate(S, niter, v0, reps=5, options=()):
+    """Best-of device time of `reps` niter-step runs -> iters/s (and the last α, β),
+    with the sector's kernel options `options` (ED_OPT_* names) during the runs."""
+    S.set_options(*options)
     try:
         for _ in range(2):
             S.lanc_run(niter, v0_dev=v0)
         runs = [S.lanc_run(niter, v0_dev=v0) for _ in range(reps)]
     finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+        S.set_options()
     return niter / (min(r[2] for r in runs) * 1e-3), runs[-1]
 
 
@@ -437,7 +433,7 @@ def main():
 
     # configs[1] with the stored matrix as ELL words in registers (MODE 2, no
     # Kronecker structure), complex(8) arithmetic, and configs[2] matrix-free
-    mode2_ips, _ = _lanc_rate(S, args.niter, v0, env={"ED_GPU_NO_PKRON": "1"})
+    mode2_ips, _ = _lanc_rate(S, args.niter, v0, options=("no_pkron",))
     with Sector(cfg, 4, 4, stored=True, direct=False, real=False, device=dev) as Sc:
         vc = v0.to(torch.complex128)
         cplx_ips, _ = _lanc_rate(Sc, args.niter, vc)

@@ -315,16 +315,7 @@ struct EpiStore {
   __device__ __forceinline__ bool skip() const { return false; }
   __device__ __forceinline__ void prepare() {}
   __device__ __forceinline__ double row(int64_t i, V acc, V) {
-#ifdef ED_EPI_NT_STORE
-    if constexpr (VC) {
-      __builtin_nontemporal_store(acc.x, (double*)(hv + i));
-      __builtin_nontemporal_store(acc.y, (double*)(hv + i) + 1);
-    } else {
-      __builtin_nontemporal_store(acc, hv + i);
-    }
-#else
     hv[i] = acc;
-#endif
     return 0.0;
   }
   __device__ __forceinline__ void finish(double) {}
@@ -513,17 +504,6 @@ template <int NT> __device__ __forceinline__ double2 ldh(const double2* p) { ret
 // +10-14 % over a plain loop on the Nlevels=28 sector), summed in row order.
 constexpr int kChunk = 16;
 
-// Optional XCD-aware slice schedule for stored sectors beyond the Infinity
-// Cache (normal mode): slices sorted by their column window ((64 s) mod dimup
-// / 64), then by down row; XCD x sweeps the contiguous part lo[x] .. lo[x+1]
-// of that list, so at any time its workgroups gather the down-spin entries
-// v[iw'][window] of one window (dimdw x ~128 columns, in the XCD's L2)
-// instead of whole rows from the MALL.  One slice per wavefront.
-struct SliceOrder {
-  const int32_t* ord;  // nullptr: natural order
-  int lo[9];
-};
-
 template <bool HC, bool VC, int NT, class Epi>
 __global__ void __launch_bounds__(kBlock) k_spmv(const val_t<HC>* __restrict__ diag,
                                                  const int64_t* __restrict__ sptr,
@@ -531,7 +511,7 @@ __global__ void __launch_bounds__(kBlock) k_spmv(const val_t<HC>* __restrict__ d
                                                  const val_t<HC>* __restrict__ vals,
                                                  const val_t<VC>* __restrict__ x,
                                                  const val_t<VC>* __restrict__ xr, int64_t dim,
-                                                 int64_t nslice, Epi epi, int xcd, SliceOrder so) {
+                                                 int64_t nslice, Epi epi, int xcd) {
   using V = val_t<VC>;
   using H = val_t<HC>;
   if (epi.skip()) return;
@@ -565,14 +545,7 @@ __global__ void __launch_bounds__(kBlock) k_spmv(const val_t<HC>* __restrict__ d
       part += epi.row(i, acc, xi);
     }
   };
-  if (so.ord) {
-    const int x = blockIdx.x & 7, wv = threadIdx.x >> 6;
-    const int step = (gridDim.x >> 3) * (kBlock / 64);
-    for (int p = so.lo[x] + (int)(blockIdx.x >> 3) * (kBlock / 64) + wv; p < so.lo[x + 1]; p += step) {
-      const int64_t i = (int64_t)so.ord[p] * 64 + (threadIdx.x & 63);
-      if (i < dim) body(i);
-    }
-  } else {
+  {
     // one row range per XCD (see k_spmv_pk)
     int64_t b = blockIdx.x;
     if (xcd) b = (b & 7) * (gridDim.x >> 3) + (b >> 3);
@@ -735,7 +708,7 @@ __global__ void __launch_bounds__(kBlock) k_spmv_pk(const val_t<HC>* __restrict_
                                                     const val_t<HC>* __restrict__ dict,
                                                     const val_t<VC>* __restrict__ x,
                                                     const val_t<VC>* __restrict__ xr, int64_t dim,
-                                                    int64_t nslice, Epi epi, int xcd, SliceOrder so) {
+                                                    int64_t nslice, Epi epi, int xcd) {
   using V = val_t<VC>;
   using H = val_t<HC>;
   if (epi.skip()) return;
@@ -774,14 +747,7 @@ __global__ void __launch_bounds__(kBlock) k_spmv_pk(const val_t<HC>* __restrict_
       part += epi.row(i, acc, xi);
     }
   };
-  if (so.ord) {
-    const int x = blockIdx.x & 7, wv = threadIdx.x >> 6;
-    const int step = (gridDim.x >> 3) * (kBlock / 64);
-    for (int p = so.lo[x] + (int)(blockIdx.x >> 3) * (kBlock / 64) + wv; p < so.lo[x + 1]; p += step) {
-      const int64_t i = (int64_t)so.ord[p] * 64 + (threadIdx.x & 63);
-      if (i < dim) body(i);
-    }
-  } else {
+  {
     // xcd: blocks are dealt round-robin to the 8 XCDs; remap so that each XCD
     // sweeps one contiguous range of rows (its L2 then serves the v gathers
     // shared by neighbouring rows)
@@ -914,15 +880,11 @@ __global__ void __launch_bounds__(kBlock) k_kron(KronArgs<HC> K, const val_t<VC>
 // pass U writes into the epilogue's scratch (its output buffer).
 constexpr int kKronUpBlock = 1024;
 constexpr int kKronDictMax = 256;
-#ifndef ED_KRON_DW_R
-#define ED_KRON_DW_R 4
-#endif
-constexpr int kKronRowsPerWave = ED_KRON_DW_R;   // pass D tile: 4 waves x 4 rows x 64 columns
+constexpr int kKronRowsPerWave = 4;   // pass D tile: 4 waves x 4 rows x 64 columns
 constexpr int kKronUimpMax = 64;      // U[imp][imp] table entries (Norb <= 3)
-#ifndef ED_KRON_UP_PF
-#define ED_KRON_UP_PF 1
-#endif
-constexpr int kKronUpPF = ED_KRON_UP_PF;
+// steps of staged rows prefetched in registers (2 and 3 measured slower:
+// register pressure)
+constexpr int kKronUpPF = 1;
 
 template <bool HC, bool VC, int CPT, int DEG, int kKronUpRows>
 __global__ void __launch_bounds__(kKronUpBlock) k_kron_up(KronArgs<HC> K, const uint32_t* __restrict__ upw,
@@ -964,9 +926,7 @@ __global__ void __launch_bounds__(kKronUpBlock) k_kron_up(KronArgs<HC> K, const 
   struct Pair {
     V a, b;
   };
-  // PF steps of rows in flight in registers (ED_KRON_UP_PF, default 2: one
-  // step's 2 rows are 55 KB per CU, too few bytes in flight to cover the
-  // loaded HBM latency at one workgroup per CU)
+  // kKronUpPF steps of rows in flight in registers
   V xr[kKronUpPF][kKronUpRows][CPT];
   int64_t base = blockIdx.x;
 #pragma unroll
@@ -994,14 +954,7 @@ __global__ void __launch_bounds__(kKronUpBlock) k_kron_up(KronArgs<HC> K, const 
     }
   int pb = 0;
   for (; base < dd; base += kKronUpRows * G) {
-
-#ifdef ED_KRON_UP_ONESET
-    // one LDS set (half the LDS: two workgroups per CU), two barriers per step
-    V* buf = bufs;
-    if (base != (int64_t)blockIdx.x) __syncthreads();  // the previous step's reads are done
-#else
     V* buf = bufs + (size_t)pb * kKronUpRows * dup;
-#endif
 #pragma unroll
     for (int j = 0; j < CPT; j++) {
       const int iu = t + kKronUpBlock * j;
@@ -1158,12 +1111,7 @@ __global__ void __launch_bounds__(kBlock) k_kron_dw(KronArgs<HC> K, const uint32
           g[r][k] = on ? x[(int)wo[r][k] + iu] : vzero<V>();
       }
       xv[r] = on ? x[i] : vzero<V>();
-#ifdef ED_KRON_DW_NT
-      // y is read once: keep it from evicting the XCD's V chunk from L2
-      yv[r] = on ? ldh<1>(ypart + i) : vzero<V>();
-#else
       yv[r] = (on && ypart) ? ypart[i] : vzero<V>();
-#endif
     }
 #pragma unroll
     for (int r = 0; r < R; r++) {

@@ -42,7 +42,9 @@ static int fail(int code, const std::string& msg) {
     if (r_ != ED_OK) return r_; \
   } while (0)
 
-static constexpr int kMaxGrid = 65536;  // one thread per row up to 16.7 M rows
+static constexpr int kMaxGrid = 65536;
+// columns of the thick-restart coefficient buffers (ncv + probe columns)
+static constexpr int kTrlanMaxCols = 64;  // one thread per row up to 16.7 M rows
 static inline int grid_for(int64_t nthreads) {
   int64_t b = (nthreads + kBlock - 1) / kBlock;
   return (int)std::max<int64_t>(1, std::min<int64_t>(b, kMaxGrid));
@@ -90,6 +92,7 @@ struct ed_sector {
   EdModel* Md = nullptr;
   SectorTables T;
   int flags = 0;
+  int opts = 0;        // ED_OPT_* kernel alternatives (ed_sector_set_options)
   bool hc = true;      // complex H values
   int64_t dim = 0, nslice = 0;
   // rows of the operator held here: [row0, row0+nrows) of the sector (the
@@ -109,9 +112,6 @@ struct ed_sector {
   uint32_t* d_words = nullptr;
   void* d_pdict = nullptr;   // real(8) or complex(8) values (hc)
   int npdict = 0;
-  // XCD column-window slice schedule (SliceOrder, stored sectors beyond the MALL)
-  int32_t* d_sorder = nullptr;
-  int sord_lo[9] = {0};
   // matrix-free
   bool kron = false;
   KronHost K;
@@ -329,48 +329,6 @@ static int64_t stored_mbytes(const ed_sector* s) {
   return s->padded * (4 + hv) + s->nrows * hv;
 }
 
-// SliceOrder for normal-mode sectors whose matrix exceeds the MALL: slices
-// sorted by column window (64 s mod dimup) / 64, then row; the list is cut
-// into 8 equal contiguous parts, one per XCD.  Opt-in (ED_GPU_SORDER=1): it
-// moves the down-spin gathers into L2 but scatters the up-spin ones (each row
-// iw is then revisited once per window): N28 packed 0.226 -> 0.255 ms real,
-// 0.361 -> 0.405 ms complex.
-static int build_sorder(ed_sector* s) {
-  const int64_t du = s->T.dimup, ns = s->nslice;
-  if (s->Mh.mode != ED_MODE_NORMAL || du < 64 || s->nrows != s->dim || ns >= ((int64_t)1 << 31) ||
-      stored_mbytes(s) <= ((int64_t)192 << 20) || !getenv("ED_GPU_SORDER"))
-    return ED_OK;
-  const int64_t nw = (du + 63) / 64;
-  if (getenv("ED_GPU_SORDER")[0] == '2') {
-    // ED_GPU_SORDER=2: XCD x owns the column windows [x nw / 8, (x+1) nw / 8)
-    // (every down-spin hop stays inside its columns) and sweeps them row by
-    // row (iw outer, window inner: the up-spin hops of a row segment stay hot)
-    std::vector<int64_t> key(ns);
-    std::vector<int32_t> ord(ns);
-    for (int64_t q = 0; q < ns; q++) {
-      const int64_t r = 64 * q, win = (r % du) / 64, x = win * 8 / nw;
-      key[q] = (x << 40) | ((r / du) << 12) | win;
-      ord[q] = (int32_t)q;
-    }
-    std::stable_sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) { return key[a] < key[b]; });
-    CK(upload(s, &s->d_sorder, ord));
-    s->sord_lo[0] = 0;
-    int64_t p = 0;
-    for (int x = 0; x < 8; x++) {
-      while (p < ns && (key[ord[p]] >> 40) <= x) p++;
-      s->sord_lo[x + 1] = (int)p;
-    }
-    return ED_OK;
-  }
-  std::vector<int32_t> cnt(nw + 1, 0), ord(ns);
-  for (int64_t q = 0; q < ns; q++) cnt[((64 * q) % du) / 64 + 1]++;
-  for (int64_t c = 0; c < nw; c++) cnt[c + 1] += cnt[c];
-  for (int64_t q = 0; q < ns; q++) ord[cnt[((64 * q) % du) / 64]++] = (int32_t)q;
-  CK(upload(s, &s->d_sorder, ord));
-  for (int x = 0; x <= 8; x++) s->sord_lo[x] = (int)(ns * x / 8);
-  return ED_OK;
-}
-
 static int build_stored(ed_sector* s) {
   const int64_t dim = s->nrows, ns = s->nslice;  // rows held by this sector object
   const uint32_t* map = s->d_map + s->row0;
@@ -423,8 +381,7 @@ static int build_stored(ed_sector* s) {
   int64_t nnz = dim;
   for (int64_t i = 0; i < dim; i++) nnz += hc[i];
   s->nnz = nnz;
-  if (s->dim <= (int64_t)kPackColMask + 1 && !getenv("ED_GPU_NO_PACK")) CK(build_pack(s));
-  CK(build_sorder(s));
+  if (s->dim <= (int64_t)kPackColMask + 1 && !(s->flags & ED_NO_PACK)) CK(build_pack(s));
   return ED_OK;
 }
 
@@ -481,9 +438,8 @@ static int build_kron_words(ed_sector* s, int sp, const std::vector<int32_t>& co
   KronHost& K = s->K;
   if (sp == 0) {
     K.two = false;
-    const char* env = getenv("ED_GPU_KRON2");
-    if (env && env[0] == '0') return ED_OK;
-    if (s->dim < kKron2MinDim && !(env && env[0] == '1')) return ED_OK;
+    if (s->flags & ED_KRON2_OFF) return ED_OK;
+    if (s->dim < kKron2MinDim && !(s->flags & ED_KRON2_ON)) return ED_OK;
     if (nr > 8192 || deg > 16 || s->dim >= ((int64_t)1 << 31)) return ED_OK;  // 32-bit element offsets
     if (K.nimp * K.nimp > kKronUimpMax) return ED_OK;                          // U table in LDS
     int cpt = 1;
@@ -664,27 +620,16 @@ static int resolve_path(const ed_sector* s, int path) {
 // range, so its L2 serves the v gathers of neighbouring rows): n28 packed
 // 0.240 -> 0.230 ms, c4 0.0193 -> 0.0173 ms.  The grid is then a multiple of
 // 8; every per-block reduction over an H·v launch must use hxv_blocks().
-static int xcd_remap() {
-  static const int on = getenv("ED_GPU_NO_XCD") ? 0 : 1;
-  return on;
-}
 // Only the packed kernel on grids of >= 1024 blocks gains (plain SELL n28:
 // 0.421 -> 0.443 ms with the remap; small grids lose blocks to the rounding).
 static bool xcd_on(const ed_sector* s, int path) {
-  return path == 0 && s->d_words && xcd_remap() && grid_for(s->nslice * 64) >= 1024;
+  return path == 0 && s->d_words && grid_for(s->nslice * 64) >= 1024;
 }
 // pass D of the two-pass Kronecker H·v: a multiple of 8 blocks (XCD column
 // chunks), 8 resident per CU
-#ifndef ED_KRON_DW_GRID
-#define ED_KRON_DW_GRID 2048
-#endif
-static constexpr int kKronDwGrid = ED_KRON_DW_GRID;
+static constexpr int kKronDwGrid = 2048;
 // pass U LDS: dictionary + two sets of `rows` staged rows
-#ifdef ED_KRON_UP_ONESET
-static constexpr int kKronUpSets = 1;
-#else
 static constexpr int kKronUpSets = 2;
-#endif
 static size_t kron_up_lds(bool hc, bool vc, int64_t du, int rows) {
   return kKronDictMax * (hc ? 16 : 8) + kKronUimpMax * 8 + kKronUpSets * rows * (size_t)((du + 1) & ~1) * (vc ? 16 : 8);
 }
@@ -693,29 +638,17 @@ static bool kron2_on(const ed_sector* s, int path, int vc) {
   if (path != 2 || !s->K.two) return false;
   return kron_up_lds(s->hc, vc, s->K.dimup, 1) <= 160 * 1024;
 }
-static bool sorder_on(const ed_sector* s, int path) { return path == 0 && s->d_sorder; }
-static SliceOrder slice_order(const ed_sector* s, int path) {
-  SliceOrder so{};
-  if (sorder_on(s, path)) {
-    so.ord = s->d_sorder;
-    for (int x = 0; x <= 8; x++) so.lo[x] = s->sord_lo[x];
-  }
-  return so;
-}
-// pass D grid: kKronDwGrid blocks (a multiple of 8: XCD column chunks);
-// ED_KRON_DW_GRID overrides it for A/B runs.  Every per-block reduction of a
-// pass-D epilogue is sized by this (through hxv_blocks).
+// pass D grid: kKronDwGrid blocks (a multiple of 8: XCD column chunks).
+// Every per-block reduction of a pass-D epilogue is sized by this (through
+// hxv_blocks).
 // Complex vectors take half the grid: their column chunk V[:, c0:c0+64] is
 // twice the bytes, and fewer chunks in flight keep it in L2 (N28 complex
 // pass D: 512 blocks 187-193 us, 1024 160 us, 2048 167 us; real: 109, 81, 80).
-static int kron_dw_grid(bool vc) {
-  static const int env = getenv("ED_KRON_DW_GRID") ? (atoi(getenv("ED_KRON_DW_GRID")) & ~7) : 0;
-  return env > 0 ? env : (vc ? kKronDwGrid / 2 : kKronDwGrid);
-}
+static int kron_dw_grid(bool vc) { return vc ? kKronDwGrid / 2 : kKronDwGrid; }
 static int hxv_blocks(const ed_sector* s, int path, int vc = 0) {
   if (kron2_on(s, path, vc)) return kron_dw_grid(vc);
   const int g = grid_for(s->nslice * 64);
-  return (xcd_on(s, path) || sorder_on(s, path)) ? (g & ~7) : g;
+  return xcd_on(s, path) ? (g & ~7) : g;
 }
 
 template <bool HC, bool VC, int CPT, int DEGU, int RU>
@@ -756,9 +689,8 @@ template <bool HC, bool VC, int CPT, int DEGU>
 static int launch_kron_up(ed_sector* s, const void* x, void* y, hipStream_t st, int64_t w0, int64_t nw) {
   // two staged rows per step when LDS allows, except at 4 columns x > 8 slots
   // per thread, where the second row's registers spill (n28b pass U: 97 us
-  // with 2 rows, 67 us with 1); ED_KRON_UP_RU=1 forces one row (A/B knob)
-  static const bool one_row = getenv("ED_KRON_UP_RU") && getenv("ED_KRON_UP_RU")[0] == '1';
-  if (!one_row && !(CPT >= 4 && DEGU > 8) && kron_up_rows(HC, VC, s->K.dimup) == 2)
+  // with 2 rows, 67 us with 1)
+  if (!(CPT >= 4 && DEGU > 8) && kron_up_rows(HC, VC, s->K.dimup) == 2)
     return launch_kron_up_t<HC, VC, CPT, DEGU, 2>(s, x, y, st, w0, nw);
   return launch_kron_up_t<HC, VC, CPT, DEGU, 1>(s, x, y, st, w0, nw);
 }
@@ -815,7 +747,6 @@ static int launch_hxv_t(ed_sector* s, int path, const void* x, Epi epi, hipStrea
   const int g = grid_for(ns * 64);
   const int gx = hxv_blocks(s, path, VC);
   const int xr = xcd_on(s, path) ? 1 : 0;
-  const SliceOrder so = slice_order(s, path);
   const V* xo = (const V*)x + s->row0;  // the rows' own entries
   // non-temporal matrix loads once the matrix cannot stay in the 256 MB MALL
   const bool nt = stored_mbytes(s) > ((int64_t)192 << 20);
@@ -823,19 +754,19 @@ static int launch_hxv_t(ed_sector* s, int path, const void* x, Epi epi, hipStrea
     using H = val_t<HC>;
     if (nt)
       hipLaunchKernelGGL((k_spmv_pk<HC, VC, 1, Epi>), dim3(gx), dim3(kBlock), 0, st, (const H*)s->d_diag,
-                         s->d_sptr, s->d_words, (const H*)s->d_pdict, (const V*)x, xo, dim, ns, epi, xr, so);
+                         s->d_sptr, s->d_words, (const H*)s->d_pdict, (const V*)x, xo, dim, ns, epi, xr);
     else
       hipLaunchKernelGGL((k_spmv_pk<HC, VC, 0, Epi>), dim3(gx), dim3(kBlock), 0, st, (const H*)s->d_diag,
-                         s->d_sptr, s->d_words, (const H*)s->d_pdict, (const V*)x, xo, dim, ns, epi, xr, so);
+                         s->d_sptr, s->d_words, (const H*)s->d_pdict, (const V*)x, xo, dim, ns, epi, xr);
   } else if (path == 0) {
     if (nt)
       hipLaunchKernelGGL((k_spmv<HC, VC, 1, Epi>), dim3(gx), dim3(kBlock), 0, st,
                          (const val_t<HC>*)s->d_diag, s->d_sptr, s->d_cols,
-                         (const val_t<HC>*)s->d_vals, (const V*)x, xo, dim, ns, epi, xr, so);
+                         (const val_t<HC>*)s->d_vals, (const V*)x, xo, dim, ns, epi, xr);
     else
       hipLaunchKernelGGL((k_spmv<HC, VC, 0, Epi>), dim3(gx), dim3(kBlock), 0, st,
                          (const val_t<HC>*)s->d_diag, s->d_sptr, s->d_cols,
-                         (const val_t<HC>*)s->d_vals, (const V*)x, xo, dim, ns, epi, xr, so);
+                         (const val_t<HC>*)s->d_vals, (const V*)x, xo, dim, ns, epi, xr);
   } else if (path == 1) {
     DevIndex idx{s->d_off, s->d_rank, s->T.ns, s->T.nst - 1};
     hipLaunchKernelGGL((k_direct<HC, VC, Epi>), dim3(g), dim3(kBlock), 0, st, s->Md, s->d_map + s->row0,
@@ -958,7 +889,7 @@ static int lanc_iter(ed_sector* s, int path, bool basis, hipStream_t st) {
   const bool two1 = g1 > kTicketMaxBlocks, two2 = g2 > kTicketMaxBlocks;
   // single-kernel step: opt-in (measured slower on c2: 13.0 vs 8.9 us/step —
   // the last block's serial sc1 pass over all rows is latency-bound)
-  if (!two1 && getenv("ED_GPU_FUSED_STEP")) {
+  if (!two1 && (s->opts & ED_OPT_FUSED_STEP)) {
     EpiLancFused<VC> f;
     f.st = w.st;
     f.P = (val_t<VC>*)w.P;
@@ -1309,7 +1240,8 @@ static int64_t persist_vrows(const ed_sector* s, int mode) {
 // ELL words per lane that compile without scratch (-Rpass-analysis=kernel-resource-usage)
 constexpr int preg_cap(bool hc, bool vc) { return vc ? (hc ? 80 : 84) : 112; }
 static int persist_mode(ed_sector* s, int vc, int path) {
-  if (getenv("ED_GPU_NO_PERSIST")) return -1;
+  const int o = s->opts;
+  if (o & ED_OPT_NO_PERSIST) return -1;
   const int64_t vs = vc ? 16 : 8;
   // rows per thread beyond which the register-resident p/w arrays spill
   // (-Rpass-analysis: 0-8 B/lane scratch up to 8 real / 5 complex rows)
@@ -1317,18 +1249,18 @@ static int persist_mode(ed_sector* s, int vc, int path) {
   if (s->dim > rpt_max * (int64_t)kPBlock) return -1;
   int64_t lds = ((persist_vrows(s, 0) * vs + 15) & ~(int64_t)15);
   // MODE 4 (Kronecker register layout, real vectors): c2 2.2 us/step
-  if (vc == 0 && !getenv("ED_GPU_NO_PKRON") && !getenv("ED_GPU_NO_PREG") &&
-      ((path == 0 && !getenv("ED_GPU_PERSIST_STORED") && build_pkron_stored(s) > 0) ||
+  if (vc == 0 && !(o & (ED_OPT_NO_PKRON | ED_OPT_NO_PREG)) &&
+      ((path == 0 && !(o & ED_OPT_PERSIST_STORED) && build_pkron_stored(s) > 0) ||
        (path == 2 && build_pkron_direct(s) > 0)) &&
       persist_lds(s, vc, 4) <= kLdsBudget)
     return 4;
   // stored: MODE 2 (ELL entries in registers; c2 4.6 us/step) by default.
   // MODE 0 streams the matrix from L2 through one CU (~40-50 GB/s) and is
   // slower than the graph-captured multi-kernel recurrence (c2: 9.8 vs 8.9
-  // us/step): opt-in only (ED_GPU_PERSIST_STORED), for coverage
+  // us/step): opt-in only (ED_OPT_PERSIST_STORED), for coverage
   if (path == 0) {
-    if (getenv("ED_GPU_PERSIST_STORED")) return lds <= kLdsBudget ? 0 : -1;
-    if (getenv("ED_GPU_NO_PREG")) return -1;
+    if (o & ED_OPT_PERSIST_STORED) return lds <= kLdsBudget ? 0 : -1;
+    if (o & ED_OPT_NO_PREG) return -1;
     // MODE 2: dictionary + v + diagonal in LDS; RPT x W words + RPT x (p, w)
     // in registers (512-thread blocks: 256 VGPRs per lane)
     if (s->dim > 10 * (int64_t)kPRegBlock) return -1;
@@ -1338,7 +1270,7 @@ static int persist_mode(ed_sector* s, int vc, int path) {
     if (persist_lds(s, vc, 2) > kLdsBudget) return -1;
     return 2;
   }
-  if (path == 2 && !getenv("ED_GPU_NO_PREG") && s->dim <= 10 * (int64_t)kPRegBlock) {
+  if (path == 2 && !(o & ED_OPT_NO_PREG) && s->dim <= 10 * (int64_t)kPRegBlock) {
     // MODE 3: ELL words generated in-kernel from the hop tables
     const KronHost& K = s->K;
     const int deg = K.degup + K.degdw;
@@ -1711,12 +1643,12 @@ struct Trlan {
   hipStream_t st = nullptr;
   int64_t dim = 0;
   int G = 1, m = 0;
-  bool fused = true;  // ED_GPU_TRLAN_UNFUSED=1: the four-sweep CGS2 (A/B)
+  bool fused = true;  // false (ED_OPT_TRLAN_UNFUSED): the four-sweep CGS2 (A/B)
   V *Vb = nullptr, *Xb = nullptr, *w = nullptr;
   double2 *h = nullptr, *coef = nullptr, *part = nullptr, *part2 = nullptr;
   // grids up to this fold the coefficient reduction into the next CGS pass
-  // (every block re-reads G x ncol partials; ED_GPU_TRLAN_NOFOLD=1: A/B)
-  const int kFinFoldG = getenv("ED_GPU_TRLAN_NOFOLD") ? 0 : 128;
+  // (every block re-reads G x ncol partials; 0 with ED_OPT_TRLAN_NOFOLD: A/B)
+  int kFinFoldG = 128;
   double *Y = nullptr, *npart = nullptr, *alpha = nullptr, *beta = nullptr;
   std::vector<void*> mine;
   std::vector<std::pair<int, hipGraphExec_t>> graphs;
@@ -1823,12 +1755,8 @@ struct Trlan {
   }
 };
 
-// blocks of the O(dim) Krylov sweeps (ED_GPU_TRLAN_GRID overrides, A/B)
-static int trlan_grid_cap() {
-  const char* e = getenv("ED_GPU_TRLAN_GRID");
-  const int g = e ? atoi(e) : 1024;
-  return std::max(1, std::min(g, 8192));
-}
+// blocks of the O(dim) Krylov sweeps
+static constexpr int kTrlanGridCap = 1024;
 
 // One thick-restart Lanczos solve on the columns [k0, m) of the basis; the
 // columns [0, k0) are locked (deflation: every new vector is orthogonalised
@@ -1925,7 +1853,7 @@ static int trlan_core(Trlan<VC>& T, int k0, int nev, int maxit, double tol, cons
 // eigenvalue of H on their orthogonal complement is computed from a fresh
 // random start (deflated solve); when it lies below the current nev-th value
 // it is a missed eigenvalue and replaces it; repeated until a deflated solve
-// finds nothing lower (ED_GPU_EIGH_NO_VERIFY=1 skips this, A/B).
+// finds nothing lower (ED_OPT_EIGH_NO_VERIFY skips this, A/B).
 template <bool VC>
 static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, const void* v0,
                      double* evals, void* evecs, int32_t* nconv, int32_t* nhv) {
@@ -1935,27 +1863,29 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
   T.path = resolve_path(s, -1);
   T.st = s->stream;
   T.dim = s->dim;
-  T.G = (int)std::min<int64_t>(grid_for(s->dim), trlan_grid_cap());
-  T.fused = !getenv("ED_GPU_TRLAN_UNFUSED");
+  T.G = (int)std::min<int64_t>(grid_for(s->dim), kTrlanGridCap);
+  T.fused = !(s->opts & ED_OPT_TRLAN_UNFUSED);
+  if (s->opts & ED_OPT_TRLAN_NOFOLD) T.kFinFoldG = 0;
   const int64_t dim = s->dim;
   const int m = (int)std::min<int64_t>(ncv, dim);
   if (nev < 1 || nev >= m) return fail(ED_ERR_ARG, "need 1 <= nev < min(ncv, dim)");
-  const bool verify = !getenv("ED_GPU_EIGH_NO_VERIFY") && dim > (int64_t)nev + 2;
-  // deflated solves: nev locked columns + mp active ones
-  static const int kmp = getenv("ED_GPU_EIGH_PROBE_NCV") ? atoi(getenv("ED_GPU_EIGH_PROBE_NCV")) : 20;
-  const int mp = (int)std::min<int64_t>(std::min(m, std::max(kmp, 4)), dim - nev);
+  // deflated solves: nev locked columns + mp active ones, within the 64
+  // columns the coefficient buffers hold (h/coef/part/alpha/beta below)
+  constexpr int kProbeNcv = 20;
+  const int mp = (int)std::min<int64_t>(std::min(std::min(m, kProbeNcv), kTrlanMaxCols - nev), dim - nev);
+  const bool verify = !(s->opts & ED_OPT_EIGH_NO_VERIFY) && dim > (int64_t)nev + 2 && mp >= 3;
   const int mcap = verify ? std::max(m, nev + mp) : m;
   const size_t vs = sizeof(V);
   CK(T.alloc((void**)&T.Vb, (size_t)mcap * dim * vs));
   CK(T.alloc((void**)&T.Xb, (size_t)mcap * dim * vs));
   CK(T.alloc((void**)&T.w, dim * vs));
-  CK(T.alloc((void**)&T.h, 64 * sizeof(double2)));
-  CK(T.alloc((void**)&T.coef, 64 * sizeof(double2)));
-  CK(T.alloc((void**)&T.part, (size_t)64 * T.G * sizeof(double2)));
-  CK(T.alloc((void**)&T.part2, (size_t)64 * T.G * sizeof(double2)));
+  CK(T.alloc((void**)&T.h, kTrlanMaxCols * sizeof(double2)));
+  CK(T.alloc((void**)&T.coef, kTrlanMaxCols * sizeof(double2)));
+  CK(T.alloc((void**)&T.part, (size_t)kTrlanMaxCols * T.G * sizeof(double2)));
+  CK(T.alloc((void**)&T.part2, (size_t)kTrlanMaxCols * T.G * sizeof(double2)));
   CK(T.alloc((void**)&T.npart, (size_t)T.G * sizeof(double)));
-  CK(T.alloc((void**)&T.alpha, 72 * sizeof(double)));
-  CK(T.alloc((void**)&T.beta, 72 * sizeof(double)));
+  CK(T.alloc((void**)&T.alpha, (kTrlanMaxCols + 8) * sizeof(double)));
+  CK(T.alloc((void**)&T.beta, (kTrlanMaxCols + 8) * sizeof(double)));
   CK(T.alloc((void**)&T.Y, (size_t)mcap * mcap * sizeof(double)));
   hipStream_t st = T.st;
   const int g = grid_for(dim);
@@ -1983,8 +1913,8 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
       // the decision needs only a loose tolerance (a missed eigenvalue lies
       // below ev[nev-1]; Ritz values approach the lowest from above); a
       // found one is then re-solved to the full tolerance
-      static const double kprobe = getenv("ED_GPU_EIGH_PROBE_TOL") ? atof(getenv("ED_GPU_EIGH_PROBE_TOL")) : 1e-5;
-      const double tprobe = std::max(tol, kprobe);
+      constexpr double kProbeTol = 1e-5;  // 1e-3 misses copies; 1e-4 and 1e-5 find them
+      const double tprobe = std::max(tol, kProbeTol);
       const double cut = ev[nev - 1] - 1e-9 * std::max(1.0, fabs(ev[nev - 1]));
       CK(trlan_core(T, nev, 1, maxit, tprobe, nullptr, 1000 + round, th2, Z2, &c2));
       if (!(c2 == 1 && th2[0] < cut)) break;
@@ -2029,7 +1959,7 @@ static int kron_split_launch(ed_sector* s, int part, int64_t o, int64_t n, const
   // the two-pass kernels serve the split too (pass U on the row block, pass D
   // on the column strip, ld = nu): same products, same order as
   // k_kron_rows / k_kron_cols
-  if (kron2_on(s, 2, VC) && !getenv("ED_GPU_SPLIT_SIMPLE")) {
+  if (kron2_on(s, 2, VC) && !(s->opts & ED_OPT_SPLIT_SIMPLE)) {
     if (part == 0) return launch_kron_up_any<HC, VC>(s, x, y, st, o, n);
     EpiStore<VC> e{(V*)y};
     return launch_kron_dw<HC, VC>(s, x, acc ? y : nullptr, e, st, (int)n, (int)n);
@@ -2199,6 +2129,14 @@ int ed_sector_create_rows(const ed_params* p, int32_t q1, int32_t q2, int32_t fl
 
 int ed_sector_destroy(ed_sector* s) {
   sector_free(s);
+  return ED_OK;
+}
+
+int ed_sector_set_options(ed_sector* s, int32_t opts) {
+  if (!s) return fail(ED_ERR_ARG, "null");
+  if (opts & ~0x7ff) return fail(ED_ERR_ARG, "unknown ED_OPT_* bits");
+  if (opts != s->opts) drop_graph(s);  // a captured recurrence bakes in the kernel choice
+  s->opts = opts;
   return ED_OK;
 }
 
@@ -2460,7 +2398,7 @@ int ed_sector_lanc_tridiag_batch(ed_sector* s, int32_t vtype, int32_t nseed, con
     be[0] = 0.0;
     if (nlanc) nlanc[k] = n;
   };
-  if (d.pm < 0 || getenv("ED_GPU_NO_BATCH")) {
+  if (d.pm < 0 || (s->opts & ED_OPT_NO_BATCH)) {
     CK(lanc_prepare(s, d.vc, nitermax, false, 0));
     for (int k = 0; k < nseed; k++) {
       CK(lanc_load_start(s, d.vc, (const unsigned char*)v0_dev + (size_t)k * s->dim * vs, true));
@@ -2837,7 +2775,7 @@ int ed_sector_eigh(ed_sector* s, int32_t vtype, int32_t nev, int32_t ncv, int32_
   if (!s || !evals || maxit < 1) return fail(ED_ERR_ARG, "bad args");
   CK(whole_only(s));
   if (vtype == 0 && s->hc) return fail(ED_ERR_ARG, "complex H needs vtype=1");
-  if (ncv > 64) return fail(ED_ERR_ARG, "ncv > 64 not supported");
+  if (ncv > kTrlanMaxCols) return fail(ED_ERR_ARG, "ncv > 64 not supported");
   HIPCK(hipSetDevice(s->device));
   return vtype ? trlan_run<true>(s, nev, ncv, maxit, tol, v0, evals, evecs, nconv, nhv)
                : trlan_run<false>(s, nev, ncv, maxit, tol, v0, evals, evecs, nconv, nhv);

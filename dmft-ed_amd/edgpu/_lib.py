@@ -11,11 +11,15 @@ import sys
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(_PKG_ROOT, "libedgpu.so")
-# experiment hook (tools/): load a variant build of the same library
-if os.environ.get("ED_GPU_LIB_VARIANT"):
-    LIB_PATH = os.path.join(_PKG_ROOT, "libedgpu_" + os.environ["ED_GPU_LIB_VARIANT"] + ".so")
 
 ED_STORED, ED_DIRECT, ED_REAL = 0x1, 0x2, 0x4
+ED_NO_PACK, ED_KRON2_OFF, ED_KRON2_ON = 0x10, 0x20, 0x40
+# kernel alternatives of a built sector (ed_sector_set_options, include/ed_gpu.h)
+OPTIONS = {
+    "no_persist": 0x001, "persist_stored": 0x002, "no_preg": 0x004, "no_pkron": 0x008,
+    "fused_step": 0x010, "split_simple": 0x020, "no_batch": 0x040, "eigh_no_verify": 0x080,
+    "trlan_unfused": 0x100, "trlan_nofold": 0x200, "trlan_multi": 0x400,
+}
 ED_OK = 0
 ERRORS = {1: "ED_ERR_ARG", 2: "ED_ERR_STATE", 3: "ED_ERR_HIP", 4: "ED_ERR_OOM",
           5: "ED_ERR_UNSUPPORTED"}
@@ -27,6 +31,7 @@ SIGNATURES = {
     "ed_sector_create": ([_P, _i32, _i32, _i32, _i32, _P, _P], ctypes.c_int),
     "ed_sector_create_rows": ([_P, _i32, _i32, _i32, _i64, _i64, _i32, _P, _P], ctypes.c_int),
     "ed_sector_destroy": ([_P], ctypes.c_int),
+    "ed_sector_set_options": ([_P, _i32], ctypes.c_int),
     "ed_sector_get_info": ([_P, _P], ctypes.c_int),
     "ed_sector_hxv_dev": ([_P, _i32, _P, _P, _P], ctypes.c_int),
     "ed_sector_hxv_dev_path": ([_P, _i32, _i32, _P, _P, _P], ctypes.c_int),

@@ -42,9 +42,15 @@ class DiagOptions:
     mpi_size: int = 1
     keep_vectors: bool = True
     # Lanczos / thick-restart eigenvectors stay in HBM (torch tensors on the
-    # sector's GPU); only the states the T=0 list keeps are retained, and
-    # nothing crosses PCIe unless a caller asks for host copies (to_host)
+    # sector's GPU) and nothing crosses PCIe unless a caller asks for host
+    # copies: to_host(vec) turns any state vector into a numpy array.  With
+    # device_vectors=False every vector is a host numpy array, as before.
     device_vectors: bool = True
+    # device vectors: after the T=0 state list is formed only its states are
+    # retained and SectorResult.vectors of every sector becomes None (the
+    # farm's HBM budget); retain_all=True keeps every sector's (dim, Neigen)
+    # block in SectorResult.vectors as well
+    retain_all: bool = False
     # sectors solved concurrently on one GPU (host threads, one HIP stream per
     # sector; ctypes releases the GIL): small sectors are launch-latency bound
     workers: int = 8
@@ -165,12 +171,16 @@ def state_list(results: Iterable[SectorResult], opt: DiagOptions) -> StateList:
     return sl
 
 
-def retain_state_vectors(sl: StateList, results: Iterable[SectorResult]) -> StateList:
+def retain_state_vectors(sl: StateList, results: Iterable[SectorResult],
+                         drop_blocks: bool = True) -> StateList:
     """Keep only the state list's vectors (ED_DIAG.f90:220-236 stores just
     those): each kept device vector is cloned out of its sector's (neigen, dim)
-    block and every sector result drops its block, so the HBM held after the
-    diagonalisation is the kept states alone."""
+    block and (drop_blocks) every sector result drops its device block, so the
+    HBM held after the diagonalisation is the kept states alone.  Host (numpy)
+    blocks are never dropped."""
     vecs = [v.clone() if (v is not None and not isinstance(v, np.ndarray)) else v for v in sl.vectors]
+    if not drop_blocks:
+        return StateList(list(sl.energies), list(sl.sectors), vecs)
     for r in results:
         if r.vectors is not None and not isinstance(r.vectors, np.ndarray):
             r.vectors = None
@@ -204,7 +214,7 @@ def ed_diag(cfg: EDConfig, opt: Optional[DiagOptions] = None,
     pick = set(sectors) if sectors is not None else None
     todo = [sec for sec in secs if pick is None or sec.isector in pick]
     results = solve_many(cfg, todo, opt, device)
-    return results, retain_state_vectors(state_list(results, opt), results)
+    return results, retain_state_vectors(state_list(results, opt), results, drop_blocks=not opt.retain_all)
 
 
 def eigenvalues_table(results: Iterable[SectorResult]) -> Dict[int, np.ndarray]:

@@ -115,7 +115,7 @@ def farm_diag(cfg: EDConfig, opt: Optional[DiagOptions] = None, *, device: int =
     for k, (q, dim, neigen, ev) in merged.items():
         loc = local.get(k)
         shadows.append(SectorResult(k, q, dim, ev, neigen, loc.vectors if loc is not None else None))
-    states = retain_state_vectors(state_list(shadows, opt), list(local.values()))
+    states = retain_state_vectors(state_list(shadows, opt), list(local.values()), drop_blocks=not opt.retain_all)
     owners = [owner_of[s] for s in states.sectors]
     tables = {k: v[3] for k, v in merged.items()}
     return FarmResult(states, owners, tables, local, assignment)

@@ -300,7 +300,11 @@ def _run_jobs_batched(cfg, states, gopt, jobs, todo, device, wm, wr, Gm, Gr, zet
                 continue
             HJ = cache.get(jobs[live[0]][5], True)
             nlanc = min(HJ.dim, gopt.lanc_nGFiter)
-            a, b, nl = _tridiag_batch(HJ, torch.stack(seeds).contiguous(), nlanc, not cplx, gopt.threshold)
+            stacked = torch.stack(seeds).contiguous()
+            # the library copies the seeds on the sector's own (non-blocking)
+            # stream: the stack kernel on torch's stream must be complete first
+            torch.cuda.current_stream(stacked.device).synchronize()
+            a, b, nl = _tridiag_batch(HJ, stacked, nlanc, not cplx, gopt.threshold)
             for q, n in enumerate(live):
                 comp, tag, k, (op, isign, ispin, terms, weight), sec, jsec = jobs[n]
                 E, z2 = tridiag_poles(a[q], b[q], nlanc)

@@ -19,7 +19,7 @@ from typing import Optional
 import numpy as np
 
 from . import _lib
-from ._lib import ED_DIRECT, ED_REAL, ED_STORED, SectorInfo, check
+from ._lib import ED_DIRECT, ED_KRON2_OFF, ED_KRON2_ON, ED_NO_PACK, ED_REAL, ED_STORED, OPTIONS, SectorInfo, check
 from .params import EDConfig
 from .sectors import Sector as SectorId
 from .sectors import setup_pointers
@@ -48,14 +48,20 @@ class Sector:
     """One symmetry sector resident on one GPU (handle API of include/ed_gpu.h)."""
 
     def __init__(self, cfg: EDConfig, q1: int, q2: int = 0, *, stored: bool = True,
-                 direct: bool = False, real: bool = False, device: int = 0, rows=None):
+                 direct: bool = False, real: bool = False, device: int = 0, rows=None,
+                 pack: bool = True, kron2: Optional[bool] = None, options=()):
         """rows=(row0, nrows): hold only those rows of H (ed_sector_create_rows,
         the reference's MPI row split); H·v then maps a whole-sector vector to
-        the nrows local entries."""
+        the nrows local entries.  pack=False keeps the plain SELL arrays only;
+        kron2 forces the two-pass Kronecker tables on (True) or off (False);
+        options: names of ED_OPT_* kernel alternatives (see set_options)."""
         lib = _lib.load()
         self.cfg = cfg
         self._params = cfg.to_ctypes()
         flags = (ED_STORED if stored else 0) | (ED_DIRECT if direct else 0) | (ED_REAL if real else 0)
+        flags |= 0 if pack else ED_NO_PACK
+        if kron2 is not None:
+            flags |= ED_KRON2_ON if kron2 else ED_KRON2_OFF
         h = ctypes.c_void_p()
         if rows is None:
             check(lib.ed_sector_create(ctypes.byref(self._params), q1, q2, flags, device, None,
@@ -73,6 +79,22 @@ class Sector:
         self.dim = int(info.dim)
         self.nnz = int(info.nnz)
         self.row0, self.nrows = int(info.row0), int(info.nrows)
+        self.options = ()
+        if options:
+            self.set_options(*options)
+
+    def set_options(self, *names: str) -> None:
+        """Select kernel alternatives by name (ED_OPT_*: no_persist,
+        persist_stored, no_preg, no_pkron, fused_step, split_simple, no_batch,
+        eigh_no_verify, trlan_unfused, trlan_nofold, trlan_multi); no names
+        restores the defaults."""
+        bits = 0
+        for n in names:
+            if n not in OPTIONS:
+                raise ValueError(f"unknown kernel option {n!r}")
+            bits |= OPTIONS[n]
+        check(_lib.load().ed_sector_set_options(self._h, bits), "ed_sector_set_options")
+        self.options = tuple(names)
 
     # ------------------------------------------------------------------ life
     def close(self):

@@ -19,8 +19,12 @@ module ED_GPU_HXV
   implicit none
   private
 
-  ! communicator of the MPI H·v (the reference's MpiComm, ED_VARS_GLOBAL.f90:228-231)
-  integer, public :: ed_gpu_comm = 0
+#ifdef _MPI
+  ! communicator of the MPI H·v (the reference's MpiComm, ED_VARS_GLOBAL.f90:228-231):
+  ! MPI_UNDEFINED until ed_gpu_set_MpiComm sets it, as the reference's MpiComm
+  integer, public :: ed_gpu_comm = MPI_UNDEFINED
+  public :: ed_gpu_set_MpiComm, ed_gpu_del_MpiComm
+#endif
 
   integer, parameter, public :: ED_MAX_NORB = 3, ED_MAX_NSPIN = 2, ED_MAX_NBATH = 32
   integer, parameter, public :: ED_STORED = 1, ED_DIRECT = 2, ED_REAL = 4
@@ -166,6 +170,8 @@ contains
 #ifdef _MPI
     integer                    :: i, ierr, nproc
     integer,allocatable        :: counts(:), offset(:)
+    ! spMatVec_mpi_cc: stop if the communicator was never set (STORED_HxV.f90:157)
+    if (ed_gpu_comm == MPI_UNDEFINED) stop "gpuMatVec_mpi_cc ERROR: MpiComm = MPI_UNDEFINED (call ed_gpu_set_MpiComm)"
     call MPI_Comm_size(ed_gpu_comm, nproc, ierr)
     call MPI_Allreduce(Nloc, N, 1, MPI_INTEGER, MPI_SUM, ed_gpu_comm, ierr)
     allocate(counts(0:nproc-1), offset(0:nproc-1))
@@ -185,6 +191,19 @@ contains
 #endif
     call ed_gpu_check(ed_gpu_hxv_mpi(int(Nloc, c_int32_t), vin, Hv), "gpuMatVec_mpi_cc")
   end subroutine gpuMatVec_mpi_cc
+
+#ifdef _MPI
+  !> ed_set_MpiComm (ED_VARS_GLOBAL.f90:295-308): the communicator of gpuMatVec_mpi_cc.
+  subroutine ed_gpu_set_MpiComm(comm)
+    integer, intent(in) :: comm
+    ed_gpu_comm = comm
+  end subroutine ed_gpu_set_MpiComm
+
+  !> ed_del_MpiComm: back to MPI_UNDEFINED.
+  subroutine ed_gpu_del_MpiComm()
+    ed_gpu_comm = MPI_UNDEFINED
+  end subroutine ed_gpu_del_MpiComm
+#endif
 
   !> Reference error convention: stop with a message (e.g. STORED_HxV.f90:50).
   subroutine ed_gpu_check(rc, where)

@@ -62,6 +62,24 @@ extern "C" {
 #define ED_STORED 0x1 /* ed_sparse_H=T: assemble H on the device (SELL-64 layout) */
 #define ED_DIRECT 0x2 /* ed_sparse_H=F: matrix-free H·v, elements regenerated     */
 #define ED_REAL   0x4 /* store H as real(8) (only when impHloc and bath are real) */
+#define ED_NO_PACK   0x10 /* stored: plain SELL arrays only (no {col|value index} words) */
+#define ED_KRON2_OFF 0x20 /* matrix-free Kronecker form: one-pass k_kron only       */
+#define ED_KRON2_ON  0x40 /* two-pass Kronecker tables below the size threshold too */
+
+/* Kernel-selection options of a built sector (ed_sector_set_options): the
+ * alternatives kept for parity tests and A/B measurements.  0 = the default
+ * choice everywhere; nothing in the library reads the environment. */
+#define ED_OPT_NO_PERSIST     0x001 /* Lanczos: graph-captured multi-kernel recurrence only   */
+#define ED_OPT_PERSIST_STORED 0x002 /* Lanczos: persistent MODE 0 (stored matrix from L2)      */
+#define ED_OPT_NO_PREG        0x004 /* Lanczos: no register-resident modes (2, 3, 4)           */
+#define ED_OPT_NO_PKRON       0x008 /* Lanczos: no Kronecker register layout (MODE 4)          */
+#define ED_OPT_FUSED_STEP     0x010 /* multi-kernel Lanczos: one-kernel step on small grids    */
+#define ED_OPT_SPLIT_SIMPLE   0x020 /* kron_rows/cols: one-thread-per-row kernels              */
+#define ED_OPT_NO_BATCH       0x040 /* lanc_tridiag_batch: seeds one after the other           */
+#define ED_OPT_EIGH_NO_VERIFY 0x080 /* eigh: no deflated search for missed degenerate copies   */
+#define ED_OPT_TRLAN_UNFUSED  0x100 /* eigh: four-sweep CGS2 instead of the fused sweeps       */
+#define ED_OPT_TRLAN_NOFOLD   0x200 /* eigh: separate coefficient kernels on small grids       */
+#define ED_OPT_TRLAN_MULTI    0x400 /* eigh: multi-kernel expansion even for one-workgroup sectors */
 
 /* status codes */
 #define ED_OK              0
@@ -142,6 +160,8 @@ int ed_sector_create(const ed_params* p, int32_t q1, int32_t q2, int32_t flags,
 int ed_sector_create_rows(const ed_params* p, int32_t q1, int32_t q2, int32_t flags, int64_t row0,
                           int64_t nrows, int32_t device, void* stream, ed_sector** out);
 int ed_sector_destroy(ed_sector* s);
+/* Select kernel alternatives (ED_OPT_* bit set, replaces the previous set). */
+int ed_sector_set_options(ed_sector* s, int32_t opts);
 int ed_sector_get_info(const ed_sector* s, ed_sector_info* info);
 
 /* H·v on device pointers (async on `stream`).  vtype: 0 = real(8) vectors,
@@ -190,8 +210,9 @@ int ed_sector_lanc_eigh(ed_sector* s, int32_t vtype, const void* v0, int32_t nit
                         int32_t* nlanc);
 /* Diagnostic: the Lanczos recurrence a run with (vtype, path) would use —
  * persistent one-workgroup mode 0 (stored, L2), 1 (Kronecker tables in LDS),
- * 2 (stored matrix in registers), or -1 (graph-captured multi-kernel).
- * Honours the ED_GPU_* environment switches. */
+ * 2 (stored matrix in registers), 3 (its matrix-free twin), 4 (Kronecker
+ * register layout) or -1 (graph-captured multi-kernel), under the sector's
+ * ED_OPT_* options. */
 int ed_sector_lanc_mode(ed_sector* s, int32_t vtype, int32_t path);
 /* Lowest `nev` eigenpairs by thick-restart Lanczos with full (CGS2)
  * reorthogonalisation, Krylov basis of `ncv` vectors resident in HBM: the

@@ -164,7 +164,7 @@ def test_full_size_roofline_sectors(pin):
 
 
 @pytest.mark.parametrize("name,factory,sectors", CASES, ids=[c[0] for c in CASES])
-def test_packed_matches_plain_sell(name, factory, sectors, monkeypatch):
+def test_packed_matches_plain_sell(name, factory, sectors):
     """Packed stored H ({col|value index} words over the distinct values) gives
     bit-identical H·v to the plain SELL arrays: real(8) H with real and complex
     vectors, and complex(8) H (the reference's arithmetic, dictionary of
@@ -174,10 +174,8 @@ def test_packed_matches_plain_sell(name, factory, sectors, monkeypatch):
     cfg = factory()
     q1, q2 = sectors[0]
     for real in ((True, False) if cfg.is_real() else (False,)):
-        monkeypatch.delenv("ED_GPU_NO_PACK", raising=False)
         with Sector(cfg, q1, q2, stored=True, real=real) as S:
-            monkeypatch.setenv("ED_GPU_NO_PACK", "1")
-            with Sector(cfg, q1, q2, stored=True, real=real) as P:
+            with Sector(cfg, q1, q2, stored=True, real=real, pack=False) as P:
                 assert P.info.packed == 0
                 assert S.info.packed == 1 and 1 <= S.info.npdict <= 256
                 i = np.arange(1, S.dim + 1, dtype=np.float64)
@@ -193,20 +191,18 @@ def test_packed_matches_plain_sell(name, factory, sectors, monkeypatch):
 
 
 @pytest.mark.parametrize("cplx", [False, True])
-def test_slice_order_schedule_bit_identical(cplx, monkeypatch):
-    """Nlevels=28 sector (matrix beyond the MALL): the XCD column-window slice
-    schedule visits every slice once with the same per-row arithmetic —
-    identical H·v to the natural order, packed real and packed complex H."""
+def test_n28_packed_matches_plain(cplx):
+    """Nlevels=28 sector (matrix beyond the MALL: non-temporal matrix loads,
+    XCD-remapped block order on the packed kernel): packed real / complex H
+    gives H·v identical to the plain SELL arrays."""
     from edgpu.hamiltonian import Sector
     from edgpu.params import make_config
 
     cfg = make_config(Norb=1, Nbath=13, bath="random", seed=3)
     g = torch.Generator(device="cuda:0").manual_seed(1)
-    monkeypatch.setenv("ED_GPU_SORDER", "1")
     with Sector(cfg, 7, 7, stored=True, real=not cplx) as S:
-        monkeypatch.delenv("ED_GPU_SORDER")
-        with Sector(cfg, 7, 7, stored=True, real=not cplx) as P:
-            assert S.info.packed == 1 and P.info.packed == 1
+        with Sector(cfg, 7, 7, stored=True, real=not cplx, pack=False) as P:
+            assert S.info.packed == 1 and P.info.packed == 0
             dt = torch.complex128 if cplx else torch.float64
             x = torch.rand(S.dim, dtype=dt, device="cuda:0", generator=g)
             y1, y2 = torch.empty_like(x), torch.empty_like(x)

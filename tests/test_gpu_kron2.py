@@ -4,8 +4,9 @@ against the one-pass k_kron and the oracle.
 The two-pass form keeps k_kron's term order per element (diagonal, up hops,
 down hops, each in slot order), so its H·v is bit-identical to k_kron's; the
 Lanczos epilogue reduces over a different grid, so alpha/beta agree to
-rounding (1e-12 relative).  ED_GPU_KRON2=1 forces the two-pass form on small
-sectors (by default it serves sectors of dim >= 2^19), =0 disables it.
+rounding (1e-12 relative).  Sector(kron2=True) forces the two-pass form on
+small sectors (by default it serves sectors of dim >= 2^19), kron2=False
+disables it.
 """
 import numpy as np
 import pytest
@@ -18,23 +19,20 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
-def _both(monkeypatch, cfg, q, real):
+def _both(cfg, q, real):
     from edgpu.hamiltonian import Sector
 
-    monkeypatch.setenv("ED_GPU_KRON2", "1")
-    A = Sector(cfg, q[0], q[1], stored=False, direct=True, real=real)
-    monkeypatch.setenv("ED_GPU_KRON2", "0")
-    B = Sector(cfg, q[0], q[1], stored=False, direct=True, real=real)
-    monkeypatch.delenv("ED_GPU_KRON2")
+    A = Sector(cfg, q[0], q[1], stored=False, direct=True, real=real, kron2=True)
+    B = Sector(cfg, q[0], q[1], stored=False, direct=True, real=real, kron2=False)
     return A, B
 
 
 @pytest.mark.parametrize("name,factory,sectors", CASES, ids=[c[0] for c in CASES])
-def test_two_pass_bit_identical(name, factory, sectors, monkeypatch):
+def test_two_pass_bit_identical(name, factory, sectors):
     cfg = factory()
     orc = Oracle(cfg)
     for q in sectors:
-        A, B = _both(monkeypatch, cfg, q, real=False)
+        A, B = _both(cfg, q, real=False)
         with A, B:
             if not A.info.kron:
                 pytest.skip("no Kronecker form (Jx/Jp or not normal mode)")
@@ -55,11 +53,11 @@ def test_two_pass_bit_identical(name, factory, sectors, monkeypatch):
     (dict(Norb=2, Nbath=5, bath="random", seed=20251015), (6, 6)),       # configs[3] largest
     (dict(Norb=2, Nbath=4, bath="random", seed=4), (3, 6)),              # du != dd
 ])
-def test_two_pass_real_vectors_and_lanczos(cfg_kw, q, monkeypatch):
+def test_two_pass_real_vectors_and_lanczos(cfg_kw, q):
     from edgpu.params import make_config
 
     cfg = make_config(**cfg_kw)
-    A, B = _both(monkeypatch, cfg, q, real=True)
+    A, B = _both(cfg, q, real=True)
     with A, B:
         i = torch.arange(1, A.dim + 1, dtype=torch.float64, device="cuda:0")
         x = torch.sin(i)

@@ -4,8 +4,8 @@ two-pass tables (k_kron_up on a rank's row block, k_kron_dw on a DimDw x nu
 column strip with row length nu).  Same products in the same order as the
 one-thread-per-row k_kron_rows / k_kron_cols: bit-identical, for every row
 block / strip of a 3-rank split, real and complex vectors, with and without
-accumulation into the strip.  ED_GPU_KRON2=1 builds the two-pass tables on
-these small sectors; ED_GPU_SPLIT_SIMPLE=1 selects the simple kernels."""
+accumulation into the strip.  kron2=True builds the two-pass tables on these
+small sectors; the split_simple option selects the simple kernels."""
 import ctypes
 
 import numpy as np
@@ -34,14 +34,13 @@ def _call(S, fn, vt, a, b, x, y, acc=None):
     (dict(Norb=2, Nbath=4, bath="random", seed=4), (3, 6)),       # DimUp != DimDw
 ])
 @pytest.mark.parametrize("cvec", [False, True])
-def test_split_kernels_bit_identical(cfg_kw, q, cvec, monkeypatch):
+def test_split_kernels_bit_identical(cfg_kw, q, cvec):
     from edgpu.dist import split
     from edgpu.hamiltonian import Sector
     from edgpu.params import make_config
 
     cfg = make_config(**cfg_kw)
-    monkeypatch.setenv("ED_GPU_KRON2", "1")
-    with Sector(cfg, q[0], q[1], stored=False, direct=True, real=True) as S:
+    with Sector(cfg, q[0], q[1], stored=False, direct=True, real=True, kron2=True) as S:
         du, dd = int(S.info.dimup), int(S.info.dimdw)
         vt = 1 if cvec else 0
         i = torch.arange(1, S.dim + 1, dtype=torch.float64, device="cuda")
@@ -53,10 +52,7 @@ def test_split_kernels_bit_identical(cfg_kw, q, cvec, monkeypatch):
             xb = X[w0:w0 + nw].reshape(-1).contiguous()
             out = []
             for simple in (False, True):
-                if simple:
-                    monkeypatch.setenv("ED_GPU_SPLIT_SIMPLE", "1")
-                else:
-                    monkeypatch.delenv("ED_GPU_SPLIT_SIMPLE", raising=False)
+                S.set_options(*(("split_simple",) if simple else ()))
                 y = torch.empty_like(xb)
                 _call(S, "ed_sector_kron_rows", vt, w0, nw, xb, y)
                 out.append(y)
@@ -68,16 +64,13 @@ def test_split_kernels_bit_identical(cfg_kw, q, cvec, monkeypatch):
             for acc in (0, 1):
                 out = []
                 for simple in (False, True):
-                    if simple:
-                        monkeypatch.setenv("ED_GPU_SPLIT_SIMPLE", "1")
-                    else:
-                        monkeypatch.delenv("ED_GPU_SPLIT_SIMPLE", raising=False)
+                    S.set_options(*(("split_simple",) if simple else ()))
                     yz = seed.clone()
                     _call(S, "ed_sector_kron_cols", vt, u0, nu, z, yz, acc)
                     out.append(yz)
                 torch.cuda.synchronize()
                 assert torch.equal(out[0], out[1]), f"cols [{u0},{u0 + nu}) acc={acc}"
-        monkeypatch.delenv("ED_GPU_SPLIT_SIMPLE", raising=False)
+        S.set_options()
         # and the assembled split product equals the whole-sector H·v to rounding
         y_full = torch.empty_like(x)
         S.hxv_dev(x, y_full, path=2)

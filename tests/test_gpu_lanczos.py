@@ -27,19 +27,15 @@ def _e0_scipy(csr, dim):
 @pytest.mark.parametrize("persist", ["default", "l2", "lds", "multi"],
                          ids=["persistent", "persist_l2", "persist_lds", "multikernel"])
 @pytest.mark.parametrize("name,factory,sectors", CASES, ids=[c[0] for c in CASES])
-def test_tridiag_and_ground_state(name, factory, sectors, persist, monkeypatch):
+def test_tridiag_and_ground_state(name, factory, sectors, persist):
     """Every device recurrence: the one-workgroup persistent kernel (default for
     sectors that fit one CU: stored matrix in registers / Kronecker tables in
     LDS), its opt-in L2-streaming stored mode, and the graph-captured
     two-kernel one."""
     from edgpu.hamiltonian import Sector
 
-    if persist == "multi":
-        monkeypatch.setenv("ED_GPU_NO_PERSIST", "1")
-    elif persist == "l2":
-        monkeypatch.setenv("ED_GPU_PERSIST_STORED", "1")
-    elif persist == "lds":
-        monkeypatch.setenv("ED_GPU_NO_PREG", "1")        # Kronecker tables in LDS (MODE 1)
+    opts = {"default": (), "multi": ("no_persist",), "l2": ("persist_stored",),
+            "lds": ("no_preg",)}[persist]                # no_preg: Kronecker tables in LDS (MODE 1)
 
     cfg = factory()
     orc = Oracle(cfg)
@@ -51,7 +47,7 @@ def test_tridiag_and_ground_state(name, factory, sectors, persist, monkeypatch):
     n = min(dim, 40)
     ar, br, nr = lanc_tridiag(csr, v0, n)
     for direct in (False, True):
-        with Sector(cfg, q1, q2, stored=not direct, direct=direct) as S:
+        with Sector(cfg, q1, q2, stored=not direct, direct=direct, options=opts) as S:
             a, b, ng = S.lanc_tridiag(v0, n)
             assert ng == nr
             k = min(15, nr)
@@ -85,7 +81,7 @@ def test_real_lanczos_c2():
 
 
 @pytest.mark.parametrize("path", ["stored_l2", "stored_reg", "stored_kr", "kron_lds", "kron_reg", "kron_kr"])
-def test_persistent_matches_multikernel(path, monkeypatch):
+def test_persistent_matches_multikernel(path):
     """Same start vector, same sector: the two recurrences agree step by step
     (first 40 steps to 1e-9; only the reduction order differs)."""
     from edgpu.hamiltonian import Sector
@@ -93,26 +89,22 @@ def test_persistent_matches_multikernel(path, monkeypatch):
 
     cfg = c2()
     kw = dict(stored=False, direct=True) if path.startswith("kron") else dict(stored=True)
-    if path == "stored_l2":
-        monkeypatch.setenv("ED_GPU_PERSIST_STORED", "1")
-    if path == "kron_lds":
-        monkeypatch.setenv("ED_GPU_NO_PREG", "1")
-    if path in ("stored_reg", "kron_reg"):
-        monkeypatch.setenv("ED_GPU_NO_PKRON", "1")
-    with Sector(cfg, 4, 4, real=True, **kw) as S:
+    opts = {"stored_l2": ("persist_stored",), "kron_lds": ("no_preg",), "stored_reg": ("no_pkron",),
+            "kron_reg": ("no_pkron",)}.get(path, ())
+    with Sector(cfg, 4, 4, real=True, options=opts, **kw) as S:
         want = {"stored_l2": 0, "stored_reg": 2, "stored_kr": 4, "kron_lds": 1, "kron_reg": 3,
                 "kron_kr": 4}[path]
         assert S.lanc_mode(real=True) == want
         v0 = np.sin(np.arange(1, S.dim + 1, dtype=np.float64))
         a1, b1, n1 = S.lanc_tridiag(v0, 60)
-        monkeypatch.setenv("ED_GPU_NO_PERSIST", "1")
+        S.set_options(*opts, "no_persist")
         a2, b2, n2 = S.lanc_tridiag(v0, 60)
     assert n1 == n2 == 60
     np.testing.assert_allclose(a1[:40], a2[:40], rtol=1e-9, atol=1e-11)
     np.testing.assert_allclose(b1[:40], b2[:40], rtol=1e-9, atol=1e-11)
 
 
-def test_fused_step_matches_two_kernel(monkeypatch):
+def test_fused_step_matches_two_kernel():
     """Single-kernel step (small grids) vs the two-kernel step: same recurrence."""
     from edgpu.hamiltonian import Sector
     from cases import c5
@@ -120,10 +112,9 @@ def test_fused_step_matches_two_kernel(monkeypatch):
     cfg = c5()
     with Sector(cfg, 7, 0, stored=True) as S:
         v0 = np.sin(np.arange(1, S.dim + 1, dtype=np.float64)) + 0j
-        monkeypatch.setenv("ED_GPU_NO_PERSIST", "1")
-        monkeypatch.setenv("ED_GPU_FUSED_STEP", "1")
+        S.set_options("no_persist", "fused_step")
         a1, b1, n1 = S.lanc_tridiag(v0, 50)
-        monkeypatch.delenv("ED_GPU_FUSED_STEP")
+        S.set_options("no_persist")
         a2, b2, n2 = S.lanc_tridiag(v0, 50)
     np.testing.assert_allclose(a1[:30], a2[:30], rtol=1e-10, atol=1e-12)
     np.testing.assert_allclose(b1[:30], b2[:30], rtol=1e-10, atol=1e-12)

@@ -1,6 +1,6 @@
 """Where the two-pass matrix-free Kronecker H·v (k_kron_up + k_kron_dw) starts
 to beat the one-pass k_kron: H·v time of configs[3] sectors of growing dim
-with ED_GPU_KRON2=0 (one pass) and =1 (two pass), HIP events, 50 launches.
+with Sector(kron2=False) (one pass) and kron2=True (two pass), HIP events, 50 launches.
 
     python tools/kron2_threshold.py
 """
@@ -20,8 +20,7 @@ out = []
 for q in [(3, 3), (3, 4), (4, 4), (4, 5), (5, 5), (5, 6), (6, 6)]:
     row = {"sector": q}
     for k in ("0", "1"):
-        os.environ["ED_GPU_KRON2"] = k
-        with Sector(cfg, q[0], q[1], stored=False, direct=True, real=True) as S:
+        with Sector(cfg, q[0], q[1], stored=False, direct=True, real=True, kron2=(k == "1")) as S:
             i = torch.arange(1, S.dim + 1, dtype=torch.float64, device="cuda")
             x = torch.sin(i)
             y = torch.empty_like(x)
@@ -38,7 +37,6 @@ for q in [(3, 3), (3, 4), (4, 4), (4, 5), (5, 5), (5, 6), (6, 6)]:
             row["two_pass" if k == "1" else "one_pass"] = round(e0.elapsed_time(e1) / 50, 5)
     print(row, flush=True)
     out.append(row)
-os.environ.pop("ED_GPU_KRON2")
 os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
 with open(os.path.join(ROOT, "gpurun_out", "kron2_threshold.json"), "w") as f:
     json.dump(out, f, indent=1)

@@ -23,15 +23,13 @@ cases = [
     ("c5 nonsu2", make_config(Norb=1, Nbath=6, Nspin=2, ed_mode="nonsu2", bath="random"), (7, 0), True),
     ("c4 real", make_config(Norb=2, Nbath=5, bath="random"), (6, 6), True),
 ]
-MODES = {"stored": [("reg", {}), ("l2", {"ED_GPU_PERSIST_STORED": "1"}), ("multi", {"ED_GPU_NO_PERSIST": "1"})],
-         "direct": [("reg", {}), ("lds", {"ED_GPU_NO_PREG": "1"}), ("multi", {"ED_GPU_NO_PERSIST": "1"})]}
+MODES = {"stored": [("reg", ()), ("l2", ("persist_stored",)), ("multi", ("no_persist",))],
+         "direct": [("reg", ()), ("lds", ("no_preg",)), ("multi", ("no_persist",))]}
 for name, cfg, q, real in cases:
     for kind in ("stored", "direct"):
-        for label, env in MODES[kind]:
-            for k in ("ED_GPU_PERSIST_STORED", "ED_GPU_NO_PERSIST", "ED_GPU_NO_PREG"):
-                os.environ.pop(k, None)
-            os.environ.update(env)
-            with Sector(cfg, q[0], q[1], stored=kind == "stored", direct=kind == "direct", real=real) as S:
+        for label, opts in MODES[kind]:
+            with Sector(cfg, q[0], q[1], stored=kind == "stored", direct=kind == "direct", real=real,
+                        options=opts) as S:
                 dt = torch.float64 if real else torch.complex128
                 v0 = torch.sin(torch.arange(1, S.dim + 1, dtype=torch.float64, device="cuda")).to(dt)
                 mode = S.lanc_mode(real=real)
