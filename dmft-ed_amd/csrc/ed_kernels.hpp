@@ -79,16 +79,17 @@ __device__ __forceinline__ int wave_max(int v) {
   for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
   return v;
 }
-// Deterministic block sum; result valid in every thread.
+// Deterministic block sum over NT threads; result valid in every thread.
+template <int NT = kBlock>
 __device__ __forceinline__ double block_sum(double v) {
-  __shared__ double ws[kBlock / 64];
+  __shared__ double ws[NT / 64];
   v = wave_sum(v);
   __syncthreads();
   if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
   __syncthreads();
   double t = 0.0;
 #pragma unroll
-  for (int w = 0; w < kBlock / 64; w++) t = t + ws[w];
+  for (int w = 0; w < NT / 64; w++) t = t + ws[w];
   return t;
 }
 
@@ -105,8 +106,9 @@ struct RedSlot {
 constexpr int kTicketMaxBlocks = 128;
 
 // Two-pass mode, pass 1: block partial -> partials[blockIdx.x].
+template <int NT = kBlock>
 __device__ __forceinline__ void block_partial(double v, double* partials) {
-  double s = block_sum(v);
+  double s = block_sum<NT>(v);
   if (threadIdx.x == 0) partials[blockIdx.x] = s;
 }
 // Pass 2 (one 256-thread block): the same fixed-order sum as grid_reduce_last.
@@ -129,12 +131,13 @@ __device__ __forceinline__ double sum_partials(const double* partials, int n) {
 // release fence (buffer_wbl2) per block writes back the XCD L2's dirty lines
 // and, with thousands of blocks that just wrote H·v outputs, serialises the
 // kernel (measured 7x slower Lanczos steps on the c4 sector).
+template <int NT = kBlock>
 __device__ __forceinline__ bool grid_reduce_last(double v, RedSlot slot, double* total) {
   __shared__ int amlast;
   // every storing wave drains its (write-through) stores before the block's
   // ticket (R1: the signalling lane signals behind a workgroup barrier)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  double s = block_sum(v);
+  double s = block_sum<NT>(v);
   if (threadIdx.x == 0) {
     __hip_atomic_store(slot.partials + blockIdx.x, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -144,9 +147,9 @@ __device__ __forceinline__ bool grid_reduce_last(double v, RedSlot slot, double*
   __syncthreads();
   if (!amlast) return false;
   double a = 0.0;
-  for (unsigned int b = threadIdx.x; b < gridDim.x; b += kBlock)
+  for (unsigned int b = threadIdx.x; b < gridDim.x; b += NT)
     a = a + __hip_atomic_load(slot.partials + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  *total = block_sum(a);
+  *total = block_sum<NT>(a);
   if (threadIdx.x == 0) *slot.counter = 0u;
   return true;
 }
@@ -318,6 +321,7 @@ struct EpiStore {
     hv[i] = acc;
     return 0.0;
   }
+  template <int NT = kBlock>
   __device__ __forceinline__ void finish(double) {}
 };
 
@@ -364,13 +368,14 @@ struct EpiLancA {
     if (bcol) bcol[i] = v;
     return redot(v, w);
   }
+  template <int NT = kBlock>
   __device__ __forceinline__ void finish(double part) {
     if (!slot.counter) {
-      block_partial(part, slot.partials);
+      block_partial<NT>(part, slot.partials);
       return;
     }
     double tot;
-    if (grid_reduce_last(part, slot, &tot) && threadIdx.x == 0) {
+    if (grid_reduce_last<NT>(part, slot, &tot) && threadIdx.x == 0) {
       st->alpha = tot;
       alpha_out[st->iter] = tot;
     }
@@ -432,18 +437,19 @@ struct EpiLancFused {
     if (bcol) bcol[i] = v;
     return redot(v, w);
   }
+  template <int NT = kBlock>
   __device__ __forceinline__ void finish(double part) {
     double alpha;
-    if (!grid_reduce_last(part, slot, &alpha)) return;
+    if (!grid_reduce_last<NT>(part, slot, &alpha)) return;
     // last block: R is no longer read by anyone (every block took its ticket
     // after its gathers completed)
     double np = 0.0;
-    for (int64_t i = threadIdx.x; i < dim; i += kBlock) {
+    for (int64_t i = threadIdx.x; i < dim; i += NT) {
       V w = sub(ld_wt(W + i), scl(alpha, ld_wt(P + i)));
       R[i] = w;
       np += redot(w, w);
     }
-    const double tot = block_sum(np);
+    const double tot = block_sum<NT>(np);
     if (threadIdx.x == 0) {
       st->alpha = alpha;
       alpha_out[st->iter] = alpha;
@@ -760,46 +766,145 @@ __global__ void __launch_bounds__(kBlock) k_spmv_pk(const val_t<HC>* __restrict_
 }
 
 // ---------------------------------------------------- matrix-free (generic)
-template <bool HC, bool VC>
-struct GatherAcc {
-  using V = val_t<VC>;
-  const V* x;
-  const V* xr;
-  DevIndex idx;
-  int64_t i;
-  V acc, xi;
-  __device__ __forceinline__ void diag(double re, double im) {
-    xi = xr[i];
-    acc = add(vzero<V>(), mul(mk<HC>(re, im), xi));
-  }
-  __device__ __forceinline__ void off(uint32_t kst, double re, double im) {
-    acc = add(acc, mul(mk<HC>(re, im), x[idx(kst)]));
-  }
+// directMatVec_cc (DIRECT_HxV.f90:21-92) in gather form, for every ed_mode.
+// One wavefront per chunk of <= 64 consecutive rows of one idw block (the
+// lanes share the down pattern idw and take consecutive up patterns of the
+// block's class).  The row's elements come from the host-built op list of
+// its block, in gen_row order (direct_candidates):
+//   - UNI ops (terms acting on down levels only): condition, sign and target
+//     block are the same for every lane, resolved on the host into a row
+//     offset and a signed value — one coalesced gather, no per-lane work;
+//   - LANE ops (terms touching up levels): condition, target pattern and
+//     Jordan-Wigner sign per lane by bit masks and popc, target row
+//     off[idw'] (block-uniform, from the op) + rank of the target up pattern
+//     (LDS table).
+// The rank table (16-bit, 2^Ns entries) and the up patterns of every class
+// (16-bit, 2^Ns) are staged in LDS once per workgroup; ops are read with
+// scalar loads.  Ops go in groups of kDirGroup with every gather of a group
+// issued before the group's terms are summed, in order, into the row: the
+// same products and additions as k_spmv, so H·v is bit-identical to the
+// stored kernel.  The diagonal is gen_row's own (its off-diagonal part is
+// dead code for DiagAcc).
+constexpr int kDirBlock = 1024;
+constexpr int kDirGroup = 8;
+struct DirOp {
+  uint32_t req_mask, req_val, flip, smask;
+  int32_t delta;  // UNI: target row - own row; LANE: first row of the target block
+  int32_t kind;   // kDirLane | kDirC0 | kDirImSigned | kDirPad
+  double re, im;  // UNI: sign applied; LANE: before the sign
+};
+constexpr int kDirLane = 1, kDirC0 = 2, kDirImSigned = 4, kDirPad = 8;
+struct DirChunk {
+  int32_t row;    // row of lane 0
+  uint32_t idw;   // down pattern of the block
+  int32_t pat0;   // index of lane 0's up pattern in the by-class table
+  int32_t n;      // rows in the chunk (<= 64)
+  int32_t op0, nop;  // the block's ops: [op0, op0 + nop), nop a multiple of kDirGroup
+  int32_t pad[2];
 };
 
-template <bool HC, bool VC, class Epi>
-__global__ void __launch_bounds__(kBlock) k_direct(const EdModel* __restrict__ Mp,
-                                                   const uint32_t* __restrict__ map, DevIndex idx,
-                                                   const val_t<VC>* __restrict__ x,
-                                                   const val_t<VC>* __restrict__ xr, int64_t dim,
-                                                   int64_t nslice, Epi epi) {
+struct DiagAcc {
+  double re = 0.0, im = 0.0;
+  __device__ __forceinline__ void diag(double r, double i) { re = r; im = i; }
+  __device__ __forceinline__ void off(uint32_t, double, double) {}
+};
+
+__device__ __forceinline__ double flip_sign(double v, uint32_t neg) {
+  return __longlong_as_double(__double_as_longlong(v) ^ ((long long)neg << 63));
+}
+
+template <bool HC, bool VC, bool PATLDS, class Epi>
+__global__ void __launch_bounds__(kDirBlock) k_direct(const EdModel* __restrict__ Mp,
+                                                      const DirChunk* __restrict__ chunks, int nchunk,
+                                                      const DirOp* __restrict__ ops,
+                                                      const uint16_t* __restrict__ rank_g,
+                                                      const uint16_t* __restrict__ pat_g,
+                                                      const uint32_t* __restrict__ map, int ns,
+                                                      const val_t<VC>* __restrict__ x, int64_t row0, Epi epi) {
+  using V = val_t<VC>;
+  using H = val_t<HC>;
   if (epi.skip()) return;
   epi.prepare();
-  const EdModel& M = *Mp;
-  double part = 0.0;
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nslice * 64;
-       i += (int64_t)gridDim.x * kBlock) {
-    if (i < dim) {
-      GatherAcc<HC, VC> g;
-      g.x = x;
-      g.xr = xr;
-      g.idx = idx;
-      g.i = i;
-      gen_row(M, map[i], g);
-      part += epi.row(i, g.acc, g.xi);
+  extern __shared__ __align__(16) unsigned char smem[];
+  uint16_t* srank = (uint16_t*)smem;
+  uint16_t* spat = srank + (1 << ns);
+  if (ns >= 3) {  // 16-byte staging of the tables
+    const int h = (1 << ns) / 8;
+    const int n4 = (PATLDS ? 2 : 1) * h;
+    const uint4* src0 = (const uint4*)rank_g;
+    const uint4* src1 = (const uint4*)pat_g;
+    for (int q = threadIdx.x; q < n4; q += kDirBlock) ((uint4*)smem)[q] = q < h ? src0[q] : src1[q - h];
+  } else {
+    for (int q = threadIdx.x; q < (1 << ns); q += kDirBlock) {
+      srank[q] = rank_g[q];
+      if (PATLDS) spat[q] = pat_g[q];
     }
   }
-  epi.finish(part);
+  __syncthreads();
+  const EdModel& M = *Mp;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // chunk data and ops: scalar loads
+  const uint32_t mask = (1u << ns) - 1u;
+  // chunk schedule: with a grid of 8k blocks each XCD (blocks b = x mod 8)
+  // walks one contiguous eighth of the chunks, so its L2 serves the gathers
+  // neighbouring rows share
+  int c, cend, cstep;
+  if ((gridDim.x & 7) == 0) {
+    const int xcd = blockIdx.x & 7;
+    c = (int)((int64_t)nchunk * xcd / 8) + (int)(blockIdx.x >> 3) * (kDirBlock / 64) + wv;
+    cend = (int)((int64_t)nchunk * (xcd + 1) / 8);
+    cstep = (int)(gridDim.x >> 3) * (kDirBlock / 64);
+  } else {
+    c = blockIdx.x * (kDirBlock / 64) + wv;
+    cend = nchunk;
+    cstep = gridDim.x * (kDirBlock / 64);
+  }
+  double part = 0.0;
+  for (; c < cend; c += cstep) {
+    const DirChunk ch = chunks[c];
+    const bool on = lane < ch.n;
+    const int row = ch.row + (on ? lane : 0);
+    uint32_t up;
+    if constexpr (PATLDS) up = spat[ch.pat0 + (on ? lane : 0)];
+    else up = map[row] & mask;
+    const uint32_t m = up | (ch.idw << ns);
+    DiagAcc dg;
+    gen_row(M, m, dg);
+    const V xi = x[row];
+    V acc = add(vzero<V>(), mul(mk<HC>(dg.re, dg.im), xi));
+    for (int o = ch.op0; o < ch.op0 + ch.nop; o += kDirGroup) {
+      int tg[kDirGroup];
+      bool vd[kDirGroup];
+      H hv[kDirGroup];
+#pragma unroll
+      for (int j = 0; j < kDirGroup; j++) {
+        const DirOp op = ops[o + j];
+        if (op.kind & kDirLane) {
+          const bool f = (m & op.req_mask) == op.req_val;
+          const uint32_t k = m ^ op.flip;
+          const uint32_t neg = (uint32_t)(__builtin_popcount(m & op.smask) + (op.kind >> 1)) & 1u;
+          vd[j] = f;
+          tg[j] = f ? op.delta + (int)srank[k & mask] : row;
+          if constexpr (HC)
+            hv[j] = make_double2(flip_sign(op.re, neg), (op.kind & kDirImSigned) ? flip_sign(op.im, neg) : op.im);
+          else
+            hv[j] = flip_sign(op.re, neg);
+        } else {
+          vd[j] = !(op.kind & kDirPad);
+          tg[j] = row + op.delta;
+          hv[j] = mk<HC>(op.re, op.im);
+        }
+      }
+      V g[kDirGroup];
+#pragma unroll
+      for (int j = 0; j < kDirGroup; j++) g[j] = x[tg[j]];
+#pragma unroll
+      for (int j = 0; j < kDirGroup; j++)
+        if (vd[j]) acc = add(acc, mul(hv[j], g[j]));
+    }
+    if (on) part += epi.row((int64_t)row - row0, acc, xi);
+  }
+  epi.template finish<kDirBlock>(part);
 }
 
 // ------------------------------------------- matrix-free (Kronecker form)
@@ -1180,6 +1285,29 @@ __global__ void __launch_bounds__(kBlock) k_kron_cols(KronArgs<HC> K, int64_t nu
   }
 }
 
+// -------------------------------- row split: columns the held rows gather
+// One bit per sector column, set for every column an off-diagonal element of
+// rows [row0, row0 + n) refers to (gen_row's elements: stored and matrix-free
+// alike).  The halo of a rank's row block for the split H·v (edgpu.dist).
+struct MarkAcc {
+  DevIndex idx;
+  uint32_t* mask;
+  __device__ __forceinline__ void diag(double, double) {}
+  __device__ __forceinline__ void off(uint32_t k, double, double) {
+    const uint32_t c = (uint32_t)idx(k);
+    atomicOr(mask + (c >> 5), 1u << (c & 31));
+  }
+};
+__global__ void __launch_bounds__(kBlock) k_mark_cols(const EdModel* __restrict__ Mp,
+                                                      const uint32_t* __restrict__ map, int64_t n,
+                                                      DevIndex idx, uint32_t* mask) {
+  const EdModel& M = *Mp;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    MarkAcc a{idx, mask};
+    gen_row(M, map[i], a);
+  }
+}
+
 // ------------------------------------------------ GF seeds: c / c^+ |state>
 // One thread per source row; every target row is hit at most once (the
 // operator is injective on the Fock basis), so plain stores suffice.
@@ -1222,6 +1350,66 @@ __global__ void __launch_bounds__(kBlock) k_apply_op_acc(const uint32_t* __restr
       }
     }
   }
+}
+
+// ------------------------------------------------ GF pole sums (device G)
+// add_to_lanczos_gf_normal (ED_GF_NORMAL.f90:620-631) / _nonsu2
+// (ED_GF_NONSU2.f90:936-950): for every frequency i, fraction by fraction in
+// list order and pole by pole (j ascending), exactly the reference's sequence
+// of additions into G(i):
+//   G(i) = G(i) + peso_j / (iw_i - isign*de_j),  de_j = E_j - Ei,
+//   peso_j = (pesoBZ * z_j) * z_j,  iw = (0, wm_i) or (wr_i, eps).
+// One thread per frequency (Matsubara then real axis); the fraction and pole
+// data are wave-uniform (scalar loads); G stays in HBM across seeds.
+struct GfFrac {
+  int32_t p0, np, comp, isign;
+  double pr, pi, ei;  // pesoBZ (complex), Ei
+  double pad;
+};
+
+// Smith's complex division (the scaling gfortran/flang use for complex /)
+__device__ __forceinline__ double2 cdiv(double2 p, double a, double b) {
+  if (fabs(b) <= fabs(a)) {
+    const double r = b / a, den = a + b * r;
+    return make_double2((p.x + p.y * r) / den, (p.y - p.x * r) / den);
+  }
+  const double r = a / b, den = a * r + b;
+  return make_double2((p.x * r + p.y) / den, (p.y * r - p.x) / den);
+}
+
+__global__ void __launch_bounds__(kBlock) k_gf_poles(const GfFrac* __restrict__ fr, int nfrac,
+                                                     const double* __restrict__ E, const double* __restrict__ z,
+                                                     const double* __restrict__ wm, int lmats,
+                                                     const double* __restrict__ wr, int lreal, double eps,
+                                                     double2* __restrict__ gm, double2* __restrict__ gr) {
+  const int t = blockIdx.x * kBlock + threadIdx.x;
+  if (t >= lmats + lreal) return;
+  const bool mats = t < lmats;
+  const int i = mats ? t : t - lmats;
+  const double re_w = mats ? 0.0 : wr[i];   // iw = xi*wm(i) = (0, wm); dcmplx(wr(i), eps)
+  const double im_w = mats ? wm[i] : eps;
+  double2* G = mats ? gm : gr;
+  const int L = mats ? lmats : lreal;
+  int cur = -1;
+  double2 g = make_double2(0.0, 0.0);
+  for (int f = 0; f < nfrac; f++) {
+    const GfFrac q = fr[f];
+    if (q.comp != cur) {
+      if (cur >= 0) G[(int64_t)cur * L + i] = g;
+      cur = q.comp;
+      g = G[(int64_t)cur * L + i];
+    }
+    const double sgn = (double)q.isign;
+    for (int j = 0; j < q.np; j++) {
+      const double zj = z[q.p0 + j];
+      const double de = E[q.p0 + j] - q.ei;
+      const double2 peso = make_double2((q.pr * zj) * zj, (q.pi * zj) * zj);
+      const double d = sgn * de;
+      const double2 c = cdiv(peso, re_w - d, im_w);
+      g = make_double2(g.x + c.x, g.y + c.y);
+    }
+  }
+  if (cur >= 0) G[(int64_t)cur * L + i] = g;
 }
 
 // ------------------------------------------------------------ Lanczos misc

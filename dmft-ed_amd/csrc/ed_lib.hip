@@ -112,7 +112,14 @@ struct ed_sector {
   uint32_t* d_words = nullptr;
   void* d_pdict = nullptr;   // real(8) or complex(8) values (hc)
   int npdict = 0;
-  // matrix-free
+  // matrix-free, generic (k_direct): chunk list, per-block op lists, 16-bit tables
+  DirChunk* d_dchunk = nullptr;
+  int ndchunk = 0;
+  DirOp* d_dops = nullptr;
+  uint16_t *d_rank16 = nullptr, *d_pat16 = nullptr;
+  bool dir_patlds = false;
+  int dir_lds = 0, dir_grid = 0;
+  // matrix-free, Kronecker form
   bool kron = false;
   KronHost K;
   // host-pointer H·v staging
@@ -133,6 +140,7 @@ struct ed_sector {
   int pkr_state = 0;        // 0 not tried, -1 ineligible, 1 tables ready
   int pkr_src = -1;         // path the tables came from (0 stored SELL, 2 hop tables)
   int pkr_E = 0, pkr_rpt = 0, pkr_du = 0, pkr_dd = 0, pkr_degu = 0, pkr_degd = 0;
+  int pkr_rpt_c = 0;        // rows per thread of the complex-vector layout (1024 threads), 0: none
   const int32_t *d_kupc = nullptr, *d_kdwc = nullptr;
   const double *d_kupv = nullptr, *d_kdwv = nullptr, *d_kdiag = nullptr;
   // graph cache for Lanczos iterations
@@ -382,6 +390,160 @@ static int build_stored(ed_sector* s) {
   for (int64_t i = 0; i < dim; i++) nnz += hc[i];
   s->nnz = nnz;
   if (s->dim <= (int64_t)kPackColMask + 1 && !(s->flags & ED_NO_PACK)) CK(build_pack(s));
+  return ED_OK;
+}
+
+// ------------------------------------------------ matrix-free (generic)
+// Host side of k_direct: the candidates of gen_row (direct_candidates), the
+// op list of every idw block (down-only terms resolved per block into a row
+// offset and a signed value, terms that cannot act in the block dropped,
+// padded to kDirGroup), the 64-row chunks of the held rows and the 16-bit
+// rank / by-class pattern tables.
+struct RecAcc {
+  std::vector<uint32_t> k;
+  std::vector<double> re, im;
+  double dr = 0.0, di = 0.0;
+  void diag(double r, double i) { dr = r; di = i; }
+  void off(uint32_t t, double r, double i) {
+    k.push_back(t);
+    re.push_back(r);
+    im.push_back(i);
+  }
+};
+static bool same_bits(double a, double b) { return memcmp(&a, &b, 8) == 0; }
+
+// The candidates must reproduce gen_row element by element (target, value
+// bits, order): checked on sample states of the sector before any launch.
+static int direct_candidates_check(const ed_sector* s, const std::vector<DirCand>& cands) {
+  const SectorTables& T = s->T;
+  const int64_t nb = (int64_t)T.blk_idw.size();
+  const int64_t step = std::max<int64_t>(1, s->dim / 4096);
+  for (int64_t i = 0; i < s->dim; i += step) {
+    const int64_t b = std::upper_bound(T.blk_off.begin(), T.blk_off.begin() + nb + 1, i) - T.blk_off.begin() - 1;
+    const uint32_t idw = T.blk_idw[b];
+    const uint32_t m = T.by_cls[T.cls_start[T.need_cls[idw]] + (i - T.blk_off[b])] | (idw << T.ns);
+    RecAcc ref;
+    gen_row(s->Mh, m, ref);
+    size_t q = 0;
+    for (const DirCand& c : cands) {
+      uint32_t k;
+      double sg;
+      if (!cand_apply(c, m, &k, &sg)) continue;
+      const double re = c.re * sg, im = c.im_signed ? c.im * sg : c.im;
+      if (q >= ref.k.size() || ref.k[q] != k || !same_bits(ref.re[q], re) || !same_bits(ref.im[q], im))
+        return fail(ED_ERR_STATE, "direct candidates differ from gen_row (row " + std::to_string(i) + ")");
+      q++;
+    }
+    if (q != ref.k.size()) return fail(ED_ERR_STATE, "direct candidates miss elements of gen_row");
+  }
+  return ED_OK;
+}
+
+static int build_direct(ed_sector* s) {
+  const SectorTables& T = s->T;
+  const int ns = T.ns;
+  const uint32_t nst = T.nst;
+  std::vector<DirCand> cands;
+  direct_candidates(s->Mh, cands);
+  CK(direct_candidates_check(s, cands));
+  std::vector<DirOp> ops;
+  std::vector<DirChunk> chunks;
+  const int64_t r0 = s->row0, r1 = s->row0 + s->nrows;
+  for (size_t b = 0; b + 1 < T.blk_off.size(); b++) {
+    const int64_t lo = std::max<int64_t>(T.blk_off[b], r0), hi = std::min<int64_t>(T.blk_off[b + 1], r1);
+    if (lo >= hi) continue;
+    const uint32_t idw = T.blk_idw[b];
+    const uint32_t mdw = idw << ns;
+    const int32_t op0 = (int32_t)ops.size();
+    for (const DirCand& c : cands) {
+      const uint32_t dmask = ~(nst - 1);  // down levels
+      if ((mdw & c.req_mask & dmask) != (c.req_val & dmask)) continue;  // cannot act in this block
+      const uint32_t idw2 = idw ^ (c.flip >> ns);
+      const int32_t off2 = T.off[idw2];
+      const bool uni = ((c.req_mask | c.flip | c.smask) & (nst - 1)) == 0;
+      DirOp o{};
+      if (uni) {
+        if (off2 < 0) return fail(ED_ERR_STATE, "direct: a down-level term leaves the sector");
+        const double sg = ((__builtin_popcount(mdw & c.smask) + c.c0) & 1) ? -1.0 : 1.0;
+        o.delta = (int32_t)(off2 - T.off[idw]);
+        o.kind = 0;
+        o.re = c.re * sg;
+        o.im = c.im_signed ? c.im * sg : c.im;
+      } else {
+        if (off2 < 0) continue;  // no up pattern can reach an empty block
+        o.req_mask = c.req_mask;
+        o.req_val = c.req_val;
+        o.flip = c.flip;
+        o.smask = c.smask;
+        o.delta = off2;
+        o.kind = kDirLane | (c.c0 ? kDirC0 : 0) | (c.im_signed ? kDirImSigned : 0);
+        o.re = c.re;
+        o.im = c.im;
+      }
+      ops.push_back(o);
+    }
+    while ((ops.size() - op0) % kDirGroup) {
+      DirOp o{};
+      o.kind = kDirPad;
+      ops.push_back(o);
+    }
+    const int32_t nop = (int32_t)ops.size() - op0;
+    const int64_t cls0 = T.cls_start[T.need_cls[idw]];
+    for (int64_t r = lo; r < hi; r += 64) {
+      DirChunk ch{};
+      ch.row = (int32_t)r;
+      ch.idw = idw;
+      ch.pat0 = (int32_t)(cls0 + (r - T.blk_off[b]));
+      ch.n = (int32_t)std::min<int64_t>(64, hi - r);
+      ch.op0 = op0;
+      ch.nop = nop;
+      chunks.push_back(ch);
+    }
+  }
+  if (ops.empty()) ops.resize(kDirGroup);  // (valid pointer)
+  std::vector<uint16_t> rk(std::max<uint32_t>(nst, 8), 0), pt(std::max<uint32_t>(nst, 8), 0);
+  for (uint32_t x = 0; x < nst; x++) {
+    rk[x] = (uint16_t)T.rank[x];
+    pt[x] = (uint16_t)T.by_cls[x];
+  }
+  s->ndchunk = (int)chunks.size();
+  if (chunks.empty()) chunks.resize(1);
+  CK(upload(s, &s->d_dchunk, chunks));
+  CK(upload(s, &s->d_dops, ops));
+  CK(upload(s, &s->d_rank16, rk));
+  CK(upload(s, &s->d_pat16, pt));
+  // both tables in LDS up to Ns = 15 (128 KB); at Ns = 16 the rank table
+  // alone (128 KB), the row's own pattern then read from H%map
+  s->dir_patlds = 4 * (int64_t)rk.size() <= 128 * 1024;
+  s->dir_lds = (int)((s->dir_patlds ? 4 : 2) * rk.size());
+  // 16 chunks per workgroup and step; at most 2 workgroups per CU: the
+  // fixed grid also sizes the per-block partials of fused epilogues
+  const int g = (int)std::min<int64_t>((s->ndchunk + 15) / 16, 512);
+  s->dir_grid = g >= 8 ? (g & ~7) : std::max(g, 1);
+  return ED_OK;
+}
+
+template <bool HC, bool VC, bool PL, class Epi>
+static int launch_direct(ed_sector* s, const void* x, Epi epi, hipStream_t st) {
+  using V = val_t<VC>;
+  auto fn = k_direct<HC, VC, PL, Epi>;
+  // dynamic LDS beyond 64 KB: allow what the 160 KB leave next to the
+  // function's static LDS (the epilogue's reduction slots)
+  static std::once_flag attr;
+  static hipError_t ae = hipSuccess;
+  std::call_once(attr, [&]() {
+    hipFuncAttributes fa{};
+    ae = hipFuncGetAttributes(&fa, (const void*)fn);
+    if (ae == hipSuccess)
+      ae = hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               160 * 1024 - (int)fa.sharedSizeBytes);
+  });
+  if (ae != hipSuccess) {
+    (void)hipGetLastError();  // not sticky for later launches
+    return fail(ED_ERR_HIP, std::string("k_direct LDS attribute -> ") + hipGetErrorString(ae));
+  }
+  hipLaunchKernelGGL(fn, dim3(s->dir_grid), dim3(kDirBlock), s->dir_lds, st, s->Md, s->d_dchunk, s->ndchunk,
+                     s->d_dops, s->d_rank16, s->d_pat16, s->d_map, s->T.ns, (const V*)x, s->row0, epi);
   return ED_OK;
 }
 
@@ -647,6 +809,7 @@ static bool kron2_on(const ed_sector* s, int path, int vc) {
 static int kron_dw_grid(bool vc) { return vc ? kKronDwGrid / 2 : kKronDwGrid; }
 static int hxv_blocks(const ed_sector* s, int path, int vc = 0) {
   if (kron2_on(s, path, vc)) return kron_dw_grid(vc);
+  if (path == 1) return s->dir_grid;
   const int g = grid_for(s->nslice * 64);
   return xcd_on(s, path) ? (g & ~7) : g;
 }
@@ -768,9 +931,9 @@ static int launch_hxv_t(ed_sector* s, int path, const void* x, Epi epi, hipStrea
                          (const val_t<HC>*)s->d_diag, s->d_sptr, s->d_cols,
                          (const val_t<HC>*)s->d_vals, (const V*)x, xo, dim, ns, epi, xr);
   } else if (path == 1) {
-    DevIndex idx{s->d_off, s->d_rank, s->T.ns, s->T.nst - 1};
-    hipLaunchKernelGGL((k_direct<HC, VC, Epi>), dim3(g), dim3(kBlock), 0, st, s->Md, s->d_map + s->row0,
-                       idx, (const V*)x, xo, dim, ns, epi);
+    const int rc = s->dir_patlds ? launch_direct<HC, VC, true>(s, x, epi, st)
+                                 : launch_direct<HC, VC, false>(s, x, epi, st);
+    if (rc != ED_OK) return rc;
   } else if (kron2_on(s, path, VC)) {
     return launch_kron2<HC, VC>(s, x, epi, st);
   } else {
@@ -1032,6 +1195,10 @@ static int build_preg(ed_sector* s) {
 // stay below the spill-free budget (-Rpass-analysis=kernel-resource-usage:
 // E=4/RPT=10 and E=8/RPT=6 compile without scratch).
 constexpr bool pkr_fits(int E, int RPT) { return RPT * (3 * E + 8) + 3 * E <= 216; }
+// complex vectors (1024 threads, <= 128 VGPRs): per row the down-hop byte
+// offsets and the complex w and p; the diagonal and the hop values in LDS
+// (-Rpass-analysis: E=4 up to 5 rows, E=8 up to 3 rows spill-free)
+constexpr bool pkr_fits_c(int E, int RPT) { return E == 4 ? RPT <= 5 : RPT <= 2; }
 static int pkr_geom(ed_sector* s, int64_t du, int64_t dd, int degu, int degd) {
   const int deg = std::max(degu, degd);
   const int E = deg <= 4 ? 4 : deg <= 8 ? 8 : 0;
@@ -1041,6 +1208,9 @@ static int pkr_geom(ed_sector* s, int64_t du, int64_t dd, int degu, int degd) {
   if (!RPT || !pkr_fits(E, RPT)) return -1;
   s->pkr_E = E;
   s->pkr_rpt = RPT;
+  const int64_t Gc = kPBlock / du, rc = (dd + Gc - 1) / Gc;
+  const int RC = rc <= 2 ? 2 : rc <= 5 ? (int)rc : 0;
+  s->pkr_rpt_c = (RC && pkr_fits_c(E, RC)) ? RC : 0;
   s->pkr_du = (int)du;
   s->pkr_dd = (int)dd;
   s->pkr_degu = degu;
@@ -1229,11 +1399,11 @@ static int persist_rpt01(int64_t dim) {
   return rpt <= 6 ? (int)rpt : rpt <= 8 ? 8 : rpt <= 10 ? 10 : rpt <= 12 ? 12 : 16;
 }
 // LDS vector rows of a persistent launch: NT * RPT (padding rows stay zero)
-static int64_t persist_vrows(const ed_sector* s, int mode) {
+static int64_t persist_vrows(const ed_sector* s, int mode, int vc = 0) {
   switch (mode) {
     case 2: return (int64_t)kPRegBlock * s->preg_rpt;
     case 3: return (int64_t)kPRegBlock * s->kreg_rpt;
-    case 4: return (int64_t)kPRegBlock * s->pkr_rpt;
+    case 4: return vc ? (int64_t)kPBlock * s->pkr_rpt_c : (int64_t)kPRegBlock * s->pkr_rpt;
     default: return (int64_t)kPBlock * persist_rpt01(s->dim);
   }
 }
@@ -1248,11 +1418,12 @@ static int persist_mode(ed_sector* s, int vc, int path) {
   const int64_t rpt_max = (vc || s->hc) ? 5 : 8;
   if (s->dim > rpt_max * (int64_t)kPBlock) return -1;
   int64_t lds = ((persist_vrows(s, 0) * vs + 15) & ~(int64_t)15);
-  // MODE 4 (Kronecker register layout, real vectors): c2 2.2 us/step
-  if (vc == 0 && !(o & (ED_OPT_NO_PKRON | ED_OPT_NO_PREG)) &&
+  // MODE 4 (Kronecker register layout, real H): c2 2.2 us/step (real
+  // vectors); complex vectors in their 1024-thread form
+  if (!(o & (ED_OPT_NO_PKRON | ED_OPT_NO_PREG)) &&
       ((path == 0 && !(o & ED_OPT_PERSIST_STORED) && build_pkron_stored(s) > 0) ||
        (path == 2 && build_pkron_direct(s) > 0)) &&
-      persist_lds(s, vc, 4) <= kLdsBudget)
+      (vc == 0 || s->pkr_rpt_c > 0) && persist_lds(s, vc, 4) <= kLdsBudget)
     return 4;
   // stored: MODE 2 (ELL entries in registers; c2 4.6 us/step) by default.
   // MODE 0 streams the matrix from L2 through one CU (~40-50 GB/s) and is
@@ -1301,9 +1472,9 @@ static int persist_mode(ed_sector* s, int vc, int path) {
 }
 
 static int64_t persist_lds(const ed_sector* s, int vc, int mode) {
-  const int64_t vs = vc ? 16 : 8, vr = persist_vrows(s, mode);
+  const int64_t vs = vc ? 16 : 8, vr = persist_vrows(s, mode, vc);
   int64_t lds = ((vr * vs + 15) & ~(int64_t)15);
-  if (mode == 4) return lds;
+  if (mode == 4) return lds + (vc ? vr * 8 + (int64_t)s->pkr_E * (s->pkr_dd + s->pkr_du) * 8 : 0);
   if (mode == 2) {
     const int64_t hs = s->hc ? 16 : 8;
     return lds + ((vr * 8 + 15) & ~(int64_t)15) + (((int64_t)s->ndict * hs + 15) & ~(int64_t)15);
@@ -1328,10 +1499,10 @@ template <bool HC, bool VC, int MODE, int RPT, int E = 1>
 static int persist_launch_t(ed_sector* s, const PersistRun<HC>& run, int64_t lds, hipStream_t st, int nb) {
   if constexpr ((MODE == 2 || MODE == 3) && RPT * E > preg_cap(HC, VC)) {
     return fail(ED_ERR_UNSUPPORTED, "register-resident ELL exceeds the spill-free budget");
-  } else if constexpr (MODE == 4 && (HC || VC || !pkr_fits(E, RPT))) {
-    return fail(ED_ERR_UNSUPPORTED, "Kronecker register layout: real H and vectors within the register budget");
+  } else if constexpr (MODE == 4 && (HC || (VC ? !pkr_fits_c(E, RPT) : !pkr_fits(E, RPT)))) {
+    return fail(ED_ERR_UNSUPPORTED, "Kronecker register layout: real H within the register budget");
   } else {
-  constexpr int NT = MODE >= 2 ? kPRegBlock : kPBlock;
+  constexpr int NT = (MODE >= 2 && !(MODE == 4 && VC)) ? kPRegBlock : kPBlock;
   auto fn = k_lanc_persist<HC, VC, MODE, RPT, E, NT>;
   HIPCK(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(fn, dim3(nb), dim3(NT), (size_t)lds, st, run);
@@ -1342,6 +1513,14 @@ static int persist_launch_t(ed_sector* s, const PersistRun<HC>& run, int64_t lds
 
 template <bool HC, bool VC, int MODE, int W>
 static int persist_launch_e(ed_sector* s, const PersistRun<HC>& run, int64_t lds, hipStream_t st, int nb) {
+  if constexpr (MODE == 4 && VC) {
+    switch (s->pkr_rpt_c) {
+      case 2: return persist_launch_t<HC, VC, MODE, 2, W>(s, run, lds, st, nb);
+      case 3: return persist_launch_t<HC, VC, MODE, 3, W>(s, run, lds, st, nb);
+      case 4: return persist_launch_t<HC, VC, MODE, 4, W>(s, run, lds, st, nb);
+      default: return persist_launch_t<HC, VC, MODE, 5, W>(s, run, lds, st, nb);
+    }
+  }
   switch (MODE == 2 ? s->preg_rpt : MODE == 3 ? s->kreg_rpt : s->pkr_rpt) {
     case 2: return persist_launch_t<HC, VC, MODE, 2, W>(s, run, lds, st, nb);
     case 4: return persist_launch_t<HC, VC, MODE, 4, W>(s, run, lds, st, nb);
@@ -1354,8 +1533,8 @@ static int persist_launch_e(ed_sector* s, const PersistRun<HC>& run, int64_t lds
 template <bool HC, bool VC, int MODE>
 static int persist_launch_m(ed_sector* s, const PersistRun<HC>& run, int64_t lds, hipStream_t st, int nb = 1) {
   if constexpr (MODE == 4) {
-    if constexpr (HC || VC) {
-      return fail(ED_ERR_UNSUPPORTED, "MODE 4 needs real H and vectors");
+    if constexpr (HC) {
+      return fail(ED_ERR_UNSUPPORTED, "MODE 4 needs a real H");
     } else {
       return s->pkr_E == 4 ? persist_launch_e<HC, VC, 4, 4>(s, run, lds, st, nb)
                            : persist_launch_e<HC, VC, 4, 8>(s, run, lds, st, nb);
@@ -2105,6 +2284,7 @@ static int sector_create(const ed_params* p, int32_t q1, int32_t q2, int32_t fla
   // Kronecker form: normal mode without Jx/Jp terms (no term moves both spins)
   s->kron = (flags & ED_DIRECT) && s->Mh.mode == ED_MODE_NORMAL && !s->Mh.jhflag && nrows == s->dim;
   if ((flags & ED_STORED) && nrows > 0) TRY(build_stored(s));
+  if ((flags & ED_DIRECT) && nrows > 0) TRY(build_direct(s));
   if (s->kron) TRY(build_kron(s));
   if (hipStreamSynchronize(s->stream) != hipSuccess) {
     sector_free(s);
@@ -2179,6 +2359,19 @@ int ed_sector_hxv_dev_path(ed_sector* s, int32_t path, int32_t vtype, const void
     return launch_hxv<false>(s, pth, v, e, st);
   }
   return fail(ED_ERR_ARG, "vtype must be 0 (real) or 1 (complex)");
+}
+
+int ed_sector_col_mask(const ed_sector* s, uint32_t* mask_dev, void* stream) {
+  if (!s || !mask_dev) return fail(ED_ERR_ARG, "null");
+  HIPCK(hipSetDevice(s->device));
+  hipStream_t st = (hipStream_t)stream;
+  HIPCK(hipMemsetAsync(mask_dev, 0, (size_t)((s->dim + 31) / 32) * 4, st));
+  if (s->nrows == 0) return ED_OK;
+  DevIndex idx{s->d_off, s->d_rank, s->T.ns, s->T.nst - 1};
+  hipLaunchKernelGGL(k_mark_cols, dim3(grid_for(s->nrows)), dim3(kBlock), 0, st, s->Md, s->d_map + s->row0,
+                     s->nrows, idx, mask_dev);
+  HIPCK(hipGetLastError());
+  return ED_OK;
 }
 
 int ed_sector_kron_rows(ed_sector* s, int32_t vtype, int64_t w0, int64_t nw, const void* x, void* y,
@@ -2557,7 +2750,7 @@ static double ql_pythag(double a, double b) {
   return p;
 }
 
-int ed_tridiag_poles(int32_t n, const double* alfa, const double* beta, double* E, double* z2) {
+int ed_tridiag_poles(int32_t n, const double* alfa, const double* beta, double* E, double* z2, double* z1) {
   if (n < 1 || !alfa || !beta || !E || !z2) return fail(ED_ERR_ARG, "bad args");
   std::vector<double> e(n, 0.0), z(n, 0.0);
   for (int i = 0; i < n; i++) E[i] = alfa[i];
@@ -2620,6 +2813,55 @@ int ed_tridiag_poles(int32_t n, const double* alfa, const double* beta, double* 
     }
   }
   for (int i = 0; i < n; i++) z2[i] = z[i] * z[i];
+  if (z1)
+    for (int i = 0; i < n; i++) z1[i] = z[i];
+  return ED_OK;
+}
+
+int ed_gf_add_poles(int32_t nfrac, const int32_t* npole, const double* E, const double* z, const double* peso_bz,
+                    const double* Ei, const int32_t* isign, const int32_t* comp, const double* wm, int32_t lmats,
+                    const double* wr, int32_t lreal, double eps, double* gm, double* gr, void* stream) {
+  if (nfrac < 0 || lmats < 0 || lreal < 0) return fail(ED_ERR_ARG, "bad sizes");
+  if (nfrac == 0 || lmats + lreal == 0) return ED_OK;
+  if (!npole || !E || !z || !peso_bz || !Ei || !isign || !comp || (lmats && (!wm || !gm)) ||
+      (lreal && (!wr || !gr)))
+    return fail(ED_ERR_ARG, "null");
+  std::vector<GfFrac> fr(nfrac);
+  int64_t np = 0;
+  for (int f = 0; f < nfrac; f++) {
+    if (npole[f] < 0 || comp[f] < 0 || (isign[f] != 1 && isign[f] != -1)) return fail(ED_ERR_ARG, "bad fraction");
+    fr[f].p0 = (int32_t)np;
+    fr[f].np = npole[f];
+    fr[f].comp = comp[f];
+    fr[f].isign = isign[f];
+    fr[f].pr = peso_bz[2 * f];
+    fr[f].pi = peso_bz[2 * f + 1];
+    fr[f].ei = Ei[f];
+    fr[f].pad = 0.0;
+    np += npole[f];
+  }
+  // one staging buffer: fractions | E | z
+  const size_t bf = fr.size() * sizeof(GfFrac), be = (size_t)std::max<int64_t>(np, 1) * 8;
+  std::vector<unsigned char> hb(bf + 2 * be);
+  memcpy(hb.data(), fr.data(), bf);
+  if (np) {
+    memcpy(hb.data() + bf, E, np * 8);
+    memcpy(hb.data() + bf + be, z, np * 8);
+  }
+  hipStream_t st = (hipStream_t)stream;
+  void* d = nullptr;
+  HIPCK(hipMallocAsync(&d, hb.size(), st));
+  HIPCK(hipMemcpyAsync(d, hb.data(), hb.size(), hipMemcpyHostToDevice, st));
+  const unsigned char* db = (const unsigned char*)d;
+  const int nt = lmats + lreal;
+  hipLaunchKernelGGL(k_gf_poles, dim3((nt + kBlock - 1) / kBlock), dim3(kBlock), 0, st, (const GfFrac*)db, nfrac,
+                     (const double*)(db + bf), (const double*)(db + bf + be), wm, lmats, wr, lreal, eps,
+                     (double2*)gm, (double2*)gr);
+  const hipError_t le = hipGetLastError();
+  (void)hipFreeAsync(d, st);
+  // the host staging vector dies on return: the copy must have completed
+  HIPCK(hipStreamSynchronize(st));
+  HIPCK(le);
   return ED_OK;
 }
 

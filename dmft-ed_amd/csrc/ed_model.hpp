@@ -398,4 +398,183 @@ ED_HD void gen_row(const EdModel& M, uint32_t m, Acc& acc) {
   }
 }
 
+// -------------------------------------------------- symbolic row generator
+// The off-diagonal terms of gen_row as state-independent candidates, in the
+// same order: candidate c acts on a state m iff (m & req_mask) == req_val;
+// its element is then (re, im) * sign at the row of m ^ flip, with the
+// Jordan-Wigner sign of the operator string o_1 .. o_n (applied in that
+// order, o_j at bit p_j):
+//   sign = (-1)^( popc(m & smask) + c0 ),  smask = XOR_j (2^p_j - 1),
+//   c0 = #{ i < j : p_i < p_j }  (each earlier flip below p_j changes the
+//   parity that jw_sign(state_{j-1}, p_j) counts by one).
+// (re, im) is gen_row's value before the signs (hr, -hi); multiplying by the
+// +-1 factors in any grouping gives the same bits.  gen_row passes a literal
+// 0.0 imaginary part for the two- and four-operator interaction terms (Jx,
+// Jp, superc pairs, nonSU2 spin-flip hybridisation): im_signed = 0 keeps it
+// unsigned there.  The matrix-free kernel
+// (k_direct) evaluates these per lane instead of re-running gen_row's
+// branchy loops; direct_candidates_check compares the two on sample states.
+struct DirCand {
+  uint32_t req_mask, req_val, flip, smask;
+  int32_t c0, im_signed;
+  double re, im;
+};
+
+struct CandBuilder {
+  DirCand c{};
+  uint32_t need1 = 0, need0 = 0;
+  int pos[4];
+  int nops = 0;
+  bool ok = true;
+  void req(int b, int v) {
+    const uint32_t m = 1u << b;
+    if (v) { ok = ok && !(need0 & m); need1 |= m; }
+    else { ok = ok && !(need1 & m); need0 |= m; }
+  }
+  void op(int p) { pos[nops++] = p; }
+  bool finish(double re, double im, bool im_signed = false) {
+    if (!ok) return false;  // contradictory bit conditions: gen_row never fires
+    c.req_mask = need1 | need0;
+    c.req_val = need1;
+    c.flip = 0;
+    c.smask = 0;
+    int c0 = 0;
+    for (int j = 0; j < nops; j++) {
+      c.flip ^= 1u << pos[j];
+      c.smask ^= pos[j] == 0 ? 0u : ((1u << pos[j]) - 1u);
+      for (int i = 0; i < j; i++) c0 += pos[i] < pos[j];
+    }
+    c.c0 = c0 & 1;
+    c.im_signed = im_signed ? 1 : 0;
+    c.re = re;
+    c.im = im;
+    return true;
+  }
+};
+
+// Host: the candidates of gen_row (identical loop structure and conditions).
+template <class Vec>
+inline void direct_candidates(const EdModel& M, Vec& out) {
+  const int ns = M.ns, norb = M.norb, nbath = M.nbath, S = M.S;
+  auto hop = [&](int a, int b, double re, double im, bool signed_im = true) {  // c+_a c_b: bit b = 1, bit a = 0
+    CandBuilder cb;
+    cb.req(b, 1);
+    cb.req(a, 0);
+    cb.op(b);
+    cb.op(a);
+    if (cb.finish(re, im, signed_im)) out.push_back(cb.c);
+  };
+  // stored/Himp.f90:27-72
+  for (int io = 0; io < norb; io++)
+    for (int jo = 0; jo < norb; jo++) {
+      double hr = M.hloc_re[0][0][io][jo], hi = M.hloc_im[0][0][io][jo];
+      if (hr != 0.0 || hi != 0.0) hop(io, jo, hr, -hi);
+      hr = M.hloc_re[S][S][io][jo];
+      hi = M.hloc_im[S][S][io][jo];
+      if (hr != 0.0 || hi != 0.0) hop(io + ns, jo + ns, hr, -hi);
+    }
+  // stored/Himp.f90:74-104
+  if (M.mode == ED_MODE_NONSU2)
+    for (int is = 0; is < 2; is++) {
+      const int js = 1 - is;
+      for (int io = 0; io < norb; io++)
+        for (int jo = 0; jo < norb; jo++) {
+          const double hr = M.hloc_re[is][js][io][jo], hi = M.hloc_im[is][js][io][jo];
+          if (hr != 0.0 || hi != 0.0) hop(io + is * ns, jo + js * ns, hr, -hi);
+        }
+    }
+  // stored/Hint.f90:169-229
+  if (norb > 1 && M.jhflag) {
+    for (int io = 0; io < norb; io++)
+      for (int jo = 0; jo < norb; jo++) {
+        if (io == jo) continue;
+        CandBuilder cb;
+        cb.req(jo, 1); cb.req(io + ns, 1); cb.req(jo + ns, 0); cb.req(io, 0);
+        cb.op(jo); cb.op(io + ns); cb.op(jo + ns); cb.op(io);
+        if (cb.finish(M.jx, 0.0)) out.push_back(cb.c);
+      }
+    for (int io = 0; io < norb; io++)
+      for (int jo = 0; jo < norb; jo++) {
+        if (io == jo) continue;
+        CandBuilder cb;
+        cb.req(jo, 1); cb.req(jo + ns, 1); cb.req(io + ns, 0); cb.req(io, 0);
+        cb.op(jo); cb.op(jo + ns); cb.op(io + ns); cb.op(io);
+        if (cb.finish(M.jp, 0.0)) out.push_back(cb.c);
+      }
+  }
+  // stored/Hbath.f90:52-135
+  if (M.bath == ED_BATH_REPLICA) {
+    for (int k = 0; k < nbath; k++)
+      for (int io = 0; io < norb; io++)
+        for (int jo = 0; jo < norb; jo++)
+          for (int sp = 0; sp < 2; sp++) {
+            const int ss = sp == 0 ? 0 : S;
+            const double hr = M.hb_re[ss][ss][io][jo][k], hi = M.hb_im[ss][ss][io][jo][k];
+            if (hr != 0.0 || hi != 0.0) hop(M.stride[io][k] + sp * ns, M.stride[jo][k] + sp * ns, hr, -hi);
+          }
+    if (M.mode == ED_MODE_NONSU2)
+      for (int k = 0; k < nbath; k++)
+        for (int is = 0; is < 2; is++) {
+          const int js = 1 - is;
+          for (int io = 0; io < norb; io++)
+            for (int jo = 0; jo < norb; jo++) {
+              const double hr = M.hb_re[is][js][io][jo][k], hi = M.hb_im[is][js][io][jo][k];
+              if (hr != 0.0 || hi != 0.0) hop(M.stride[io][k] + is * ns, M.stride[jo][k] + js * ns, hr, -hi);
+            }
+        }
+  }
+  // stored/Hbath.f90:142-178
+  if (M.mode == ED_MODE_SUPERC)
+    for (int o = 0; o < M.ne; o++)
+      for (int k = 0; k < nbath; k++) {
+        const int ms = M.stride[o][k];
+        const double dd = M.d[0][o][k];
+        if (dd == 0.0) continue;
+        {
+          CandBuilder cb;
+          cb.req(ms, 1); cb.req(ms + ns, 1);
+          cb.op(ms); cb.op(ms + ns);
+          if (cb.finish(dd, 0.0)) out.push_back(cb.c);
+        }
+        {
+          CandBuilder cb;
+          cb.req(ms, 0); cb.req(ms + ns, 0);
+          cb.op(ms + ns); cb.op(ms);
+          if (cb.finish(dd, 0.0)) out.push_back(cb.c);
+        }
+      }
+  // stored/Himp_bath.f90:192-249
+  for (int o = 0; o < norb; o++)
+    for (int k = 0; k < nbath; k++) {
+      const int ms = M.stride[o][k];
+      for (int sp = 0; sp < 2; sp++) {
+        const int ss = sp == 0 ? 0 : S;
+        const double hr = M.hyb_re[ss][o][k], hi = M.hyb_im[ss][o][k];
+        if (hr == 0.0 && hi == 0.0) continue;
+        const int a = o + sp * ns, b = ms + sp * ns;
+        hop(b, a, hr, -hi);  // bit a = 1, bit b = 0: c+_b c_a
+        hop(a, b, hr, -hi);  // bit a = 0, bit b = 1: c+_a c_b
+      }
+    }
+  // stored/Himp_bath.f90:253-310 (no u /= 0 test)
+  if (M.mode == ED_MODE_NONSU2 && M.bath != ED_BATH_REPLICA)
+    for (int o = 0; o < norb; o++)
+      for (int k = 0; k < nbath; k++) {
+        const int ms = M.stride[o][k];
+        const double uu = M.u[0][o][k], ud = M.u[S][o][k];
+        hop(ms + ns, o, uu, 0.0, false);
+        hop(o, ms + ns, uu, 0.0, false);
+        hop(ms, o + ns, ud, 0.0, false);
+        hop(o + ns, ms, ud, 0.0, false);
+      }
+}
+
+// Evaluate candidate c on state m: true if it fires; target state, sign.
+ED_HD bool cand_apply(const DirCand& c, uint32_t m, uint32_t* k, double* sg) {
+  if ((m & c.req_mask) != c.req_val) return false;
+  *k = m ^ c.flip;
+  *sg = ((__builtin_popcount(m & c.smask) + c.c0) & 1) ? -1.0 : 1.0;
+  return true;
+}
+
 }  // namespace edg

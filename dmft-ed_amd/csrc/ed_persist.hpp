@@ -262,25 +262,59 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
       }
     }
   }
-  // --- MODE 4: Kronecker register layout (real H, real vectors).  Up-hop
-  // list (target rank as a byte offset inside the V row, value) once per
-  // thread; down-hop entries (LDS byte address, value) and the diagonal per
-  // row; no dictionary, no matrix byte in LDS.
+  // --- MODE 4: Kronecker register layout (real H).  Up-hop list (target
+  // rank as a byte offset inside the V row, value) once per thread; down-hop
+  // entries (LDS byte address, value) and the diagonal per row; no
+  // dictionary, no matrix byte in LDS.  Complex vectors (the reference's
+  // complex(8) arithmetic on a real H): 1024-thread workgroups, the down-hop
+  // values read from a [slot][iw] table behind the vector in LDS (lanes of
+  // one iw broadcast) instead of registers, whose budget the complex w and
+  // p take.
   constexpr bool KR = MODE == 4;
+  constexpr bool KRV = KR && VC;
   int ucol[KR ? E : 1];
-  double uval[KR ? E : 1];
+  double uval[(KR && !VC) ? E : 1];
   int dcol[KR ? RPT * E : 1];
-  double dval[KR ? RPT * E : 1];
-  double dgr[KR ? RPT : 1];
+  double dval[(KR && !VC) ? RPT * E : 1];
+  double dgr[(KR && !VC) ? RPT : 1];
+  const double* sdv = nullptr;   // KRV: down-hop values [e * dd + iw]
+  const double* suv = nullptr;   // KRV: up-hop values [e * du + iu] (reordered lists)
+  const double* sdg = nullptr;   // KRV: diagonal [VROWS] (padding rows 0)
+  int giw = 0;                   // KR: g of the thread (row slot r has iw = g + G*r)
   if constexpr (KR) {
     const int du = a.kdu, dd = a.kdd, G = NT / du;
     const bool act = tid < G * du;
     const int g = act ? tid / du : 0;
+    giw = g;
+    if constexpr (KRV) {
+      // LDS: vector | diagonal | down-hop values
+      double* tg = (double*)(smem + (((int64_t)VROWS * sizeof(V) + 15) & ~(int64_t)15));
+      for (int x = tid; x < VROWS; x += NT) {
+        double d = 0.0;
+        if (x < dim) {
+          if (a.kdiag) {
+            d = a.kdiag[x];
+          } else {
+            const KronArgs<HC>& K = a.K;
+            const int xw = x / du, xu = x - xw * du;
+            d = re_of(add(add(K.aup[xu], K.adw[xw]), mk<HC>(K.uimp[K.impu[xu] * K.nimp + K.impd[xw]], 0.0)));
+          }
+        }
+        tg[x] = d;
+      }
+      double* t = tg + VROWS;
+      for (int x = tid; x < E * dd; x += NT) t[x] = x < a.kdegd * dd ? a.kdwv[x] : 0.0;
+      double* tu = t + E * dd;
+      for (int x = tid; x < E * du; x += NT) tu[x] = x < a.kdegu * du ? a.kupv[x] : 0.0;
+      sdg = tg;
+      sdv = t;
+      suv = tu;
+    }
 #pragma unroll
     for (int e = 0; e < E; e++) {
       const bool ok = act && e < a.kdegu;
       ucol[e] = ok ? a.kupc[e * du + q.iu] * (int)sizeof(V) : 0;
-      uval[e] = ok ? a.kupv[e * du + q.iu] : 0.0;
+      if constexpr (!KRV) uval[e] = ok ? a.kupv[e * du + q.iu] : 0.0;
     }
 #pragma unroll
     for (int r = 0; r < RPT; r++) {
@@ -289,19 +323,27 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
 #pragma unroll
       for (int e = 0; e < E; e++) {
         const bool ok = okr && e < a.kdegd;
-        dcol[r * E + e] = (ok ? a.kdwc[e * dd + iw] * du + q.iu : 0) * (int)sizeof(V);
-        dval[r * E + e] = ok ? a.kdwv[e * dd + iw] : 0.0;
-      }
-      double d = 0.0;
-      if (okr) {
-        if (a.kdiag) {
-          d = a.kdiag[PROW(r)];
+        if constexpr (KRV) {
+          // padding slots gather the row's own (zero) padding entry, valid
+          // rows beyond their degree a zero table value
+          dcol[r * E + e] = (ok ? a.kdwc[e * dd + iw] * du + q.iu : (okr ? 0 : PROW(r))) * (int)sizeof(V);
         } else {
-          const KronArgs<HC>& K = a.K;
-          d = re_of(add(add(K.aup[q.iu], K.adw[iw]), mk<HC>(K.uimp[K.impu[q.iu] * K.nimp + K.impd[iw]], 0.0)));
+          dcol[r * E + e] = (ok ? a.kdwc[e * dd + iw] * du + q.iu : 0) * (int)sizeof(V);
+          dval[r * E + e] = ok ? a.kdwv[e * dd + iw] : 0.0;
         }
       }
-      dgr[r] = d;
+      if constexpr (!KRV) {
+        double d = 0.0;
+        if (okr) {
+          if (a.kdiag) {
+            d = a.kdiag[PROW(r)];
+          } else {
+            const KronArgs<HC>& K = a.K;
+            d = re_of(add(add(K.aup[q.iu], K.adw[iw]), mk<HC>(K.uimp[K.impu[q.iu] * K.nimp + K.impd[iw]], 0.0)));
+          }
+        }
+        dgr[r] = d;
+      }
     }
   }
 
@@ -465,14 +507,28 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
           acc = fmac(acc, h, vl[x & kPkColMask]);
         }
       } else if constexpr (KR) {
-        acc = mul(dgr[r], ur);
+        if constexpr (KRV) acc = mul(sdg[i], ur);
+        else acc = mul(dgr[r], ur);
         {
         const unsigned char* rb = (const unsigned char*)(vl + (i - q.iu));  // row iw of V
+        if constexpr (KRV) {
+          // idle lanes (tid >= G*DimUp) read table column 0 with ucol = 0: their row base is a zero padding row
 #pragma unroll
-        for (int e = 0; e < E; e++) acc = fmac(acc, uval[e], *(const V*)(rb + ucol[e]));
+          for (int e = 0; e < E; e++) acc = fmac(acc, suv[e * a.kdu + q.iu], *(const V*)(rb + ucol[e]));
+        } else {
 #pragma unroll
-        for (int e = 0; e < E; e++)
-          acc = fmac(acc, dval[r * E + e], *(const V*)((const unsigned char*)vl + dcol[r * E + e]));
+          for (int e = 0; e < E; e++) acc = fmac(acc, uval[e], *(const V*)(rb + ucol[e]));
+        }
+        if constexpr (KRV) {
+          const int iwc = min(giw + (NT / a.kdu) * r, a.kdd - 1);
+#pragma unroll
+          for (int e = 0; e < E; e++)
+            acc = fmac(acc, sdv[e * a.kdd + iwc], *(const V*)((const unsigned char*)vl + dcol[r * E + e]));
+        } else {
+#pragma unroll
+          for (int e = 0; e < E; e++)
+            acc = fmac(acc, dval[r * E + e], *(const V*)((const unsigned char*)vl + dcol[r * E + e]));
+        }
         }
       } else {
         acc = vzero<V>();

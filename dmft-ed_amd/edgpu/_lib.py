@@ -36,6 +36,7 @@ SIGNATURES = {
     "ed_sector_hxv_dev": ([_P, _i32, _P, _P, _P], ctypes.c_int),
     "ed_sector_hxv_dev_path": ([_P, _i32, _i32, _P, _P, _P], ctypes.c_int),
     "ed_sector_hxv": ([_P, _i32, _P, _P], ctypes.c_int),
+    "ed_sector_col_mask": ([_P, _P, _P], ctypes.c_int),
     "ed_sector_map": ([_P, _P], ctypes.c_int),
     "ed_sector_dump_csr": ([_P, _P, _P, _P], ctypes.c_int),
     "ed_sector_lanc_tridiag": ([_P, _i32, _P, _i32, _f64, _P, _P, _P], ctypes.c_int),
@@ -51,7 +52,9 @@ SIGNATURES = {
     "ed_sector_apply_op_acc": ([_P, _P, _i32, _i32, _f64, _f64, _i32, _P, _P, _P], ctypes.c_int),
     "ed_sector_lanc_tridiag_dev": ([_P, _i32, _P, _i32, _f64, _P, _P, _P], ctypes.c_int),
     "ed_sector_lanc_tridiag_batch": ([_P, _i32, _i32, _P, _i32, _f64, _P, _P, _P], ctypes.c_int),
-    "ed_tridiag_poles": ([_i32, _P, _P, _P, _P], ctypes.c_int),
+    "ed_tridiag_poles": ([_i32, _P, _P, _P, _P, _P], ctypes.c_int),
+    "ed_gf_add_poles": ([_i32, _P, _P, _P, _P, _P, _P, _P, _P, _i32, _P, _i32, _f64, _P, _P, _P],
+                        ctypes.c_int),
     "ed_gpu_init": ([_P], ctypes.c_int),
     "ed_gpu_set_device": ([_i32], ctypes.c_int),
     "ed_gpu_build_sector": ([_i32, _i32, _i32, _P], ctypes.c_int),

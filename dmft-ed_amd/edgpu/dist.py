@@ -28,8 +28,13 @@ scalars per step.
 
 Any other sector (superc, nonsu2, Jx/Jp, Jz_basis ...) uses `DistRowSector`:
 the reference's own layout — each rank builds rows [r0, r0+n) of the stored
-(or matrix-free generic) H on its GPU (ed_sector_create_rows) and all-gathers
-the vector before each product, exactly spMatVec_mpi_cc's Allgatherv.
+(or matrix-free generic) H on its GPU (ed_sector_create_rows).  Instead of
+spMatVec_mpi_cc's whole-vector Allgatherv it exchanges a halo: at
+construction every rank lists the columns its rows refer to
+(ed_sector_col_mask), sends each owner the list of its entries it needs, and
+per H·v one all-to-all moves exactly those entries, scattered into a
+full-length scratch vector before the local product (same values at every
+column the rows read: bit-identical to the Allgatherv product).
 
 The collective backend is the default process group (nccl = RCCL on the GPU
 box; gloo in the CPU tests, where `ops` injects reference factor products).
@@ -246,13 +251,18 @@ class DistRowSector:
     """One sector split by rows over the ranks of the default process group,
     any ed_mode (build_Hv_sector with MpiStatus, ED_HAMILTONIAN.f90:55-62,
     `mpi_split`).
-    Vectors are 1-D tensors holding this rank's rows; H·v all-gathers the
-    whole vector (spMatVec_mpi_cc STORED_HxV.f90:147-197) and applies the
-    local rows with global columns.  `hxv_rows` (injectable, CPU tests)
-    maps a whole vector to the local rows of H·v."""
+    Vectors are 1-D tensors holding this rank's rows; H·v applies the local
+    rows with global columns to a full-length vector that holds this rank's
+    entries and the halo — the entries of other ranks its rows refer to,
+    received by one all-to-all (halo=True, default) — or the whole
+    all-gathered vector (halo=False: spMatVec_mpi_cc's Allgatherv,
+    STORED_HxV.f90:175-189).  `hxv_rows` (injectable, CPU tests) maps a
+    whole vector to the local rows of H·v; `cols_needed` then lists the
+    global columns those rows refer to."""
 
     def __init__(self, cfg=None, q1: int = 0, q2: int = 0, *, device: int = 0, real: Optional[bool] = None,
-                 stored: bool = True, hxv_rows=None, dim: Optional[int] = None, dtype=None):
+                 stored: bool = True, hxv_rows=None, dim: Optional[int] = None, dtype=None,
+                 halo: bool = True, cols_needed=None):
         import torch
 
         dist = _dist()
@@ -276,6 +286,14 @@ class DistRowSector:
                 y = torch.empty(S.nrows, dtype=v.dtype, device=v.device)
                 S.hxv_dev(v, y)
                 return y
+
+            if halo and self.world > 1:
+                mask = torch.empty((dim + 31) // 32, dtype=torch.int32, device=self.device)
+                st = torch.cuda.current_stream(self.device)
+                check(_lib.load().ed_sector_col_mask(S.handle, ctypes.c_void_p(mask.data_ptr()),
+                                                     ctypes.c_void_p(st.cuda_stream)), "ed_sector_col_mask")
+                bits = np.unpackbits(mask.cpu().numpy().view(np.uint8), bitorder="little")
+                cols_needed = np.flatnonzero(bits[:dim])
         else:
             self.dtype = dtype or torch.complex128
             self.device = torch.device("cpu")
@@ -283,6 +301,59 @@ class DistRowSector:
         self.r0, self.n = mpi_split(dim, self.world)
         self._rows = hxv_rows
         self.comm_cpu = dist is not None and dist.get_backend() != "nccl"
+        self.halo = bool(halo and self.world > 1)
+        if self.halo:
+            if cols_needed is None:
+                raise ValueError("halo exchange needs the columns the local rows refer to")
+            self._setup_halo(np.asarray(cols_needed, dtype=np.int64))
+
+    # ----------------------------------------------------------------- halo
+    def _a2a(self, send, in_splits, out_splits):
+        import torch
+
+        dist = _dist()
+        recv = torch.empty(sum(out_splits), dtype=send.dtype, device=send.device)
+        if self.comm_cpu:
+            r = recv.cpu()
+            dist.all_to_all_single(r, send.cpu(), output_split_sizes=out_splits, input_split_sizes=in_splits)
+            return r.to(send.device)
+        dist.all_to_all_single(recv, send, output_split_sizes=out_splits, input_split_sizes=in_splits)
+        return recv
+
+    def _setup_halo(self, cols):
+        """Who needs which of my entries: every rank sends each owner the
+        (sorted) global columns it needs from it; the owner keeps them as
+        local indices.  Two all-to-alls, once per sector."""
+        import torch
+
+        P, r = self.world, self.rank
+        lo, hi = self.r0[r], self.r0[r] + self.n[r]
+        cols = np.unique(cols)
+        cols = cols[(cols < lo) | (cols >= hi)]
+        starts = np.asarray(self.r0, dtype=np.int64)
+        owner = np.searchsorted(starts, cols, side="right") - 1
+        need = [cols[owner == q] for q in range(P)]
+        cnt = torch.tensor([len(x) for x in need], dtype=torch.int64, device=self.device)
+        got = self._a2a(cnt, [1] * P, [1] * P).cpu().numpy()
+        req = torch.from_numpy(np.concatenate(need).astype(np.int64)).to(self.device)
+        want = self._a2a(req, [len(x) for x in need], [int(c) for c in got])
+        self._send_idx = (want - lo).to(torch.int64)           # my entries, grouped by destination rank
+        self._send_splits = [int(c) for c in got]
+        self._recv_splits = [len(x) for x in need]
+        self._halo_cols = req                                    # global columns, in arrival order
+        self._xfull = None
+        self.halo_size = int(req.numel())
+
+    def _with_halo(self, x):
+        import torch
+
+        if self._xfull is None or self._xfull.dtype != x.dtype:
+            self._xfull = torch.zeros(self.dim, dtype=x.dtype, device=x.device)
+        recv = self._a2a(x.index_select(0, self._send_idx), self._send_splits, self._recv_splits)
+        r0, n = self.local_rows
+        self._xfull[r0:r0 + n] = x
+        self._xfull.index_copy_(0, self._halo_cols, recv)
+        return self._xfull
 
     @property
     def local_rows(self) -> Tuple[int, int]:
@@ -317,6 +388,8 @@ class DistRowSector:
         return torch.cat([p[:k] for p, k in zip(parts, self.n)])
 
     def hxv(self, x):
+        if self.halo:
+            return self._rows(self._with_halo(x))
         return self._rows(self.gather(x))
 
     def close(self):

@@ -16,7 +16,10 @@ G_{aa,ss}.  Per kept state |gs> (energy E_i), orbital a, spin s:
     G(iw_n) += w/(iw_n - isign*(E_j - E_i)), G(w) += w/(w + i eps - isign*(E_j - E_i))
     with w_n = pi/beta (2n-1) and w = linspace(wini, wfin, Lreal)
     (allocate_grids, ED_AUX_FUNX.f90:449-461).
-The pole sum runs in torch on the GPU (200 poles x 10^4 frequencies per seed).
+The pole sums of all seeds run in one device kernel (ed_gf_add_poles) into
+G arrays kept in HBM, in the serial job order and the reference's per-pole
+addition order; the frequency grids are uploaded once per build and G is
+copied to the host (or all-reduced on the device) once at the end.
 """
 from __future__ import annotations
 
@@ -65,38 +68,80 @@ def realaxis(wini: float, wfin: float, L: int) -> np.ndarray:
     return np.linspace(wini, wfin, L)
 
 
-def tridiag_poles(alfa: np.ndarray, beta: np.ndarray, n: int) -> Tuple[np.ndarray, np.ndarray]:
+def tridiag_poles(alfa: np.ndarray, beta: np.ndarray, n: int, first_row: bool = False):
     """Eigenvalues of tridiag(alfa(1:n), beta(2:n)) and squared first components
     (tql2 / eigh of add_to_lanczos_gf_*, ED_GF_NONSU2.f90:936, ED_GF_NORMAL.f90:
     612-618): `ed_tridiag_poles`, the implicit-QL iteration carrying only the
-    first row of the eigenvector matrix (O(n^2))."""
+    first row of the eigenvector matrix (O(n^2)).  first_row: return the
+    components Z(1,j) themselves instead of their squares."""
     a = np.ascontiguousarray(alfa[:n], dtype=np.float64)
     b = np.zeros(n, dtype=np.float64)
     b[1:n] = beta[1:n]
     E = np.empty(n, dtype=np.float64)
     z2 = np.empty(n, dtype=np.float64)
-    check(_lib.load().ed_tridiag_poles(n, a.ctypes.data, b.ctypes.data, E.ctypes.data, z2.ctypes.data),
-          "ed_tridiag_poles")
-    return E, z2
+    z1 = np.empty(n, dtype=np.float64)
+    check(_lib.load().ed_tridiag_poles(n, a.ctypes.data, b.ctypes.data, E.ctypes.data, z2.ctypes.data,
+                                       z1.ctypes.data), "ed_tridiag_poles")
+    return (E, z1) if first_row else (E, z2)
 
 
-def add_poles(G_mats, G_real, peso_bz: float, Ei: float, E: np.ndarray, z2: np.ndarray,
-              isign: int, wm: np.ndarray, wr: np.ndarray, eps: float) -> None:
-    """add_to_lanczos_gf_normal inner loops (ED_GF_NORMAL.f90:620-631), as one
-    (L x nlanc) broadcast on the GPU (no host fallback)."""
-    import torch
+class PoleSums:
+    """Device side of add_to_lanczos_gf_normal / _nonsu2 (ED_GF_NORMAL.f90:
+    620-631, ED_GF_NONSU2.f90:936-950): the frequency grids are uploaded once,
+    G lives in HBM as (Nspin, Nspin, Norb, L) complex arrays, and `add` queues
+    one continued fraction (its poles from ed_tridiag_poles) for component
+    (ispin, jspin, iorb).  `flush` sums every queued fraction in one launch of
+    ed_gf_add_poles, in queue order and pole by pole (the reference's order of
+    additions into G(i))."""
 
-    if not torch.cuda.is_available():
-        raise RuntimeError("add_poles: the Green's function pole sum runs on the GPU")
-    de = E - Ei
-    peso = peso_bz * z2
-    dev = "cuda"
-    iw = torch.from_numpy(1j * wm).to(dev)
-    rw = torch.from_numpy(wr + 1j * eps).to(dev)
-    p = torch.from_numpy(peso.astype(np.complex128)).to(dev)
-    d = torch.from_numpy((isign * de).astype(np.complex128)).to(dev)
-    G_mats += (p[None, :] / (iw[:, None] - d[None, :])).sum(1).cpu().numpy()
-    G_real += (p[None, :] / (rw[:, None] - d[None, :])).sum(1).cpu().numpy()
+    def __init__(self, nspin: int, norb: int, wm: np.ndarray, wr: np.ndarray, eps: float, device: int):
+        import torch
+
+        if not torch.cuda.is_available():
+            raise RuntimeError("the Green's function pole sum runs on the GPU (no host fallback)")
+        self.dev = torch.device("cuda", device)
+        self.nspin, self.norb, self.eps = nspin, norb, float(eps)
+        self.wm = torch.from_numpy(np.ascontiguousarray(wm, dtype=np.float64)).to(self.dev)
+        self.wr = torch.from_numpy(np.ascontiguousarray(wr, dtype=np.float64)).to(self.dev)
+        self.Gm = torch.zeros((nspin, nspin, norb, len(wm)), dtype=torch.complex128, device=self.dev)
+        self.Gr = torch.zeros((nspin, nspin, norb, len(wr)), dtype=torch.complex128, device=self.dev)
+        self._q = []
+
+    def add(self, comp, peso_bz, Ei: float, E: np.ndarray, z: np.ndarray, isign: int) -> None:
+        ispin, jspin, iorb = comp
+        c = (ispin * self.nspin + jspin) * self.norb + iorb
+        pb = complex(peso_bz)
+        self._q.append((c, pb.real, pb.imag, float(Ei), int(isign), np.asarray(E, np.float64),
+                        np.asarray(z, np.float64)))
+
+    def flush(self) -> None:
+        import torch
+
+        if not self._q:
+            return
+        q, self._q = self._q, []
+        npole = np.array([len(t[5]) for t in q], dtype=np.int32)
+        E = np.ascontiguousarray(np.concatenate([t[5] for t in q]))
+        z = np.ascontiguousarray(np.concatenate([t[6] for t in q]))
+        pb = np.ascontiguousarray(np.array([[t[1], t[2]] for t in q], dtype=np.float64).reshape(-1))
+        ei = np.array([t[3] for t in q], dtype=np.float64)
+        sg = np.array([t[4] for t in q], dtype=np.int32)
+        comp = np.array([t[0] for t in q], dtype=np.int32)
+        st = torch.cuda.current_stream(self.dev)
+        P = ctypes.c_void_p
+        check(_lib.load().ed_gf_add_poles(len(q), P(npole.ctypes.data), P(E.ctypes.data), P(z.ctypes.data),
+                                          P(pb.ctypes.data), P(ei.ctypes.data), P(sg.ctypes.data),
+                                          P(comp.ctypes.data), P(self.wm.data_ptr()), self.wm.numel(),
+                                          P(self.wr.data_ptr()), self.wr.numel(), self.eps,
+                                          P(self.Gm.data_ptr()), P(self.Gr.data_ptr()), P(st.cuda_stream)),
+              "ed_gf_add_poles")
+
+    def to_host(self, Gm: np.ndarray, Gr: np.ndarray) -> None:
+        """Add the device G into the host (Nspin, Nspin, Norb, Norb, L) arrays."""
+        gm, gr = self.Gm.cpu().numpy(), self.Gr.cpu().numpy()
+        for o in range(self.norb):
+            Gm[:, :, o, o] += gm[:, :, o]
+            Gr[:, :, o, o] += gr[:, :, o]
 
 
 def _seed(src: Sector, dst: Sector, op: int, terms, vec: np.ndarray, cplx: bool):
@@ -230,8 +275,8 @@ def _job_list(cfg: EDConfig, states: StateList):
     return jobs, pairs
 
 
-def _run_job(cfg, states, gopt, job, cache, wm, wr, G_m, G_r, record, zeta):
-    """One tridiagonalisation + pole sum (add_to_lanczos_gf_normal / _nonsu2)."""
+def _run_job(cfg, states, gopt, job, cache, poles, record, zeta):
+    """One tridiagonalisation; its poles are queued on `poles` (PoleSums)."""
     comp, tag, k, (op, isign, ispin, terms, weight), sec, jsec = job
     e_i, vec = states.energies[k], states.vectors[k]
     if vec is None:
@@ -244,11 +289,11 @@ def _run_job(cfg, states, gopt, job, cache, wm, wr, G_m, G_r, record, zeta):
     nlanc = min(HJ.dim, gopt.lanc_nGFiter)
     a, b, n = _tridiag_dev(HJ, seed, nlanc, not cplx, gopt.threshold)
     # the reference diagonalises all nlanc entries (unset ones stay 0)
-    E, z2 = tridiag_poles(a, b, nlanc)
+    E, z = tridiag_poles(a, b, nlanc, first_row=True)
     if record is not None:
         record.append(dict(channel=tag, isector=states.sectors[k], op=op, norm2=norm2, alfa=a, beta=b,
                            nlanc=n))
-    add_poles(G_m, G_r, weight * norm2 / zeta, e_i, E, z2, isign, wm, wr, gopt.eps)
+    poles.add(comp, weight * norm2 / zeta, e_i, E, z, isign)
 
 
 def _tridiag_batch(S: Sector, seeds, nlanc: int, real: bool, threshold: float):
@@ -266,11 +311,11 @@ def _tridiag_batch(S: Sector, seeds, nlanc: int, real: bool, threshold: float):
     return a, b, n
 
 
-def _run_jobs_batched(cfg, states, gopt, jobs, todo, device, wm, wr, Gm, Gr, zeta, record=None):
+def _run_jobs_batched(cfg, states, gopt, jobs, todo, device, poles, zeta, record=None):
     """The seed loop grouped by (target sector, vector type): each group's
-    seeds are built on the device, tridiagonalised in one batched launch, and
-    their pole sums computed per job exactly as _run_job; contributions are
-    added to G in job order (the serial loop's sequence of additions)."""
+    seeds are built on the device and tridiagonalised in one batched launch;
+    the poles are queued in job order (the serial loop's sequence of
+    additions)."""
     import torch
 
     torch.cuda.set_device(device)
@@ -283,7 +328,7 @@ def _run_jobs_batched(cfg, states, gopt, jobs, todo, device, wm, wr, Gm, Gr, zet
             raise ValueError("the Green's function needs the state vectors (keep_vectors=True)")
         cplx = (not cfg.is_real()) or is_complex_vector(vec) or any(np.imag(c) != 0 for _, c in terms)
         groups.setdefault((jsec.q1, jsec.q2, cplx), []).append(n)
-    contrib = {}
+    fracs = {}
     try:
         for (_, _, cplx), members in groups.items():
             live, seeds, norms = [], [], []
@@ -307,28 +352,22 @@ def _run_jobs_batched(cfg, states, gopt, jobs, todo, device, wm, wr, Gm, Gr, zet
             a, b, nl = _tridiag_batch(HJ, stacked, nlanc, not cplx, gopt.threshold)
             for q, n in enumerate(live):
                 comp, tag, k, (op, isign, ispin, terms, weight), sec, jsec = jobs[n]
-                E, z2 = tridiag_poles(a[q], b[q], nlanc)
+                E, z = tridiag_poles(a[q], b[q], nlanc, first_row=True)
                 if record is not None:
                     record.append((n, dict(channel=tag, isector=states.sectors[k], op=op, norm2=norms[q],
                                            alfa=a[q], beta=b[q], nlanc=int(nl[q]))))
-                c_m = np.zeros(gopt.Lmats, dtype=np.complex128)
-                c_r = np.zeros(gopt.Lreal, dtype=np.complex128)
-                add_poles(c_m, c_r, weight * norms[q] / zeta, states.energies[k], E, z2, isign, wm, wr, gopt.eps)
-                contrib[n] = (c_m, c_r)
+                fracs[n] = (comp, weight * norms[q] / zeta, states.energies[k], E, z, isign)
     finally:
         cache.close()
     for n in todo:
-        if n in contrib:
-            ispin, jspin, iorb = jobs[n][0]
-            Gm[ispin, jspin, iorb, iorb] += contrib[n][0]
-            Gr[ispin, jspin, iorb, iorb] += contrib[n][1]
+        if n in fracs:
+            poles.add(*fracs[n])
 
 
-def _run_jobs_threaded(cfg, states, gopt, jobs, todo, device, wm, wr, Gm, Gr, zeta):
+def _run_jobs_threaded(cfg, states, gopt, jobs, todo, device, poles, zeta):
     """The seed loop on `gopt.workers` host threads (one sector cache per
-    thread); each job's pole sum goes into its own zero arrays, which are then
-    added to G in job order — the same sequence of additions as the serial
-    loop."""
+    thread); each job's poles are queued in job order afterwards — the same
+    sequence of additions as the serial loop."""
     import threading
     from concurrent.futures import ThreadPoolExecutor
 
@@ -343,21 +382,25 @@ def _run_jobs_threaded(cfg, states, gopt, jobs, todo, device, wm, wr, Gm, Gr, ze
         with lock:
             caches.append(local.cache)
 
+    class _Rec:
+        def __init__(self):
+            self.q = []
+
+        def add(self, *a):
+            self.q.append(a)
+
     def work(n):
-        c_m = np.zeros(gopt.Lmats, dtype=np.complex128)
-        c_r = np.zeros(gopt.Lreal, dtype=np.complex128)
-        _run_job(cfg, states, gopt, jobs[n], local.cache, wm, wr, c_m, c_r, None, zeta)
-        return c_m, c_r
+        r = _Rec()
+        _run_job(cfg, states, gopt, jobs[n], local.cache, r, None, zeta)
+        return r.q
 
     order = sorted(todo, key=lambda n: -jobs[n][5].dim)   # longest first
     try:
         with ThreadPoolExecutor(max_workers=min(gopt.workers, len(todo)), initializer=init) as ex:
             futs = {n: ex.submit(work, n) for n in order}
             for n in todo:
-                c_m, c_r = futs[n].result()
-                ispin, jspin, iorb = jobs[n][0]
-                Gm[ispin, jspin, iorb, iorb] += c_m
-                Gr[ispin, jspin, iorb, iorb] += c_r
+                for fr in futs[n].result():
+                    poles.add(*fr)
     finally:
         for c in caches:
             c.close()
@@ -421,13 +464,14 @@ def build_gf(cfg: EDConfig, states: StateList, gopt: Optional[GFOptions] = None,
         mine = set(range(len(jobs)))
     zeta = float(states.size)       # T=0: zeta_function = state_list%size (ED_DIAG.f90:411)
     todo = [n for n in range(len(jobs)) if n in mine]
+    poles = PoleSums(Nsp, No, wm, wr, gopt.eps, device) if runner is None else None
     if runner is None and gopt.batch:
         rec = [] if record is not None else None
-        _run_jobs_batched(cfg, states, gopt, jobs, todo, device, wm, wr, Gm, Gr, zeta, rec)
+        _run_jobs_batched(cfg, states, gopt, jobs, todo, device, poles, zeta, rec)
         if record is not None:
             record.extend(r for _, r in sorted(rec, key=lambda t: t[0]))
     elif runner is None and record is None and gopt.workers > 1 and len(todo) > 1:
-        _run_jobs_threaded(cfg, states, gopt, jobs, todo, device, wm, wr, Gm, Gr, zeta)
+        _run_jobs_threaded(cfg, states, gopt, jobs, todo, device, poles, zeta)
     else:
         cache = _SectorCache(cfg, gopt, device)
         try:
@@ -436,19 +480,31 @@ def build_gf(cfg: EDConfig, states: StateList, gopt: Optional[GFOptions] = None,
                 ispin, jspin, iorb = job[0]
                 g_m, g_r = Gm[ispin, jspin, iorb, iorb], Gr[ispin, jspin, iorb, iorb]
                 if runner is None:
-                    _run_job(cfg, states, gopt, job, cache, wm, wr, g_m, g_r, record, zeta)
+                    _run_job(cfg, states, gopt, job, cache, poles, record, zeta)
                 else:
                     runner(cfg, states, gopt, job, wm, wr, g_m, g_r, zeta)
         finally:
             cache.close()
+    if poles is not None:
+        poles.flush()
     if world > 1:
         import torch
 
-        dev = torch.device("cuda", device) if dist.get_backend() == "nccl" else torch.device("cpu")
-        for G in (Gm, Gr):
-            t = torch.view_as_real(torch.from_numpy(G).to(dev))   # (re, im) pairs: plain f64 sum
-            dist.all_reduce(t)
-            G[...] = torch.view_as_complex(t).cpu().numpy()
+        if poles is not None and dist.get_backend() == "nccl":
+            for t in (poles.Gm, poles.Gr):            # device G, summed over ranks in HBM
+                dist.all_reduce(torch.view_as_real(t))
+        elif poles is not None:
+            for t in (poles.Gm, poles.Gr):
+                h = torch.view_as_real(t).cpu()
+                dist.all_reduce(h)
+                torch.view_as_real(t).copy_(h)
+        else:
+            for G in (Gm, Gr):
+                t = torch.view_as_real(torch.from_numpy(G))   # (re, im) pairs: plain f64 sum
+                dist.all_reduce(t)
+                G[...] = torch.view_as_complex(t).numpy()
+    if poles is not None:
+        poles.to_host(Gm, Gr)
     for ispin, jspin, iorb in pairs:               # build_gf_nonsu2 :35-48
         for G in (Gm, Gr):
             G[ispin, jspin, iorb, iorb] = 0.5 * (G[ispin, jspin, iorb, iorb]

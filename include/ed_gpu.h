@@ -172,6 +172,12 @@ int ed_sector_hxv_dev(ed_sector* s, int32_t vtype, const void* v, void* hv, void
  * stored kernel (0). -1 = default for the sector. */
 int ed_sector_hxv_dev_path(ed_sector* s, int32_t path, int32_t vtype, const void* v,
                            void* hv, void* stream);
+/* Columns the held rows refer to (the halo of a row-split sector,
+ * ed_sector_create_rows): mask_dev[(dim+31)/32] (device, zeroed here) gets bit
+ * c set for every column c of an off-diagonal element of the held rows.
+ * Async on `stream`.  edgpu.dist exchanges only these entries of the vector
+ * instead of the reference's whole-vector Allgatherv (STORED_HxV.f90:175-189). */
+int ed_sector_col_mask(const ed_sector* s, uint32_t* mask_dev, void* stream);
 /* Host-pointer H·v (synchronous, complex(8) vectors of length nloc = dim). */
 int ed_sector_hxv(ed_sector* s, int32_t nloc, const double* v, double* hv);
 
@@ -275,11 +281,26 @@ int ed_sector_lanc_tridiag_batch(ed_sector* s, int32_t vtype, int32_t nseed, con
                                  int32_t nitermax, double threshold, double* alfa, double* beta,
                                  int32_t* nlanc);
 /* GF poles of one continued fraction (host, O(n^2)): E[n] ascending eigenvalues
- * of tridiag(alfa[0:n], beta[1:n]) and z2[n] the squared first components of
- * their eigenvectors.  Replaces tql2 in add_to_lanczos_gf_nonsu2
- * (ED_GF_NONSU2.f90:936; ED_GF_SHARED.f90:76-214) and eigh in
- * add_to_lanczos_gf_normal (ED_GF_NORMAL.f90:612-618). */
-int ed_tridiag_poles(int32_t n, const double* alfa, const double* beta, double* E, double* z2);
+ * of tridiag(alfa[0:n], beta[1:n]), z2[n] the squared first components of
+ * their eigenvectors and (z1 != NULL) the first components themselves, Z(1,j).
+ * Replaces tql2 in add_to_lanczos_gf_nonsu2 (ED_GF_NONSU2.f90:936;
+ * ED_GF_SHARED.f90:76-214) and eigh in add_to_lanczos_gf_normal
+ * (ED_GF_NORMAL.f90:612-618). */
+int ed_tridiag_poles(int32_t n, const double* alfa, const double* beta, double* E, double* z2, double* z1);
+/* Pole sums of nfrac continued fractions into device-resident G, in list
+ * order — the inner loops of add_to_lanczos_gf_normal (ED_GF_NORMAL.f90:
+ * 620-631) and add_to_lanczos_gf_nonsu2 (ED_GF_NONSU2.f90:936-950): fraction
+ * f has npole[f] poles (E, z = Z(1,j): concatenated over fractions, host
+ * arrays), weight pesoBZ = peso_bz[2f] + i peso_bz[2f+1], energy Ei[f], sign
+ * isign[f] = +-1 and target component comp[f]; for every frequency
+ *   gm[comp][i] += (pesoBZ*z_j)*z_j / (i*wm[i] - isign*(E_j - Ei))
+ *   gr[comp][i] += (pesoBZ*z_j)*z_j / (wr[i] + i*eps - isign*(E_j - Ei))
+ * pole by pole (the reference's addition order).  gm (ncomp x lmats), gr
+ * (ncomp x lreal): complex(8) device arrays; wm[lmats], wr[lreal]: device.
+ * Synchronous on `stream` (the host pole data is staged). */
+int ed_gf_add_poles(int32_t nfrac, const int32_t* npole, const double* E, const double* z, const double* peso_bz,
+                    const double* Ei, const int32_t* isign, const int32_t* comp, const double* wm, int32_t lmats,
+                    const double* wr, int32_t lreal, double eps, double* gm, double* gr, void* stream);
 
 /* ------------------------------------------------------ reference-style API */
 int ed_gpu_init(const ed_params* p);          /* ed_init_solver parameter hand-over */

@@ -124,10 +124,15 @@ def _row_worker(rank, world, port, q):
 
     r0, cnt = mpi_split(n, world)
     Hloc = H[r0[rank]:r0[rank] + cnt[rank]]
-    ds = DistRowSector(hxv_rows=lambda v: torch.from_numpy(Hloc @ v.numpy()), dim=n)
+    rows = lambda v: torch.from_numpy(Hloc @ v.numpy())    # noqa: E731
+    ds = DistRowSector(hxv_rows=rows, dim=n, cols_needed=Hloc.indices)            # halo exchange
+    full = DistRowSector(hxv_rows=rows, dim=n, halo=False)                        # Allgatherv
     i = np.arange(1, n + 1, dtype=np.float64)
     x = torch.from_numpy(np.sin(i) + 1j * np.cos(3 * i))
-    y = ds.gather(ds.hxv(ds.scatter(x)))
+    yl = ds.hxv(ds.scatter(x))
+    assert torch.equal(yl, full.hxv(full.scatter(x)))        # bit-identical to the Allgatherv product
+    assert ds.halo_size < n - cnt[rank]                      # fewer entries than the whole vector
+    y = ds.gather(yl)
     err = float(np.max(np.abs(y.numpy() - H @ x.numpy())))
     a, b, nl = dist_lanczos(ds, ds.scatter(x), 40)
     ar, br, nr = lanc_tridiag((rp, cols, vals), x.numpy(), 40)
@@ -139,8 +144,9 @@ def _row_worker(rank, world, port, q):
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_gloo_row_split_matches_full(world):
-    """spMatVec_mpi_cc semantics on `world` gloo ranks: local rows, Allgatherv
-    of the vector, distributed plain Lanczos."""
+    """spMatVec_mpi_cc semantics on `world` gloo ranks: local rows, the halo
+    exchange (bit-identical to the Allgatherv of the vector), distributed plain
+    Lanczos."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()

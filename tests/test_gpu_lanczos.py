@@ -16,6 +16,8 @@ from oracle.oracle import Oracle, lanc_eigh, lanc_tridiag, start_vector
 
 pytestmark = pytest.mark.gpu
 
+torch = pytest.importorskip("torch")
+
 
 def _e0_scipy(csr, dim):
     A = sp.csr_matrix((csr[2], csr[1], csr[0]), shape=(dim, dim))
@@ -135,3 +137,56 @@ def test_c4_half_filled_ground_state_pin():
             e0, vec, n = S.lanc_eigh(nitermax=512, threshold=1e-12)
             assert abs(e0 - (-14.70964221)) < 5e-9
             assert abs(np.linalg.norm(vec) - 1.0) < 1e-10
+
+
+@pytest.mark.parametrize("direct", [False, True], ids=["stored", "direct"])
+def test_complex_vectors_kronecker_register_layout(direct):
+    """The reference's arithmetic — complex(8) vectors — on a real H through
+    the Kronecker register layout (persistent MODE 4, 1024-thread complex
+    form): alpha/beta (first 15 steps) and E0 against the oracle's complex
+    recurrence at 1e-10, and 40 steps against the multi-kernel one at 1e-9."""
+    from edgpu.hamiltonian import Sector
+    from cases import c2
+
+    cfg = c2()
+    orc = Oracle(cfg)
+    hmap = orc.build_sector(4, 4)
+    csr = orc.build_csr(hmap)
+    v0 = start_vector(len(hmap))
+    ar, br, nr = lanc_tridiag(csr, v0, 60)
+    kw = dict(stored=False, direct=True) if direct else dict(stored=True)
+    with Sector(cfg, 4, 4, real=True, **kw) as S:
+        assert S.lanc_mode(real=False) == 4
+        a, b, n = S.lanc_tridiag(v0, 60, real=False)
+        assert n == nr == 60
+        np.testing.assert_allclose(a[:15], ar[:15], rtol=1e-10, atol=1e-12)
+        np.testing.assert_allclose(b[:15], br[:15], rtol=1e-10, atol=1e-12)
+        e0, vec, _ = S.lanc_eigh(nitermax=512, threshold=1e-12, v0=v0, real=False)
+        eref, _, _ = lanc_eigh(csr, v0, 512)
+        assert abs(e0 - eref) <= 1e-10 * abs(eref)
+        assert vec.dtype == np.complex128 and abs(np.linalg.norm(vec) - 1.0) < 1e-10
+        S.set_options("no_persist")
+        a2, b2, n2 = S.lanc_tridiag(v0, 60, real=False)
+    np.testing.assert_allclose(a[:40], a2[:40], rtol=1e-9, atol=1e-11)
+    np.testing.assert_allclose(b[:40], b2[:40], rtol=1e-9, atol=1e-11)
+
+
+def test_complex_vectors_batched_mode4():
+    """Batched complex runs (one 1024-thread workgroup per start vector) give
+    each run's single-launch alpha/beta."""
+    from edgpu.gf import _tridiag_batch
+    from edgpu.hamiltonian import Sector
+    from cases import c2
+
+    with Sector(c2(), 4, 4, real=True, stored=True) as S:
+        assert S.lanc_mode(real=False) == 4
+        i = torch.arange(1, S.dim + 1, dtype=torch.float64, device="cuda:0")
+        seeds = torch.stack([torch.complex(torch.sin(k * i), torch.cos(3 * k * i)) for k in (1, 2, 3)])
+        seeds = seeds / seeds.abs().pow(2).sum(1, keepdim=True).sqrt()
+        torch.cuda.synchronize()
+        a, b, n = _tridiag_batch(S, seeds.contiguous(), 50, False, 0.0)
+        for k in range(3):
+            a1, b1, n1 = S.lanc_tridiag(seeds[k].cpu().numpy(), 50, 0.0, real=False)
+            assert n[k] == n1
+            np.testing.assert_array_equal(a[k], a1)
+            np.testing.assert_array_equal(b[k], b1)

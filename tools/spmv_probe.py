@@ -1,6 +1,6 @@
 """Launch one H·v kernel repeatedly on a chosen sector (for rocprofv3 runs).
 
-usage: python tools/spmv_probe.py [--sector n28|n28b|c4|c4r|c2] [--path 0|1|2] [--complex] [--iters N]
+usage: python tools/spmv_probe.py [--sector n28|n28b|n28j|n26s|c4|c4r|c2] [--path 0|1|2] [--complex] [--iters N]
 Prints the HIP-event average per launch on the launch stream.
 """
 import argparse
@@ -20,6 +20,9 @@ SECTORS = {
     "n28b": (dict(Norb=2, Nbath=6), (7, 7)),
     "c4": (dict(Norb=2, Nbath=5), (6, 6)),
     "c2": (dict(Norb=1, Nbath=7), (4, 4)),
+    # HBM-sized sectors without the Kronecker form (stored or generic matrix-free only)
+    "n28j": (dict(Norb=2, Nbath=6, Uloc=(2.0, 2.0, 0.0), Ust=1.0, Jh=0.5, Jx=0.5, Jp=0.5), (7, 7)),
+    "n26s": (dict(Norb=1, Nbath=12, Nspin=2, ed_mode="nonsu2"), (13, 0)),
 }
 
 ap = argparse.ArgumentParser()
