@@ -15,7 +15,9 @@ device matrix, sit in registers — DESIGN.md §1).  Beside it:
     words in registers (MODE 2, no Kronecker structure used);
   * direct_iters_per_s: configs[2], matrix-free tables (MODE 4 from the hop
     tables);
-  * complex_iters_per_s: complex(8) H and vectors (the reference's arithmetic);
+  * complex_iters_per_s: complex(8) vectors (the reference's arithmetic) on the
+    real(8) stored values of the same H (persistent MODE 4, 1024-thread complex
+    form); complex_h_iters_per_s: complex(8) H values and vectors (MODE 2);
   * validation: the lowest Ritz value of the last timed run's tridiagonal
     against the committed oracle E0 (tests/golden/c2_e0.json) at 1e-10.
 Sections (rank 0 prints, all ranks take part):
@@ -47,7 +49,7 @@ import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 GOLD = os.path.join(ROOT, "tests", "golden")
-PROFILES = os.path.join(ROOT, "profiles", "r2")
+PROFILES = os.path.join(ROOT, "profiles", "r3")
 
 
 def spmv_bytes_real(nnz, dim):
@@ -259,7 +261,7 @@ def _lanc_rate(S, niter, v0, reps=5, options=()):
     return niter / (min(r[2] for r in runs) * 1e-3), runs[-1]
 
 
-def bench_batched(S, v0, niter, last_alpha, ks=(256, 1024)):
+def bench_batched(S, v0, niter, last_alpha, ks=(256, 1024), cplx=False):
     """The whole chip on configs[1]: K independent Lanczos recurrences on the
     same sector in ONE persistent launch (ed_sector_lanc_tridiag_batch, one
     workgroup per start vector — how the Green's-function seeds of a target
@@ -272,14 +274,15 @@ def bench_batched(S, v0, niter, last_alpha, ks=(256, 1024)):
     out = {}
     for k in ks:
         seeds = v0.unsqueeze(0).repeat(k, 1)
-        seeds[1:] *= 1.0 + 0.05 * torch.rand(k - 1, v0.numel(), dtype=v0.dtype, device=v0.device, generator=g)
+        seeds[1:] *= 1.0 + 0.05 * torch.rand(k - 1, v0.numel(), dtype=torch.float64, device=v0.device, generator=g)
         seeds = seeds.contiguous()
-        _tridiag_batch(S, seeds, niter, True, 1e-300)
+        torch.cuda.synchronize()
+        _tridiag_batch(S, seeds, niter, not cplx, 1e-300)
         best = None
         for _ in range(3):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            a, b, n = _tridiag_batch(S, seeds, niter, True, 1e-300)
+            a, b, n = _tridiag_batch(S, seeds, niter, not cplx, 1e-300)
             dt = time.perf_counter() - t0
             best = dt if best is None else min(best, dt)
         dev = float(np.max(np.abs(a[0] - last_alpha[:niter])) / np.max(np.abs(last_alpha[:niter])))
@@ -287,20 +290,21 @@ def bench_batched(S, v0, niter, last_alpha, ks=(256, 1024)):
         out[str(k)] = {"iters_per_s": round(k * niter / best, 1), "wall_s": round(best, 5),
                        "alpha_seed0_rel_dev": dev}
     out["note"] = ("K start vectors on the configs[1] sector, one workgroup each, one launch "
-                   "(the headline value is ONE recurrence on one CU)")
+                   "(the headline value is ONE recurrence on one CU)" +
+                   ("; complex(8) vectors on the real(8) stored H (MODE 4, 1024 threads per run)" if cplx else ""))
     return out
 
 
 def _traffic(name):
     """Per-launch HBM-side bytes from a committed rocprofv3 summary
-    (profiles/r2/<name>.json: 2 x FETCH_SIZE + WRITE_SIZE, the gfx950 x2
+    (profiles/r3/<name>.json: 2 x FETCH_SIZE + WRITE_SIZE, the gfx950 x2
     calibrated for 4/8/16-B lane loads in profiles/r2/fetch_calib.json)."""
     f = os.path.join(PROFILES, name)
     if not os.path.exists(f):
         return None, None
     with open(f) as fh:
         tj = json.load(fh)
-    return tj.get("traffic_bytes_per_launch"), f"profiles/r2/{name}"
+    return tj.get("traffic_bytes_per_launch"), f"profiles/r3/{name}"
 
 
 def roofline_sweep(Sector, make_config):
@@ -342,8 +346,40 @@ def roofline_sweep(Sector, make_config):
         if two:
             row["matrix_free"]["two_pass_gbs"] = round(40 * dim / (msk * 1e-3) / 1e9, 1)
         out[name] = row
+    # HBM-sized sectors WITHOUT the Kronecker form: the stored kernel (real and
+    # complex H) and the generic matrix-free k_direct are the only paths
+    for name, kw, q in (("n28j", dict(Norb=2, Nbath=6, Uloc=(2.0, 2.0, 0.0), Ust=1.0, Jh=0.5, Jx=0.5, Jp=0.5),
+                         (7, 7)),
+                        ("n26s", dict(Norb=1, Nbath=12, Nspin=2, ed_mode="nonsu2"), (13, 0))):
+        cfg = make_config(bath="random", seed=SEED, **kw)
+        row = {}
+        for cplx in (False, True):
+            inf = {}
+            dim, nnz, ms = measure_hxv(Sector, cfg, q, 30, path=0, info=inf, cplx=cplx)
+            if inf["packed"]:
+                Bown = (spmv_bytes_packed_complex if cplx else spmv_bytes_packed)(inf["padded"], dim)
+            else:
+                Bown = (20 * nnz + 8 * (dim + 1) + 32 * dim) if cplx else spmv_bytes_real(nnz, dim)
+            tr, tsrc = _traffic(f"spmv_{name}{'_cplx' if cplx else ''}_traffic.json")
+            row["stored_complex" if cplx else "stored"] = {
+                "dim": dim, "nnz": nnz, "ms_per_launch": round(ms, 4), "bytes_per_launch": Bown,
+                "achieved": round(Bown / (ms * 1e-3) / 1e9, 1),
+                "frac": round(Bown / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                "traffic": tr, "traffic_source": tsrc,
+                "physical_gbs": round(tr / (ms * 1e-3) / 1e9, 1) if tr else None,
+                "kernel": ("k_spmv_pk" if inf["packed"] else "k_spmv") + ("<complex>" if cplx else "<real>")}
+        _, _, msd = measure_hxv(Sector, cfg, q, 20, path=1)
+        td, tdsrc = _traffic(f"direct_{name}_traffic.json")
+        row["direct_generic"] = {"ms_per_hxv": round(msd, 4),
+                                 "frac_16dim": round(16 * dim / (msd * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                 "traffic": td, "traffic_source": tdsrc,
+                                 "kernel": "k_direct (wave per 64-row chunk, op lists, LDS rank tables)"}
+        out[name] = row
     out["workloads"] = {"n28b": "Norb=2 Nbath=6 (Nlevels=28) (7,7) sector, random bath, real(8)",
-                        "c4_66": "configs[3] Norb=2 Nbath=5 half-filled (6,6) sector, random bath, real(8)"}
+                        "c4_66": "configs[3] Norb=2 Nbath=5 half-filled (6,6) sector, random bath, real(8)",
+                        "n28j": "Norb=2 Nbath=6 (Nlevels=28) (7,7) with Jx=Jp=0.5 (no Kronecker form), random bath",
+                        "n26s": "nonSU2 Norb=1 Nbath=12 (Nlevels=26) N=13 sector (spin flips: no Kronecker form), "
+                                "random bath"}
     return out
 
 
@@ -434,10 +470,12 @@ def main():
     # configs[1] with the stored matrix as ELL words in registers (MODE 2, no
     # Kronecker structure), complex(8) arithmetic, and configs[2] matrix-free
     mode2_ips, _ = _lanc_rate(S, args.niter, v0, options=("no_pkron",))
+    vc = torch.complex(v0, torch.cos(3 * torch.arange(1, S.dim + 1, dtype=torch.float64, device="cuda")))
+    cplx_ips, (ac, bc_, _) = _lanc_rate(S, args.niter, vc)
+    cplx_mode = S.lanc_mode(real=False, path=0)
     with Sector(cfg, 4, 4, stored=True, direct=False, real=False, device=dev) as Sc:
-        vc = v0.to(torch.complex128)
-        cplx_ips, _ = _lanc_rate(Sc, args.niter, vc)
-        cplx_mode = Sc.lanc_mode(real=False, path=0)
+        cplxh_ips, _ = _lanc_rate(Sc, args.niter, vc)
+        cplxh_mode = Sc.lanc_mode(real=False, path=0)
     with Sector(cfg, 4, 4, stored=False, direct=True, real=True, device=dev) as Sd:
         direct_ips, _ = _lanc_rate(Sd, args.niter, v0)
         direct_mode = Sd.lanc_mode(real=True, path=2)
@@ -452,6 +490,7 @@ def main():
         dim2, nnz2, ms2 = measure_hxv(Sector, cfg, (4, 4), 2000)
         gbs2 = spmv_bytes_real(nnz2, dim2) / (ms2 * 1e-3) / 1e9
         batched = bench_batched(S, v0, args.niter, np.asarray(last[0]))
+        batched_c = bench_batched(S, vc, args.niter, np.asarray(ac), cplx=True)
         roof, kron = None, None
         if not args.no_roofline:
             cfg28 = make_config(Norb=1, Nbath=13, bath="random", seed=SEED)
@@ -494,7 +533,8 @@ def main():
             # generic matrix-free (any ed_mode) and complex(8) stored H·v on the same sector
             _, _, msd = measure_hxv(Sector, cfg28, (7, 7), 20, path=1)
             td, tdsrc = _traffic("direct_n28_traffic.json")
-            kron["direct_generic"] = {"ms_per_hxv": round(msd, 4), "kernel": "k_direct (row regenerated per H·v)",
+            kron["direct_generic"] = {"ms_per_hxv": round(msd, 4),
+                                      "kernel": "k_direct (wave per 64-row chunk, op lists, LDS rank tables)",
                                       "frac_16dim": round(Bk / (msd * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                                       "traffic": td, "traffic_source": tdsrc}
             infc = {}
@@ -537,8 +577,12 @@ def main():
             "direct_iters_per_s": round(direct_ips, 1),
             "direct_note": f"configs[2]: same sector, matrix-free hop tables (persistent MODE {direct_mode})",
             "complex_iters_per_s": round(cplx_ips, 1),
-            "complex_note": f"complex(8) H and vectors, stored (persistent MODE {cplx_mode}); dtype of cpu_baseline",
+            "complex_note": f"complex(8) vectors on the real(8) stored H (persistent MODE {cplx_mode}); the "
+                            "arithmetic of cpu_baseline (its H has zero imaginary parts)",
+            "complex_h_iters_per_s": round(cplxh_ips, 1),
+            "complex_h_note": f"complex(8) H values and vectors, stored (persistent MODE {cplxh_mode})",
             "batched_c2": batched,
+            "batched_c2_complex": batched_c,
             "spmv_gbs_c2": round(gbs2, 1),
             "spmv_ms_c2": round(ms2, 5),
             "farm_c4": farm,

@@ -783,15 +783,25 @@ __global__ void __launch_bounds__(kBlock) k_spmv_pk(const val_t<HC>* __restrict_
 // scalar loads.  Ops go in groups of kDirGroup with every gather of a group
 // issued before the group's terms are summed, in order, into the row: the
 // same products and additions as k_spmv, so H·v is bit-identical to the
-// stored kernel.  The diagonal is gen_row's own (its off-diagonal part is
-// dead code for DiagAcc).
+// stored kernel.  The diagonal is gen_row's own (gen_diag).  Every op of a
+// group is evaluated branch-free (a down-level op reads the rank table at its
+// own pattern and ignores it), so the group's LDS reads and gathers issue
+// back to back.
 constexpr int kDirBlock = 1024;
-constexpr int kDirGroup = 8;
+constexpr int kDirGroup = 4;
 struct DirOp {
   uint32_t req_mask, req_val, flip, smask;
   int32_t delta;  // UNI: target row - own row; LANE: first row of the target block
   int32_t kind;   // kDirLane | kDirC0 | kDirImSigned | kDirPad
   double re, im;  // UNI: sign applied; LANE: before the sign
+};
+// kDirGroup ops field by field in 64-byte lines: one group is three
+// s_load_dwordx16 and one wait (op by op, the struct's fields came in
+// dependent scalar loads: ~70 round trips per chunk)
+struct __align__(64) DirGroup {
+  uint32_t req_mask[kDirGroup], req_val[kDirGroup], flip[kDirGroup], smask[kDirGroup];
+  int32_t delta[kDirGroup], kind[kDirGroup], pad_[8];
+  double re[kDirGroup], im[kDirGroup];
 };
 constexpr int kDirLane = 1, kDirC0 = 2, kDirImSigned = 4, kDirPad = 8;
 struct DirChunk {
@@ -803,12 +813,6 @@ struct DirChunk {
   int32_t pad[2];
 };
 
-struct DiagAcc {
-  double re = 0.0, im = 0.0;
-  __device__ __forceinline__ void diag(double r, double i) { re = r; im = i; }
-  __device__ __forceinline__ void off(uint32_t, double, double) {}
-};
-
 __device__ __forceinline__ double flip_sign(double v, uint32_t neg) {
   return __longlong_as_double(__double_as_longlong(v) ^ ((long long)neg << 63));
 }
@@ -816,7 +820,7 @@ __device__ __forceinline__ double flip_sign(double v, uint32_t neg) {
 template <bool HC, bool VC, bool PATLDS, class Epi>
 __global__ void __launch_bounds__(kDirBlock) k_direct(const EdModel* __restrict__ Mp,
                                                       const DirChunk* __restrict__ chunks, int nchunk,
-                                                      const DirOp* __restrict__ ops,
+                                                      const DirGroup* __restrict__ grp,
                                                       const uint16_t* __restrict__ rank_g,
                                                       const uint16_t* __restrict__ pat_g,
                                                       const uint32_t* __restrict__ map, int ns,
@@ -840,8 +844,12 @@ __global__ void __launch_bounds__(kDirBlock) k_direct(const EdModel* __restrict_
       if (PATLDS) spat[q] = pat_g[q];
     }
   }
+  // the model constants in LDS: gen_diag's loops read them as broadcast LDS
+  // loads (from the scalar cache every loop iteration waited on its loads)
+  __shared__ EdModel M;
+  for (int q = threadIdx.x; q < (int)(sizeof(EdModel) / 4); q += kDirBlock)
+    ((uint32_t*)&M)[q] = ((const uint32_t*)Mp)[q];
   __syncthreads();
-  const EdModel& M = *Mp;
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // chunk data and ops: scalar loads
   const uint32_t mask = (1u << ns) - 1u;
@@ -868,32 +876,33 @@ __global__ void __launch_bounds__(kDirBlock) k_direct(const EdModel* __restrict_
     if constexpr (PATLDS) up = spat[ch.pat0 + (on ? lane : 0)];
     else up = map[row] & mask;
     const uint32_t m = up | (ch.idw << ns);
-    DiagAcc dg;
-    gen_row(M, m, dg);
+    double dre, dim_;
+    gen_diag(M, m, &dre, &dim_);
     const V xi = x[row];
-    V acc = add(vzero<V>(), mul(mk<HC>(dg.re, dg.im), xi));
-    for (int o = ch.op0; o < ch.op0 + ch.nop; o += kDirGroup) {
+    V acc = add(vzero<V>(), mul(mk<HC>(dre, dim_), xi));
+    const int g1 = (ch.op0 + ch.nop) / kDirGroup;
+    for (int gi = ch.op0 / kDirGroup; gi < g1; gi++) {
+      const DirGroup G = grp[gi];
       int tg[kDirGroup];
       bool vd[kDirGroup];
       H hv[kDirGroup];
+      int rk[kDirGroup];
+#pragma unroll
+      for (int j = 0; j < kDirGroup; j++) rk[j] = srank[(m ^ G.flip[j]) & mask];
 #pragma unroll
       for (int j = 0; j < kDirGroup; j++) {
-        const DirOp op = ops[o + j];
-        if (op.kind & kDirLane) {
-          const bool f = (m & op.req_mask) == op.req_val;
-          const uint32_t k = m ^ op.flip;
-          const uint32_t neg = (uint32_t)(__builtin_popcount(m & op.smask) + (op.kind >> 1)) & 1u;
-          vd[j] = f;
-          tg[j] = f ? op.delta + (int)srank[k & mask] : row;
-          if constexpr (HC)
-            hv[j] = make_double2(flip_sign(op.re, neg), (op.kind & kDirImSigned) ? flip_sign(op.im, neg) : op.im);
-          else
-            hv[j] = flip_sign(op.re, neg);
-        } else {
-          vd[j] = !(op.kind & kDirPad);
-          tg[j] = row + op.delta;
-          hv[j] = mk<HC>(op.re, op.im);
-        }
+        const int kind = G.kind[j];
+        const bool lop = kind & kDirLane;
+        // UNI / pad ops: req_mask = req_val = 0 (always fires, pads never: kDirPad)
+        const bool f = ((m & G.req_mask[j]) == G.req_val[j]) & !(kind & kDirPad);
+        const uint32_t neg = lop ? (uint32_t)(__builtin_popcount(m & G.smask[j]) + (kind >> 1)) & 1u : 0u;
+        vd[j] = f;
+        const int t1 = lop ? G.delta[j] + rk[j] : row + G.delta[j];
+        tg[j] = f ? t1 : row;
+        if constexpr (HC)
+          hv[j] = make_double2(flip_sign(G.re[j], neg), (kind & kDirImSigned) ? flip_sign(G.im[j], neg) : G.im[j]);
+        else
+          hv[j] = flip_sign(G.re[j], neg);
       }
       V g[kDirGroup];
 #pragma unroll

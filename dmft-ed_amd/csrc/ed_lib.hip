@@ -115,7 +115,7 @@ struct ed_sector {
   // matrix-free, generic (k_direct): chunk list, per-block op lists, 16-bit tables
   DirChunk* d_dchunk = nullptr;
   int ndchunk = 0;
-  DirOp* d_dops = nullptr;
+  DirGroup* d_dops = nullptr;
   uint16_t *d_rank16 = nullptr, *d_pat16 = nullptr;
   bool dir_patlds = false;
   int dir_lds = 0, dir_grid = 0;
@@ -501,6 +501,19 @@ static int build_direct(ed_sector* s) {
     }
   }
   if (ops.empty()) ops.resize(kDirGroup);  // (valid pointer)
+  std::vector<DirGroup> groups(ops.size() / kDirGroup);
+  for (size_t q = 0; q < ops.size(); q++) {
+    DirGroup& G = groups[q / kDirGroup];
+    const int j = (int)(q % kDirGroup);
+    G.req_mask[j] = ops[q].req_mask;
+    G.req_val[j] = ops[q].req_val;
+    G.flip[j] = ops[q].flip;
+    G.smask[j] = ops[q].smask;
+    G.delta[j] = ops[q].delta;
+    G.kind[j] = ops[q].kind;
+    G.re[j] = ops[q].re;
+    G.im[j] = ops[q].im;
+  }
   std::vector<uint16_t> rk(std::max<uint32_t>(nst, 8), 0), pt(std::max<uint32_t>(nst, 8), 0);
   for (uint32_t x = 0; x < nst; x++) {
     rk[x] = (uint16_t)T.rank[x];
@@ -509,7 +522,7 @@ static int build_direct(ed_sector* s) {
   s->ndchunk = (int)chunks.size();
   if (chunks.empty()) chunks.resize(1);
   CK(upload(s, &s->d_dchunk, chunks));
-  CK(upload(s, &s->d_dops, ops));
+  CK(upload(s, &s->d_dops, groups));
   CK(upload(s, &s->d_rank16, rk));
   CK(upload(s, &s->d_pat16, pt));
   // both tables in LDS up to Ns = 15 (128 KB); at Ns = 16 the rank table
@@ -1672,6 +1685,10 @@ static double pythag(double a, double b) {
   return p;
 }
 // d[n] diag, e[n] with e[0] ignored (e[i] couples i-1,i); z column-major n x n or null.
+// FAST: hypot in place of EISPACK's iterative pythag (the restart
+// eigenproblem of the thick-restart solver; Ritz values of the plain
+// Lanczos keep the reference's pythag)
+template <bool FAST = false>
 static int tql2(int n, double* d, double* e, double* z) {
   if (n == 1) return 0;
   for (int i = 1; i < n; i++) e[i - 1] = e[i];
@@ -1690,7 +1707,7 @@ static int tql2(int n, double* d, double* e, double* z) {
         int l1 = l + 1, l2 = l1 + 1;
         double g = d[l];
         double p = (d[l1] - g) / (2.0 * e[l]);
-        double r = pythag(p, 1.0);
+        double r = FAST ? hypot(p, 1.0) : pythag(p, 1.0);
         double sr = p >= 0.0 ? fabs(r) : -fabs(r);
         d[l] = e[l] / (p + sr);
         d[l1] = e[l] * (p + sr);
@@ -1706,7 +1723,7 @@ static int tql2(int n, double* d, double* e, double* z) {
           s2 = s;
           g = c * e[i];
           h = c * p;
-          r = pythag(p, e[i]);
+          r = FAST ? hypot(p, e[i]) : pythag(p, e[i]);
           e[i + 1] = s * r;
           s = e[i] / r;
           c = p / r;
@@ -1800,6 +1817,82 @@ static void jacobi_eigh(int n, std::vector<double> A, std::vector<double>& w, st
   Z.swap(Zs);
 }
 
+// Householder reduction of a real symmetric matrix to tridiagonal form with
+// the transformation accumulated (EISPACK tred2 / Numerical Recipes §11.2):
+// A (n x n, column-major, A(i,j) = A[i + n*j]) is overwritten by Q with
+// Q^T A Q = tridiag(d, e), e[i] coupling i-1 and i (e[0] = 0).  With tql2
+// (same z convention) the projected matrix of a restart costs O(n^3) with a
+// small constant: the cyclic Jacobi took ~0.5 ms per 23 x 23 restart on the
+// host, most of a small sector's solve.
+static void tred2(int n, double* A, double* d, double* e) {
+#define TA(i, j) A[(i) + (size_t)n * (j)]
+  for (int i = n - 1; i > 0; i--) {
+    const int l = i - 1;
+    double h = 0.0, scale = 0.0;
+    if (l > 0) {
+      for (int k = 0; k <= l; k++) scale += fabs(TA(i, k));
+      if (scale == 0.0) {
+        e[i] = TA(i, l);
+      } else {
+        for (int k = 0; k <= l; k++) {
+          TA(i, k) /= scale;
+          h += TA(i, k) * TA(i, k);
+        }
+        double f = TA(i, l);
+        double g = f >= 0.0 ? -sqrt(h) : sqrt(h);
+        e[i] = scale * g;
+        h -= f * g;
+        TA(i, l) = f - g;
+        f = 0.0;
+        for (int j = 0; j <= l; j++) {
+          TA(j, i) = TA(i, j) / h;
+          g = 0.0;
+          for (int k = 0; k <= j; k++) g += TA(j, k) * TA(i, k);
+          for (int k = j + 1; k <= l; k++) g += TA(k, j) * TA(i, k);
+          e[j] = g / h;
+          f += e[j] * TA(i, j);
+        }
+        const double hh = f / (h + h);
+        for (int j = 0; j <= l; j++) {
+          f = TA(i, j);
+          e[j] = g = e[j] - hh * f;
+          for (int k = 0; k <= j; k++) TA(j, k) -= (f * e[k] + g * TA(i, k));
+        }
+      }
+    } else {
+      e[i] = TA(i, l);
+    }
+    d[i] = h;
+  }
+  d[0] = 0.0;
+  e[0] = 0.0;
+  for (int i = 0; i < n; i++) {
+    const int l = i - 1;
+    if (d[i] != 0.0) {
+      for (int j = 0; j <= l; j++) {
+        double g = 0.0;
+        for (int k = 0; k <= l; k++) g += TA(i, k) * TA(k, j);
+        for (int k = 0; k <= l; k++) TA(k, j) -= g * TA(k, i);
+      }
+    }
+    d[i] = TA(i, i);
+    TA(i, i) = 1.0;
+    for (int j = 0; j <= l; j++) TA(j, i) = TA(i, j) = 0.0;
+  }
+#undef TA
+}
+
+// Symmetric eigenproblem of the projected matrix: ascending w, eigenvectors
+// as the columns of Z (column-major).  tred2 + tql2; the cyclic Jacobi only if
+// the QL iteration does not converge.
+static void sym_eigh(int n, const std::vector<double>& A, std::vector<double>& w, std::vector<double>& Z) {
+  Z = A;
+  w.assign(n, 0.0);
+  std::vector<double> e(n, 0.0);
+  tred2(n, Z.data(), w.data(), e.data());
+  if (tql2<true>(n, w.data(), e.data(), Z.data()) != 0) jacobi_eigh(n, A, w, Z);
+}
+
 __global__ void k_hash_vec(double* v, int64_t n, uint64_t seed) {
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
     uint64_t z = (uint64_t)(i + 1 + seed * 0x632BE59BD9B4E019ull) * 0x9E3779B97F4A7C15ull;
@@ -1828,6 +1921,7 @@ struct Trlan {
   // grids up to this fold the coefficient reduction into the next CGS pass
   // (every block re-reads G x ncol partials; 0 with ED_OPT_TRLAN_NOFOLD: A/B)
   int kFinFoldG = 128;
+  bool graphs_on = true;  // false (ED_OPT_NO_GRAPH): sweeps launched directly
   double *Y = nullptr, *npart = nullptr, *alpha = nullptr, *beta = nullptr;
   std::vector<void*> mine;
   std::vector<std::pair<int, hipGraphExec_t>> graphs;
@@ -1910,7 +2004,7 @@ struct Trlan {
     hipGraphExec_t ge = nullptr;
     for (auto& g : graphs)
       if (g.first == j0) ge = g.second;
-    if (!ge && n > 2) {
+    if (!ge && n > 2 && graphs_on) {
       hipGraph_t g;
       HIPCK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
       int rc = ED_OK;
@@ -1997,7 +2091,7 @@ static int trlan_core(Trlan<VC>& T, int k0, int nev, int maxit, double tol, cons
       if (j0 >= m) break;
     }
     const double beta = be[m - 1];
-    jacobi_eigh(ma, Tm, theta, Z);
+    sym_eigh(ma, Tm, theta, Z);
     // ARPACK-style test: |beta_m * Z(m-1,i)| <= tol * max(eps^(2/3), |theta_i|)
     const double eps23 = 3.6e-11;
     conv = 0;
@@ -2045,6 +2139,7 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
   T.G = (int)std::min<int64_t>(grid_for(s->dim), kTrlanGridCap);
   T.fused = !(s->opts & ED_OPT_TRLAN_UNFUSED);
   if (s->opts & ED_OPT_TRLAN_NOFOLD) T.kFinFoldG = 0;
+  T.graphs_on = !(s->opts & ED_OPT_NO_GRAPH);
   const int64_t dim = s->dim;
   const int m = (int)std::min<int64_t>(ncv, dim);
   if (nev < 1 || nev >= m) return fail(ED_ERR_ARG, "need 1 <= nev < min(ncv, dim)");
@@ -2314,7 +2409,7 @@ int ed_sector_destroy(ed_sector* s) {
 
 int ed_sector_set_options(ed_sector* s, int32_t opts) {
   if (!s) return fail(ED_ERR_ARG, "null");
-  if (opts & ~0x7ff) return fail(ED_ERR_ARG, "unknown ED_OPT_* bits");
+  if (opts & ~0xfff) return fail(ED_ERR_ARG, "unknown ED_OPT_* bits");
   if (opts != s->opts) drop_graph(s);  // a captured recurrence bakes in the kernel choice
   s->opts = opts;
   return ED_OK;

@@ -166,8 +166,8 @@ ED_HD double hint_value(const EdModel& M, uint32_t upbits, uint32_t dwbits) {
 //   void diag(double re, double im);                 // once, first
 //   void off(uint32_t k, double re, double im);      // off-diagonal, in order
 // `ValuesOnly` accs may ignore arguments; the compiler removes dead math.
-template <class Acc>
-ED_HD void gen_row(const EdModel& M, uint32_t m, Acc& acc) {
+// The diagonal element of the row of state m (reference order, see gen_row).
+ED_HD void gen_diag(const EdModel& M, uint32_t m, double* dre, double* dim_) {
   const int ns = M.ns, norb = M.norb, nbath = M.nbath, S = M.S;
   // nup(iorb)/ndw(iorb) of the reference, evaluated on the fly (no local arrays:
   // dynamically indexed arrays would spill to scratch on the GPU)
@@ -212,9 +212,20 @@ ED_HD void gen_row(const EdModel& M, uint32_t m, Acc& acc) {
     dr = dr + hr;
     di = di + hi;
   }
-  acc.diag(dr, di);
+  *dre = dr;
+  *dim_ = di;
 #undef nup
 #undef ndw
+}
+
+template <class Acc>
+ED_HD void gen_row(const EdModel& M, uint32_t m, Acc& acc) {
+  const int norb = M.norb, nbath = M.nbath, S = M.S, ns = M.ns;
+  {
+    double dr, di;
+    gen_diag(M, m, &dr, &di);
+    acc.diag(dr, di);
+  }
 
   // ---- stored/Himp.f90:27-72 same-spin impurity hops, value conj(h)*sg1*sg2
   for (int io = 0; io < norb; io++)

@@ -1,0 +1,69 @@
+"""configs[3] sector farm on one GPU for profiling: wall time, and per Lanczos
+sector the solve time, H·v products and restarts' worth of work.
+
+    python tools/farm_prof.py [--workers N] [--reps R] [--serial-stats out.json]
+
+--serial-stats: additionally solve every Lanczos sector alone on one thread
+(create / eigh / close timed separately, nhv from ed_sector_eigh) and write a
+JSON table (the fixed-cost fit of edgpu.farm.sector_cost comes from it).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "dmft-ed_amd"), os.path.join(ROOT, "tests")]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+torch.cuda.init()
+from edgpu.diag import DiagOptions, _start_vector, lanczos_params  # noqa: E402
+from edgpu.farm import farm_diag  # noqa: E402
+from edgpu.hamiltonian import Sector  # noqa: E402
+from edgpu.sectors import setup_pointers  # noqa: E402
+from golden.golden_configs import c4_config  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--workers", type=int, default=8)
+ap.add_argument("--reps", type=int, default=2)
+ap.add_argument("--serial-stats", default="")
+ap.add_argument("--options", default="", help="comma-separated ED_OPT_* names for every sector")
+a = ap.parse_args()
+cfg = c4_config("random")
+opts = tuple(x for x in a.options.split(",") if x)
+
+if a.serial_stats:
+    opt = DiagOptions()
+    rows = []
+    for sec in setup_pointers(cfg):
+        neigen, nitermax, nblock = lanczos_params(sec.dim, opt)
+        if neigen == sec.dim or sec.dim <= opt.lanc_dim_threshold:
+            continue
+        t0 = time.perf_counter()
+        S = Sector(cfg, sec.q1, sec.q2, stored=True, real=True, options=opts)
+        t1 = time.perf_counter()
+        w, X, nconv, nhv = S.eigh(neigen=neigen, ncv=min(nblock, 64), maxit=nitermax,
+                                  v0=_start_vector(sec.dim, False), on_device=True)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        S.close()
+        t3 = time.perf_counter()
+        rows.append(dict(sector=[sec.q1, sec.q2], dim=sec.dim, create_s=round(t1 - t0, 5),
+                         eigh_s=round(t2 - t1, 5), close_s=round(t3 - t2, 5), nhv=nhv, nconv=nconv))
+        print(rows[-1], flush=True)
+    tot = {k: round(sum(r[k] for r in rows), 4) for k in ("create_s", "eigh_s", "close_s")}
+    tot["nhv"] = sum(r["nhv"] for r in rows)
+    print("serial totals", tot, flush=True)
+    with open(a.serial_stats, "w") as f:
+        json.dump(dict(config="configs[3] random bath, Lanczos sectors, one thread", options=list(opts),
+                       totals=tot, sectors=rows), f, indent=1)
+
+opt = DiagOptions(workers=a.workers)
+for rep in range(a.reps):
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    res = farm_diag(cfg, opt)
+    torch.cuda.synchronize()
+    print(f"farm workers={a.workers} wall {time.perf_counter() - t:.4f} s states={res.states.size}", flush=True)
