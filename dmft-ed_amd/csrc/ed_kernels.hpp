@@ -166,7 +166,7 @@ struct DevIndex {
 };
 
 // ------------------------------------------------------------- basis / map
-__global__ void __launch_bounds__(kBlock) k_build_map(const int64_t* __restrict__ blk_off,
+static __global__ void __launch_bounds__(kBlock) k_build_map(const int64_t* __restrict__ blk_off,
                                                       const uint32_t* __restrict__ blk_idw, int nblk,
                                                       const int32_t* __restrict__ need_cls,
                                                       const uint32_t* __restrict__ by_cls,
@@ -194,7 +194,7 @@ struct CountAcc {
 };
 
 // cnt[i] = off-diagonal elements of row i; width[s] = max over slice s.
-__global__ void __launch_bounds__(kBlock) k_count(const EdModel* __restrict__ Mp,
+static __global__ void __launch_bounds__(kBlock) k_count(const EdModel* __restrict__ Mp,
                                                   const uint32_t* __restrict__ map, int64_t dim,
                                                   int64_t nslice, uint16_t* __restrict__ cnt,
                                                   int32_t* __restrict__ width) {
@@ -214,7 +214,7 @@ __global__ void __launch_bounds__(kBlock) k_count(const EdModel* __restrict__ Mp
 }
 
 // Exclusive scan of 64*width -> sptr (int64), three-pass.
-__global__ void __launch_bounds__(1024) k_scan_blocks(const int32_t* __restrict__ width, int64_t n,
+static __global__ void __launch_bounds__(1024) k_scan_blocks(const int32_t* __restrict__ width, int64_t n,
                                                       int64_t* __restrict__ out,
                                                       int64_t* __restrict__ bsum) {
   __shared__ int64_t s[1024];
@@ -231,7 +231,7 @@ __global__ void __launch_bounds__(1024) k_scan_blocks(const int32_t* __restrict_
   if (i < n) out[i] = s[threadIdx.x] - x;  // exclusive within block
   if (threadIdx.x == 1023) bsum[blockIdx.x] = s[1023];
 }
-__global__ void k_scan_spine(int64_t* __restrict__ bsum, int64_t nb, int64_t* __restrict__ total) {
+static __global__ void k_scan_spine(int64_t* __restrict__ bsum, int64_t nb, int64_t* __restrict__ total) {
   if (threadIdx.x == 0 && blockIdx.x == 0) {
     int64_t acc = 0;
     for (int64_t b = 0; b < nb; b++) {
@@ -242,7 +242,7 @@ __global__ void k_scan_spine(int64_t* __restrict__ bsum, int64_t nb, int64_t* __
     *total = acc;
   }
 }
-__global__ void __launch_bounds__(1024) k_scan_add(int64_t* __restrict__ out, int64_t n,
+static __global__ void __launch_bounds__(1024) k_scan_add(int64_t* __restrict__ out, int64_t n,
                                                    const int64_t* __restrict__ bsum,
                                                    const int64_t* __restrict__ total) {
   int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x;
@@ -459,7 +459,7 @@ struct EpiLancFused {
 };
 
 // Two-pass finishing kernels of one Lanczos step (one block of kBlock threads).
-__global__ void __launch_bounds__(kBlock) k_lanc_fin_a(const double* __restrict__ partials, int n,
+static __global__ void __launch_bounds__(kBlock) k_lanc_fin_a(const double* __restrict__ partials, int n,
                                                        LancState* st, double* alpha_out) {
   if (st->done) return;
   const double tot = sum_partials(partials, n);
@@ -478,7 +478,7 @@ __device__ __forceinline__ void lanc_set_beta(double tot, LancState* st, double*
   st->iter = it + 1;
   if (b < st->thresh) st->done = 1;
 }
-__global__ void __launch_bounds__(kBlock) k_lanc_fin_b(const double* __restrict__ partials, int n,
+static __global__ void __launch_bounds__(kBlock) k_lanc_fin_b(const double* __restrict__ partials, int n,
                                                        LancState* st, double* beta_out) {
   if (st->done) return;
   const double tot = sum_partials(partials, n);
@@ -603,7 +603,7 @@ __device__ __forceinline__ bool wave_key_leader(unsigned long long key) {
   return lead;
 }
 
-__global__ void __launch_bounds__(kBlock) k_dict_insert(const double* __restrict__ vals, int64_t n,
+static __global__ void __launch_bounds__(kBlock) k_dict_insert(const double* __restrict__ vals, int64_t n,
                                                         unsigned long long* table,
                                                         unsigned int* overflow) {
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
@@ -631,7 +631,7 @@ __global__ void __launch_bounds__(kBlock) k_dict_insert(const double* __restrict
   }
 }
 
-__global__ void __launch_bounds__(kBlock) k_dict_pack(const int32_t* __restrict__ cols,
+static __global__ void __launch_bounds__(kBlock) k_dict_pack(const int32_t* __restrict__ cols,
                                                       const double* __restrict__ vals, int64_t n,
                                                       const unsigned long long* __restrict__ table,
                                                       const uint8_t* __restrict__ tidx,
@@ -656,7 +656,7 @@ __device__ __forceinline__ unsigned long long pair_key(double2 v) {
   return k == kDictEmpty ? 0x7ff8dead00000001ull : k;
 }
 
-__global__ void __launch_bounds__(kBlock) k_dict_insert_c(const double2* __restrict__ vals, int64_t n,
+static __global__ void __launch_bounds__(kBlock) k_dict_insert_c(const double2* __restrict__ vals, int64_t n,
                                                           unsigned long long* table, double2* reps,
                                                           unsigned int* overflow) {
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
@@ -687,7 +687,7 @@ __global__ void __launch_bounds__(kBlock) k_dict_insert_c(const double2* __restr
   }
 }
 
-__global__ void __launch_bounds__(kBlock) k_dict_pack_c(const int32_t* __restrict__ cols,
+static __global__ void __launch_bounds__(kBlock) k_dict_pack_c(const int32_t* __restrict__ cols,
                                                         const double2* __restrict__ vals, int64_t n,
                                                         const unsigned long long* __restrict__ table,
                                                         const double2* __restrict__ reps,
@@ -783,10 +783,11 @@ __global__ void __launch_bounds__(kBlock) k_spmv_pk(const val_t<HC>* __restrict_
 // scalar loads.  Ops go in groups of kDirGroup with every gather of a group
 // issued before the group's terms are summed, in order, into the row: the
 // same products and additions as k_spmv, so H·v is bit-identical to the
-// stored kernel.  The diagonal is gen_row's own (gen_diag).  Every op of a
-// group is evaluated branch-free (a down-level op reads the rank table at its
-// own pattern and ignores it), so the group's LDS reads and gathers issue
-// back to back.
+// stored kernel.  The diagonal is gen_row's own (gen_diag).  An op's kind is
+// scalar: down-level ops and pads skip the per-lane evaluation (uniform
+// branch); the group's LDS reads and gathers still issue back to back.  The
+// two directions of a hop on up levels are one op (kDirXor, build_direct):
+// ~half the per-lane evaluations of a normal-mode row.
 constexpr int kDirBlock = 1024;
 constexpr int kDirGroup = 4;
 struct DirOp {
@@ -803,7 +804,8 @@ struct __align__(64) DirGroup {
   int32_t delta[kDirGroup], kind[kDirGroup], pad_[8];
   double re[kDirGroup], im[kDirGroup];
 };
-constexpr int kDirLane = 1, kDirC0 = 2, kDirImSigned = 4, kDirPad = 8;
+// kDirXor: merged hop pair, fires when exactly one of the two flip bits is set
+constexpr int kDirLane = 1, kDirC0 = 2, kDirImSigned = 4, kDirPad = 8, kDirXor = 16;
 struct DirChunk {
   int32_t row;    // row of lane 0
   uint32_t idw;   // down pattern of the block
@@ -891,18 +893,22 @@ __global__ void __launch_bounds__(kDirBlock) k_direct(const EdModel* __restrict_
       for (int j = 0; j < kDirGroup; j++) rk[j] = srank[(m ^ G.flip[j]) & mask];
 #pragma unroll
       for (int j = 0; j < kDirGroup; j++) {
-        const int kind = G.kind[j];
-        const bool lop = kind & kDirLane;
-        // UNI / pad ops: req_mask = req_val = 0 (always fires, pads never: kDirPad)
-        const bool f = ((m & G.req_mask[j]) == G.req_val[j]) & !(kind & kDirPad);
-        const uint32_t neg = lop ? (uint32_t)(__builtin_popcount(m & G.smask[j]) + (kind >> 1)) & 1u : 0u;
-        vd[j] = f;
-        const int t1 = lop ? G.delta[j] + rk[j] : row + G.delta[j];
-        tg[j] = f ? t1 : row;
-        if constexpr (HC)
-          hv[j] = make_double2(flip_sign(G.re[j], neg), (kind & kDirImSigned) ? flip_sign(G.im[j], neg) : G.im[j]);
-        else
-          hv[j] = flip_sign(G.re[j], neg);
+        const int kind = G.kind[j];  // scalar: the branches below are uniform
+        if (kind & kDirLane) {
+          bool f = (m & G.req_mask[j]) == G.req_val[j];
+          if (kind & kDirXor) f = f & (__builtin_popcount(m & G.flip[j]) == 1);
+          const uint32_t neg = (uint32_t)(__builtin_popcount(m & G.smask[j]) + (kind >> 1)) & 1u;
+          vd[j] = f;
+          tg[j] = f ? G.delta[j] + rk[j] : row;
+          if constexpr (HC)
+            hv[j] = make_double2(flip_sign(G.re[j], neg), (kind & kDirImSigned) ? flip_sign(G.im[j], neg) : G.im[j]);
+          else
+            hv[j] = flip_sign(G.re[j], neg);
+        } else {  // down-level op (signed value, row offset) or pad (never fires)
+          vd[j] = !(kind & kDirPad);
+          tg[j] = row + G.delta[j];
+          hv[j] = mk<HC>(G.re[j], G.im[j]);
+        }
       }
       V g[kDirGroup];
 #pragma unroll
@@ -1307,7 +1313,7 @@ struct MarkAcc {
     atomicOr(mask + (c >> 5), 1u << (c & 31));
   }
 };
-__global__ void __launch_bounds__(kBlock) k_mark_cols(const EdModel* __restrict__ Mp,
+static __global__ void __launch_bounds__(kBlock) k_mark_cols(const EdModel* __restrict__ Mp,
                                                       const uint32_t* __restrict__ map, int64_t n,
                                                       DevIndex idx, uint32_t* mask) {
   const EdModel& M = *Mp;
@@ -1386,7 +1392,7 @@ __device__ __forceinline__ double2 cdiv(double2 p, double a, double b) {
   return make_double2((p.x * r + p.y) / den, (p.y * r - p.x) / den);
 }
 
-__global__ void __launch_bounds__(kBlock) k_gf_poles(const GfFrac* __restrict__ fr, int nfrac,
+static __global__ void __launch_bounds__(kBlock) k_gf_poles(const GfFrac* __restrict__ fr, int nfrac,
                                                      const double* __restrict__ E, const double* __restrict__ z,
                                                      const double* __restrict__ wm, int lmats,
                                                      const double* __restrict__ wr, int lreal, double eps,

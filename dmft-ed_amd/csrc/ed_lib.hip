@@ -12,6 +12,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <mutex>
 #include <string>
 #include <map>
@@ -21,26 +22,16 @@
 #include "ed_persist.hpp"
 #include "ed_trlan.hpp"
 #include "ed_tables.hpp"
+#include "ed_host.hpp"
 
 using namespace edg;
 
 // ------------------------------------------------------------------ errors
-static thread_local std::string g_err;
-static int fail(int code, const std::string& msg) {
-  g_err = msg;
-  return code;
+// (fail / HIPCK / CK in ed_host.hpp; the message slot is this TU's)
+std::string& ed_err_slot() {
+  static thread_local std::string e;
+  return e;
 }
-#define HIPCK(x)                                                                       \
-  do {                                                                                 \
-    hipError_t e_ = (x);                                                               \
-    if (e_ != hipSuccess)                                                              \
-      return fail(ED_ERR_HIP, std::string(#x) + " -> " + hipGetErrorString(e_));       \
-  } while (0)
-#define CK(x)                  \
-  do {                         \
-    int r_ = (x);              \
-    if (r_ != ED_OK) return r_; \
-  } while (0)
 
 static constexpr int kMaxGrid = 65536;
 // columns of the thick-restart coefficient buffers (ncv + probe columns)
@@ -439,6 +430,82 @@ static int direct_candidates_check(const ed_sector* s, const std::vector<DirCand
   return ED_OK;
 }
 
+// Merge LANE op b into a (previous op of the same block) when they are the two
+// directions of one hop: same two flip bits (up levels), same value and
+// target block, conditions equal except on the flip bits where they read
+// (1,0) and (0,1), and a Jordan-Wigner parity that agrees once the flip bits'
+// part of popc(m & smask) is folded into the constant.
+static bool dir_merge(DirOp& a, const DirOp& b, uint32_t nst) {
+  if (!(a.kind & kDirLane) || (a.kind & kDirXor) || !(b.kind & kDirLane)) return false;
+  const uint32_t fl = a.flip;
+  if (fl != b.flip || __builtin_popcount(fl) != 2 || (fl & ~(nst - 1)) != 0) return false;
+  if (a.delta != b.delta || !same_bits(a.re, b.re) || !same_bits(a.im, b.im) ||
+      (a.kind & kDirImSigned) != (b.kind & kDirImSigned) || a.smask != b.smask)
+    return false;
+  if (a.req_mask != b.req_mask || (a.req_mask & fl) != fl) return false;
+  if ((a.req_val & ~fl) != (b.req_val & ~fl)) return false;
+  const uint32_t va = a.req_val & fl, vb = b.req_val & fl;
+  if (__builtin_popcount(va) != 1 || (va ^ vb) != fl) return false;
+  const int pa = (__builtin_popcount(va & a.smask) + ((a.kind & kDirC0) ? 1 : 0)) & 1;
+  const int pb = (__builtin_popcount(vb & b.smask) + ((b.kind & kDirC0) ? 1 : 0)) & 1;
+  if (pa != pb) return false;
+  a.req_mask &= ~fl;
+  a.req_val &= ~fl;
+  a.smask &= ~fl;
+  a.kind = (a.kind & ~kDirC0) | (pa ? kDirC0 : 0) | kDirXor;
+  return true;
+}
+
+// The kernel's view of one op (host restatement of k_direct's evaluation):
+// fires?, target row, sign.
+static bool dir_apply(const DirOp& o, uint32_t m, uint32_t mask, int64_t row, const std::vector<uint32_t>& rank,
+                      int64_t* tgt, double* sg) {
+  if (o.kind & kDirPad) return false;
+  if (!(o.kind & kDirLane)) {
+    *tgt = row + o.delta;
+    *sg = 1.0;
+    return true;
+  }
+  bool f = (m & o.req_mask) == o.req_val;
+  if (o.kind & kDirXor) f = f && __builtin_popcount(m & o.flip) == 1;
+  if (!f) return false;
+  *tgt = o.delta + (int64_t)rank[(m ^ o.flip) & mask];
+  *sg = ((__builtin_popcount(m & o.smask) + ((o.kind & kDirC0) ? 1 : 0)) & 1) ? -1.0 : 1.0;
+  return true;
+}
+
+// The final op lists against gen_row on sample rows: targets (through the
+// sector's index), value bits and order.
+static int direct_ops_check(const ed_sector* s, const std::vector<DirOp>& ops, const std::vector<DirChunk>& chunks) {
+  const SectorTables& T = s->T;
+  const uint32_t mask = T.nst - 1;
+  const size_t step = std::max<size_t>(1, chunks.size() / 512);
+  for (size_t ci = 0; ci < chunks.size(); ci += step) {
+    const DirChunk& ch = chunks[ci];
+    for (int l = 0; l < ch.n; l += std::max(1, ch.n / 8)) {
+      const int64_t row = ch.row + l;
+      const uint32_t m = T.by_cls[ch.pat0 + l] | (ch.idw << T.ns);
+      RecAcc ref;
+      gen_row(s->Mh, m, ref);
+      size_t q = 0;
+      for (int k = ch.op0; k < ch.op0 + ch.nop; k++) {
+        int64_t tg;
+        double sg;
+        if (!dir_apply(ops[k], m, mask, row, T.rank, &tg, &sg)) continue;
+        const DirOp& o = ops[k];
+        const double re = (o.kind & kDirLane) ? o.re * sg : o.re;
+        const double im = (o.kind & kDirLane) && (o.kind & kDirImSigned) ? o.im * sg : o.im;
+        if (q >= ref.k.size() || table_index(T, ref.k[q]) != tg || !same_bits(ref.re[q], re) ||
+            !same_bits(ref.im[q], im))
+          return fail(ED_ERR_STATE, "direct op lists differ from gen_row (row " + std::to_string(row) + ")");
+        q++;
+      }
+      if (q != ref.k.size()) return fail(ED_ERR_STATE, "direct op lists miss elements of gen_row");
+    }
+  }
+  return ED_OK;
+}
+
 static int build_direct(ed_sector* s) {
   const SectorTables& T = s->T;
   const int ns = T.ns;
@@ -480,6 +547,10 @@ static int build_direct(ed_sector* s) {
         o.re = c.re;
         o.im = c.im;
       }
+      // the two directions of a hop (c+_a c_b then c+_b c_a, adjacent in
+      // gen_row order, exclusive conditions): one op firing on "exactly one
+      // of the two flip bits set" (halves the per-lane op evaluations)
+      if (!uni && (int32_t)ops.size() > op0 && dir_merge(ops.back(), o, nst)) continue;
       ops.push_back(o);
     }
     while ((ops.size() - op0) % kDirGroup) {
@@ -500,6 +571,7 @@ static int build_direct(ed_sector* s) {
       chunks.push_back(ch);
     }
   }
+  CK(direct_ops_check(s, ops, chunks));
   if (ops.empty()) ops.resize(kDirGroup);  // (valid pointer)
   std::vector<DirGroup> groups(ops.size() / kDirGroup);
   for (size_t q = 0; q < ops.size(); q++) {
@@ -1207,11 +1279,9 @@ static int build_preg(ed_sector* s) {
 // entries once plus RPT rows x (E down-hop entries, diagonal, r, p, w) must
 // stay below the spill-free budget (-Rpass-analysis=kernel-resource-usage:
 // E=4/RPT=10 and E=8/RPT=6 compile without scratch).
-constexpr bool pkr_fits(int E, int RPT) { return RPT * (3 * E + 8) + 3 * E <= 216; }
 // complex vectors (1024 threads, <= 128 VGPRs): per row the down-hop byte
 // offsets and the complex w and p; the diagonal and the hop values in LDS
 // (-Rpass-analysis: E=4 up to 5 rows, E=8 up to 3 rows spill-free)
-constexpr bool pkr_fits_c(int E, int RPT) { return E == 4 ? RPT <= 5 : RPT <= 2; }
 static int pkr_geom(ed_sector* s, int64_t du, int64_t dd, int degu, int degd) {
   const int deg = std::max(degu, degd);
   const int E = deg <= 4 ? 4 : deg <= 8 ? 8 : 0;
@@ -1406,11 +1476,6 @@ static int build_pkron_direct(ed_sector* s) {
 // Returns the persistent mode (0 stored, 1 Kronecker, 2 stored in registers)
 // or -1 when the sector does not fit one workgroup's LDS / register budget.
 static int64_t persist_lds(const ed_sector* s, int vc, int mode);
-// Rows per thread of the 1024-thread modes (0, 1): the launch's template value
-static int persist_rpt01(int64_t dim) {
-  const int64_t rpt = (dim + kPBlock - 1) / kPBlock;
-  return rpt <= 6 ? (int)rpt : rpt <= 8 ? 8 : rpt <= 10 ? 10 : rpt <= 12 ? 12 : 16;
-}
 // LDS vector rows of a persistent launch: NT * RPT (padding rows stay zero)
 static int64_t persist_vrows(const ed_sector* s, int mode, int vc = 0) {
   switch (mode) {
@@ -1421,7 +1486,6 @@ static int64_t persist_vrows(const ed_sector* s, int mode, int vc = 0) {
   }
 }
 // ELL words per lane that compile without scratch (-Rpass-analysis=kernel-resource-usage)
-constexpr int preg_cap(bool hc, bool vc) { return vc ? (hc ? 80 : 84) : 112; }
 static int persist_mode(ed_sector* s, int vc, int path) {
   const int o = s->opts;
   if (o & ED_OPT_NO_PERSIST) return -1;
@@ -1508,71 +1572,17 @@ static int64_t persist_lds(const ed_sector* s, int vc, int mode) {
   return lds;
 }
 
-template <bool HC, bool VC, int MODE, int RPT, int E = 1>
-static int persist_launch_t(ed_sector* s, const PersistRun<HC>& run, int64_t lds, hipStream_t st, int nb) {
-  if constexpr ((MODE == 2 || MODE == 3) && RPT * E > preg_cap(HC, VC)) {
-    return fail(ED_ERR_UNSUPPORTED, "register-resident ELL exceeds the spill-free budget");
-  } else if constexpr (MODE == 4 && (HC || (VC ? !pkr_fits_c(E, RPT) : !pkr_fits(E, RPT)))) {
-    return fail(ED_ERR_UNSUPPORTED, "Kronecker register layout: real H within the register budget");
-  } else {
-  constexpr int NT = (MODE >= 2 && !(MODE == 4 && VC)) ? kPRegBlock : kPBlock;
-  auto fn = k_lanc_persist<HC, VC, MODE, RPT, E, NT>;
-  HIPCK(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  hipLaunchKernelGGL(fn, dim3(nb), dim3(NT), (size_t)lds, st, run);
-  HIPCK(hipGetLastError());
-  return ED_OK;
-  }
-}
-
-template <bool HC, bool VC, int MODE, int W>
-static int persist_launch_e(ed_sector* s, const PersistRun<HC>& run, int64_t lds, hipStream_t st, int nb) {
-  if constexpr (MODE == 4 && VC) {
-    switch (s->pkr_rpt_c) {
-      case 2: return persist_launch_t<HC, VC, MODE, 2, W>(s, run, lds, st, nb);
-      case 3: return persist_launch_t<HC, VC, MODE, 3, W>(s, run, lds, st, nb);
-      case 4: return persist_launch_t<HC, VC, MODE, 4, W>(s, run, lds, st, nb);
-      default: return persist_launch_t<HC, VC, MODE, 5, W>(s, run, lds, st, nb);
-    }
-  }
-  switch (MODE == 2 ? s->preg_rpt : MODE == 3 ? s->kreg_rpt : s->pkr_rpt) {
-    case 2: return persist_launch_t<HC, VC, MODE, 2, W>(s, run, lds, st, nb);
-    case 4: return persist_launch_t<HC, VC, MODE, 4, W>(s, run, lds, st, nb);
-    case 6: return persist_launch_t<HC, VC, MODE, 6, W>(s, run, lds, st, nb);
-    case 8: return persist_launch_t<HC, VC, MODE, 8, W>(s, run, lds, st, nb);
-    default: return persist_launch_t<HC, VC, MODE, 10, W>(s, run, lds, st, nb);
-  }
-}
-
-template <bool HC, bool VC, int MODE>
-static int persist_launch_m(ed_sector* s, const PersistRun<HC>& run, int64_t lds, hipStream_t st, int nb = 1) {
-  if constexpr (MODE == 4) {
-    if constexpr (HC) {
-      return fail(ED_ERR_UNSUPPORTED, "MODE 4 needs a real H");
-    } else {
-      return s->pkr_E == 4 ? persist_launch_e<HC, VC, 4, 4>(s, run, lds, st, nb)
-                           : persist_launch_e<HC, VC, 4, 8>(s, run, lds, st, nb);
-    }
-  } else if constexpr (MODE >= 2) {
-    switch (MODE == 2 ? s->preg_E : s->kreg_W) {
-      case 8: return persist_launch_e<HC, VC, MODE, 8>(s, run, lds, st, nb);
-      case 12: return persist_launch_e<HC, VC, MODE, 12>(s, run, lds, st, nb);
-      case 14: return persist_launch_e<HC, VC, MODE, 14>(s, run, lds, st, nb);
-      default: return persist_launch_e<HC, VC, MODE, 16>(s, run, lds, st, nb);
-    }
-  } else {
-  switch (persist_rpt01(s->dim)) {
-    case 1: return persist_launch_t<HC, VC, MODE, 1>(s, run, lds, st, nb);
-    case 2: return persist_launch_t<HC, VC, MODE, 2>(s, run, lds, st, nb);
-    case 3: return persist_launch_t<HC, VC, MODE, 3>(s, run, lds, st, nb);
-    case 4: return persist_launch_t<HC, VC, MODE, 4>(s, run, lds, st, nb);
-    case 5: return persist_launch_t<HC, VC, MODE, 5>(s, run, lds, st, nb);
-    case 6: return persist_launch_t<HC, VC, MODE, 6>(s, run, lds, st, nb);
-    case 8: return persist_launch_t<HC, VC, MODE, 8>(s, run, lds, st, nb);
-    case 10: return persist_launch_t<HC, VC, MODE, 10>(s, run, lds, st, nb);
-    case 12: return persist_launch_t<HC, VC, MODE, 12>(s, run, lds, st, nb);
-    default: return persist_launch_t<HC, VC, MODE, 16>(s, run, lds, st, nb);
-  }
-  }
+static PersistGeom persist_geom(const ed_sector* s) {
+  PersistGeom g;
+  g.dim = s->dim;
+  g.preg_E = s->preg_E;
+  g.preg_rpt = s->preg_rpt;
+  g.kreg_W = s->kreg_W;
+  g.kreg_rpt = s->kreg_rpt;
+  g.pkr_E = s->pkr_E;
+  g.pkr_rpt = s->pkr_rpt;
+  g.pkr_rpt_c = s->pkr_rpt_c;
+  return g;
 }
 
 // Workspace of a batched persistent launch: nb runs on the same H, run b at
@@ -1641,20 +1651,13 @@ static int persist_iters(ed_sector* s, int mode, bool basis, int niter, int firs
       fill(r);
       if (mode == 1 || mode == 3) r.K = kron_args<true>(s);
       if (mode == 4) return fail(ED_ERR_UNSUPPORTED, "MODE 4 needs real H");
-      return mode == 0 ? persist_launch_m<true, true, 0>(s, r, lds, st, nb)
-             : mode == 1 ? persist_launch_m<true, true, 1>(s, r, lds, st, nb)
-             : mode == 2 ? persist_launch_m<true, true, 2>(s, r, lds, st, nb)
-                         : persist_launch_m<true, true, 3>(s, r, lds, st, nb);
+      return persist_launch(true, true, mode, persist_geom(s), &r, lds, st, nb);
     }
   }
   PersistRun<false> r;
   fill(r);
   if (mode == 1 || mode == 3 || (mode == 4 && s->kron)) r.K = kron_args<false>(s);
-  return mode == 0 ? persist_launch_m<false, VC, 0>(s, r, lds, st, nb)
-         : mode == 1 ? persist_launch_m<false, VC, 1>(s, r, lds, st, nb)
-         : mode == 2 ? persist_launch_m<false, VC, 2>(s, r, lds, st, nb)
-         : mode == 3 ? persist_launch_m<false, VC, 3>(s, r, lds, st, nb)
-                     : persist_launch_m<false, VC, 4>(s, r, lds, st, nb);
+  return persist_launch(false, VC, mode, persist_geom(s), &r, lds, st, nb);
 }
 
 static int persist_set_thresh(ed_sector* s, double thresh, hipStream_t st) {
@@ -1907,6 +1910,37 @@ __global__ void k_hash_vec(double* v, int64_t n, uint64_t seed) {
 // stay on the device; one expansion sweep (j0 .. m-1) is captured once per
 // start column into a hipGraph (j0 = 0 and j0 = nkeep), so a restart cycle is
 // one graph launch + one host sync for the m x m projected problem.
+// Workgroups of persistent sweeps in flight in this process.  A sweep's
+// workgroups wait for each other at grid barriers, so all of them must be
+// resident at once; concurrent sweeps (farm worker threads) whose workgroups
+// together exceed what the chip holds would each keep part of their grid
+// spinning while the rest cannot be placed.  k_trl_sweep admits 2 workgroups
+// per CU (launch bounds); the budget is half of that, so two processes
+// sharing a GPU fit as well.  Blocking acquire (no fallback to the graph
+// sweep: results do not depend on the schedule).
+static constexpr int kPSweepBudget = 256;
+struct PSweepBudget {
+  std::mutex mu;
+  std::condition_variable cv;
+  int used = 0;
+};
+static PSweepBudget g_psb;
+struct PSweepSlot {
+  int n;
+  explicit PSweepSlot(int n_) : n(n_) {
+    std::unique_lock<std::mutex> lk(g_psb.mu);
+    g_psb.cv.wait(lk, [&] { return g_psb.used + n <= kPSweepBudget; });
+    g_psb.used += n;
+  }
+  ~PSweepSlot() {
+    {
+      std::lock_guard<std::mutex> lk(g_psb.mu);
+      g_psb.used -= n;
+    }
+    g_psb.cv.notify_all();
+  }
+};
+
 template <bool VC>
 struct Trlan {
   using V = val_t<VC>;
@@ -1914,7 +1948,7 @@ struct Trlan {
   int path = 0;
   hipStream_t st = nullptr;
   int64_t dim = 0;
-  int G = 1, m = 0;
+  int G = 1, m = 0, mcap = 0;  // mcap: basis columns allocated
   bool fused = true;  // false (ED_OPT_TRLAN_UNFUSED): the four-sweep CGS2 (A/B)
   V *Vb = nullptr, *Xb = nullptr, *w = nullptr;
   double2 *h = nullptr, *coef = nullptr, *part = nullptr, *part2 = nullptr;
@@ -1923,6 +1957,13 @@ struct Trlan {
   int kFinFoldG = 128;
   bool graphs_on = true;  // false (ED_OPT_NO_GRAPH): sweeps launched directly
   double *Y = nullptr, *npart = nullptr, *alpha = nullptr, *beta = nullptr;
+  double *npA = nullptr, *npB = nullptr;  // |w|^2 partials before / after the first CGS pass (DGKS)
+  // persistent sweep (k_trl_sweep): grid, ping-pong residuals, barrier words
+  int PG = 0;                    // 0: multi-kernel sweeps
+  V* wb = nullptr;
+  unsigned int* bar = nullptr;   // [0] arrival counter, [1] abort word
+  unsigned int bar_count = 0;    // counter value after the last launch
+  unsigned int abort_h = 0;      // abort word read back with alpha/beta
   std::vector<void*> mine;
   std::vector<std::pair<int, hipGraphExec_t>> graphs;
   int nhv = 0;
@@ -1940,11 +1981,11 @@ struct Trlan {
   // with jn >= 0: alpha[jn], beta[jn] = ||x|| afterwards
   // one fused sweep (k_cgs) with the column group rounded up to 8/16/24/32
   bool cgs(int ncol, const double2* hin, V* x, double2* pt, double* np, const double2* pin = nullptr,
-           int add = 0) {
+           int add = 0, const double* dgA = nullptr, const double* dgB = nullptr) {
     const int nc = (ncol + 7) / 8 * 8;
 #define ED_CGS(NCV) \
   hipLaunchKernelGGL((k_cgs<VC, NCV>), dim3(G), dim3(kBlock), 0, st, Vb, ncol, hin, x, dim, pt, np, pin, G, \
-                     coef, add)
+                     coef, add, dgA, dgB)
     if (nc <= 8) ED_CGS(8);
     else if (nc <= 16) ED_CGS(16);
     else if (nc <= 24) ED_CGS(24);
@@ -1954,18 +1995,21 @@ struct Trlan {
     return true;
   }
   int orth(int ncol, V* x, int jn, V* out = nullptr) {
-    // fused CGS2: dots | x -= V h1, dots | x -= V h2, |x|^2  (V streamed 3x)
-    if (fused && ncol > 0 && cgs(ncol, nullptr, x, part, nullptr)) {
+    // fused CGS: dots + |x|^2 | x -= V h1, dots, |x'|^2 | (DGKS: only if
+    // |x'| <= 0.717 |x|) x -= V h2, |x''|^2 — V streamed 2x or 3x
+    if (fused && ncol > 0 && cgs(ncol, nullptr, x, part, npA)) {
       if (G <= kFinFoldG) {
         // small grids: each pass forms the previous pass's coefficients from
         // its partials (k_vdot_fin folded in: 5 launches per step, not 7)
-        cgs(ncol, nullptr, x, part2, nullptr, part, 0);
-        cgs(ncol, nullptr, x, nullptr, npart, part2, 1);
+        cgs(ncol, nullptr, x, part2, npB, part, 0);
+        cgs(ncol, nullptr, x, nullptr, npart, part2, 1, npA, npB);
       } else {
-        hipLaunchKernelGGL(k_vdot_fin<VC>, dim3(ncol), dim3(kBlock), 0, st, part, G, h, coef, 0);
-        cgs(ncol, h, x, part, nullptr);
-        hipLaunchKernelGGL(k_vdot_fin<VC>, dim3(ncol), dim3(kBlock), 0, st, part, G, h, coef, 1);
-        cgs(ncol, h, x, nullptr, npart);
+        hipLaunchKernelGGL(k_vdot_fin<VC>, dim3(ncol), dim3(kBlock), 0, st, part, G, h, coef, 0,
+                           (const double*)nullptr, (const double*)nullptr);
+        cgs(ncol, h, x, part2, npB);
+        hipLaunchKernelGGL(k_vdot_fin<VC>, dim3(ncol), dim3(kBlock), 0, st, part2, G, h, coef, 1,
+                           (const double*)npA, (const double*)npB);
+        cgs(ncol, h, x, nullptr, npart, nullptr, 0, npA, npB);
       }
       if (out && jn >= 0)  // + V_{j+1} = x / beta_j in the same launch
         hipLaunchKernelGGL(k_coef_scale<VC>, dim3(G), dim3(kBlock), 0, st, npart, G, coef, jn, alpha, beta,
@@ -1981,7 +2025,8 @@ struct Trlan {
     const dim3 gp(G, (ncol + kVCols - 1) / kVCols);
     for (int pass = 0; pass < 2 && ncol > 0; pass++) {
       hipLaunchKernelGGL(k_vdot_part<VC>, gp, dim3(kBlock), 0, st, Vb, ncol, x, dim, part);
-      hipLaunchKernelGGL(k_vdot_fin<VC>, dim3(ncol), dim3(kBlock), 0, st, part, G, h, coef, pass);
+      hipLaunchKernelGGL(k_vdot_fin<VC>, dim3(ncol), dim3(kBlock), 0, st, part, G, h, coef, pass,
+                         (const double*)nullptr, (const double*)nullptr);
       hipLaunchKernelGGL(k_vaxpy<VC>, dim3(G), dim3(kBlock), 0, st, Vb, ncol, h, x, dim,
                          pass == 1 ? npart : nullptr);
     }
@@ -1989,6 +2034,24 @@ struct Trlan {
                        jn >= 0 ? alpha : nullptr, beta);  // beta[m]: scratch slot
     if (out && jn >= 0)
       hipLaunchKernelGGL(k_scale_into<VC>, dim3(grid_for(dim)), dim3(kBlock), 0, st, x, out, beta + jn, dim);
+    return ED_OK;
+  }
+  // V[:, k0:k0+nout] = V[:, k0:k0+ncol] Y (Y on the device, ld ncol): in
+  // place up to 32 columns, else through Xb and a copy back
+  int rotate(int k0, int ncol, int nout, int g) {
+    const dim3 gr(std::min(g, 2048));
+    if (ncol <= 16)
+      hipLaunchKernelGGL((k_rotate_ip<VC, 16>), gr, dim3(kBlock), 0, st, col(Vb, k0), ncol, Y, ncol, nout, dim);
+    else if (ncol <= 32 && (!VC || ncol <= 24))
+      hipLaunchKernelGGL((k_rotate_ip<VC, VC ? 24 : 32>), gr, dim3(kBlock), 0, st, col(Vb, k0), ncol, Y, ncol,
+                         nout, dim);
+    else {
+      if (!Xb) CK(alloc((void**)&Xb, (size_t)mcap * dim * sizeof(V)));  // first use (nout < mcap)
+      hipLaunchKernelGGL(k_rotate<VC>, gr, dim3(kBlock), (size_t)ncol * nout * sizeof(double), st, col(Vb, k0),
+                         ncol, Y, ncol, nout, Xb, dim);
+      HIPCK(hipMemcpyAsync(col(Vb, k0), Xb, (size_t)nout * dim * sizeof(V), hipMemcpyDeviceToDevice, st));
+    }
+    HIPCK(hipGetLastError());
     return ED_OK;
   }
   // Lanczos step j: w = H V_j, CGS2, alpha_j, beta_j; V_{j+1} = w / beta_j
@@ -1999,8 +2062,59 @@ struct Trlan {
     CK(orth(j + 1, w, j, j + 1 < m ? col(Vb, j + 1) : nullptr));
     return ED_OK;
   }
+  template <bool HC, bool PK, int NC>
+  void psweep_launch(const TrlSweepArgs<HC>& a) {
+    const size_t lds = PG == 1 ? (size_t)dim * sizeof(V) : 0;  // solo: the gathered vector
+    hipLaunchKernelGGL((k_trl_sweep<HC, VC, PK, NC>), dim3(PG), dim3(kBlock), lds, st, a);
+  }
+  template <bool HC>
+  int psweep_t(int j0) {
+    using H = val_t<HC>;
+    TrlSweepArgs<HC> a;
+    a.diag = (const H*)s->d_diag;
+    a.sptr = s->d_sptr;
+    a.words = s->d_words;
+    a.dict = (const H*)s->d_pdict;
+    a.cols = s->d_cols;
+    a.vals = (const H*)s->d_vals;
+    a.dim = dim;
+    a.nslice = s->nslice;
+    a.Vb = Vb;
+    a.wbuf = wb;
+    a.wout = w;
+    a.p1 = part;
+    a.p2 = part2;
+    a.pn = npart;
+    a.alpha = alpha;
+    a.beta = beta;
+    a.bar = bar;
+    a.bar0 = bar_count;
+    a.j0 = j0;
+    a.m = m;
+    const bool pk = s->d_words != nullptr;
+    if (m <= 24) {
+      if (pk) psweep_launch<HC, true, 24>(a);
+      else psweep_launch<HC, false, 24>(a);
+    } else {
+      if (pk) psweep_launch<HC, true, 32>(a);
+      else psweep_launch<HC, false, 32>(a);
+    }
+    HIPCK(hipGetLastError());
+    bar_count += (unsigned int)(3 * PG * (m - j0));
+    HIPCK(hipMemcpyAsync(&abort_h, bar + 1, sizeof(unsigned int), hipMemcpyDeviceToHost, st));
+    return ED_OK;
+  }
   int sweep(int j0) {
     const int n = m - j0;
+    if constexpr (!VC) {
+      if (PG > 0 && m <= 32) {  // one launch for the whole sweep
+        PSweepSlot slot(PG);      // held until the sweep has finished
+        CK(psweep_t<false>(j0));
+        HIPCK(hipStreamSynchronize(st));
+        nhv += n;
+        return ED_OK;
+      }
+    }
     hipGraphExec_t ge = nullptr;
     for (auto& g : graphs)
       if (g.first == j0) ge = g.second;
@@ -2030,6 +2144,10 @@ struct Trlan {
 
 // blocks of the O(dim) Krylov sweeps
 static constexpr int kTrlanGridCap = 1024;
+// persistent sweeps (k_trl_sweep): sector size limit and rows per workgroup
+static constexpr int64_t kPSweepMaxDim = 131072;
+static constexpr int64_t kPSweepRows = 256;
+static constexpr int64_t kPSweepSolo = 2048;  // one workgroup, vector in LDS (<= 32 KB)
 
 // One thick-restart Lanczos solve on the columns [k0, m) of the basis; the
 // columns [0, k0) are locked (deflation: every new vector is orthogonalised
@@ -2068,6 +2186,7 @@ static int trlan_core(Trlan<VC>& T, int k0, int nev, int maxit, double tol, cons
       HIPCK(hipMemcpyAsync(al.data(), T.alpha, m * sizeof(double), hipMemcpyDeviceToHost, st));
       HIPCK(hipMemcpyAsync(be.data(), T.beta, m * sizeof(double), hipMemcpyDeviceToHost, st));
       HIPCK(hipStreamSynchronize(st));
+      if (T.abort_h) return fail(ED_ERR_HIP, "persistent Krylov sweep: grid barrier timed out");
       int jb = -1;
       for (int j = j0; j < m; j++) {
         const int l = j - k0;
@@ -2101,9 +2220,7 @@ static int trlan_core(Trlan<VC>& T, int k0, int nev, int maxit, double tol, cons
     // thick restart: keep nkeep Ritz vectors + the residual direction
     const int nkeep = std::max(nev, std::min(ma - 2, nev + (ma - nev) / 2));
     HIPCK(hipMemcpyAsync(T.Y, Z.data(), (size_t)ma * ma * sizeof(double), hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(k_rotate<VC>, dim3(std::min(g, 2048)), dim3(kBlock), (size_t)ma * nkeep * sizeof(double),
-                       st, T.col(T.Vb, k0), ma, T.Y, ma, nkeep, T.Xb, dim);
-    HIPCK(hipMemcpyAsync(T.col(T.Vb, k0), T.Xb, (size_t)nkeep * dim * vs, hipMemcpyDeviceToDevice, st));
+    CK(T.rotate(k0, ma, nkeep, g));
     hipLaunchKernelGGL(k_scale_into<VC>, dim3(g), dim3(kBlock), 0, st, T.w, T.col(T.Vb, k0 + nkeep),
                        T.beta + (m - 1), dim);
     HIPCK(hipGetLastError());
@@ -2149,33 +2266,42 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
   const int mp = (int)std::min<int64_t>(std::min(std::min(m, kProbeNcv), kTrlanMaxCols - nev), dim - nev);
   const bool verify = !(s->opts & ED_OPT_EIGH_NO_VERIFY) && dim > (int64_t)nev + 2 && mp >= 3;
   const int mcap = verify ? std::max(m, nev + mp) : m;
+  T.mcap = mcap;
   const size_t vs = sizeof(V);
   CK(T.alloc((void**)&T.Vb, (size_t)mcap * dim * vs));
-  CK(T.alloc((void**)&T.Xb, (size_t)mcap * dim * vs));
   CK(T.alloc((void**)&T.w, dim * vs));
   CK(T.alloc((void**)&T.h, kTrlanMaxCols * sizeof(double2)));
   CK(T.alloc((void**)&T.coef, kTrlanMaxCols * sizeof(double2)));
   CK(T.alloc((void**)&T.part, (size_t)kTrlanMaxCols * T.G * sizeof(double2)));
   CK(T.alloc((void**)&T.part2, (size_t)kTrlanMaxCols * T.G * sizeof(double2)));
   CK(T.alloc((void**)&T.npart, (size_t)T.G * sizeof(double)));
+  CK(T.alloc((void**)&T.npA, (size_t)T.G * sizeof(double)));
+  CK(T.alloc((void**)&T.npB, (size_t)T.G * sizeof(double)));
   CK(T.alloc((void**)&T.alpha, (kTrlanMaxCols + 8) * sizeof(double)));
   CK(T.alloc((void**)&T.beta, (kTrlanMaxCols + 8) * sizeof(double)));
   CK(T.alloc((void**)&T.Y, (size_t)mcap * mcap * sizeof(double)));
+  // persistent sweeps: whole stored sectors up to kPSweepMaxDim rows, about
+  // kPSweepRows rows per workgroup (opt-in: ED_OPT_TRLAN_PSWEEP; measured
+  // slower than the multi-kernel sweeps)
+  // (real vectors: the complex instantiations spill at the 2-per-CU bound)
+  if (!VC && T.path == 0 && T.fused && s->row0 == 0 && s->nrows == dim && dim <= kPSweepMaxDim &&
+      (s->opts & ED_OPT_TRLAN_PSWEEP) && (s->d_words || s->d_cols)) {
+    T.PG = dim <= kPSweepSolo ? 1 : (int)std::min<int64_t>((dim + kPSweepRows - 1) / kPSweepRows, 128);
+    CK(T.alloc((void**)&T.wb, 2 * dim * vs));
+    CK(T.alloc((void**)&T.bar, 2 * sizeof(unsigned int)));
+    HIPCK(hipMemsetAsync(T.bar, 0, 2 * sizeof(unsigned int), T.st));
+  }
   hipStream_t st = T.st;
   const int g = grid_for(dim);
   T.m = m;
   std::vector<double> theta, Z;
   int conv = 0;
   CK(trlan_core(T, 0, nev, maxit, tol, v0, 0, theta, Z, &conv));
-  // Ritz vectors -> Xb[0, nev)
+  // Ritz vectors -> Vb[0, nev): the result vectors live there from here on
+  // (locked columns of the deflated solves)
   HIPCK(hipMemcpyAsync(T.Y, Z.data(), (size_t)m * m * sizeof(double), hipMemcpyHostToDevice, st));
-  hipLaunchKernelGGL(k_rotate<VC>, dim3(std::min(g, 2048)), dim3(kBlock), (size_t)m * nev * sizeof(double), st,
-                     T.Vb, m, T.Y, m, nev, T.Xb, dim);
-  HIPCK(hipGetLastError());
+  CK(T.rotate(0, m, nev, g));
   std::vector<double> ev(theta.begin(), theta.begin() + nev);
-  // the result vectors live in Vb[0, nev) from here on (locked columns of the
-  // deflated solves, which use Xb as scratch)
-  HIPCK(hipMemcpyAsync(T.Vb, T.Xb, (size_t)nev * dim * vs, hipMemcpyDeviceToDevice, st));
   if (verify && conv == nev) {
     for (int round = 0; round < nev; round++) {
       // solve for the lowest eigenvalue on the complement of the nev vectors
@@ -2197,7 +2323,7 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
         if (!(c2 == 1 && th2[0] < cut)) break;
       }
       const double mu = th2[0];
-      // a missed eigenvalue: its Ritz vector -> Xb[nev], then insert in order
+      // a missed eigenvalue: its Ritz vector -> w, then insert in order
       // (drop the current largest)
       const int ma2 = T.m - nev;
       HIPCK(hipMemcpyAsync(T.Y, Z2.data(), (size_t)ma2 * sizeof(double), hipMemcpyHostToDevice, st));
@@ -2266,7 +2392,7 @@ static int kron_split(ed_sector* s, int part, int32_t vtype, int64_t o, int64_t 
 // ---------------------------------------------------------------- C-ABI
 extern "C" {
 
-const char* ed_gpu_last_error(void) { return g_err.c_str(); }
+const char* ed_gpu_last_error(void) { return ed_err_slot().c_str(); }
 
 // Jz_basis sectors: every off-diagonal element must land inside the sector
 // (the reference would insert it at column binary_search(...) = 0).  Host

@@ -79,7 +79,7 @@ extern "C" {
 #define ED_OPT_EIGH_NO_VERIFY 0x080 /* eigh: no deflated search for missed degenerate copies   */
 #define ED_OPT_TRLAN_UNFUSED  0x100 /* eigh: four-sweep CGS2 instead of the fused sweeps       */
 #define ED_OPT_TRLAN_NOFOLD   0x200 /* eigh: separate coefficient kernels on small grids       */
-#define ED_OPT_TRLAN_MULTI    0x400 /* eigh: multi-kernel expansion even for one-workgroup sectors */
+#define ED_OPT_TRLAN_PSWEEP   0x400 /* eigh: one persistent launch per expansion sweep (opt-in) */
 #define ED_OPT_NO_GRAPH       0x800 /* eigh: Krylov sweeps launched directly, not as hipGraphs  */
 
 /* status codes */

@@ -33,3 +33,4 @@ with Sector(cfg, *a.sector, stored=True, real=True, options=tuple(x for x in a.o
     torch.cuda.synchronize()
     print(f"sector {a.sector} dim {S.dim}: {(time.perf_counter() - t) / a.reps * 1e3:.3f} ms per eigh, "
           f"{nhv} H.v, nconv {nconv}", flush=True)
+    print("evals", " ".join(f"{float(x):.14f}" for x in w), flush=True)

@@ -30,6 +30,7 @@ ap.add_argument("--workers", type=int, default=8)
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--serial-stats", default="")
 ap.add_argument("--options", default="", help="comma-separated ED_OPT_* names for every sector")
+ap.add_argument("--timeline", default="", help="write per-sector (start, end, thread, dim) of the last rep")
 a = ap.parse_args()
 cfg = c4_config("random")
 opts = tuple(x for x in a.options.split(",") if x)
@@ -61,9 +62,38 @@ if a.serial_stats:
                        totals=tot, sectors=rows), f, indent=1)
 
 opt = DiagOptions(workers=a.workers)
+import threading  # noqa: E402
+
+from edgpu.diag import solve_sector  # noqa: E402
+
+events = []
+
+
+def timed_solver(cfg_, sec, opt_, device):
+    t0 = time.perf_counter()
+    r = solve_sector(cfg_, sec, opt_, device)
+    events.append(dict(sector=[sec.q1, sec.q2], dim=sec.dim, t0=t0, t1=time.perf_counter(),
+                       thread=threading.get_ident(), method=r.method))
+    return r
+
+
 for rep in range(a.reps):
+    events.clear()
     torch.cuda.synchronize()
     t = time.perf_counter()
-    res = farm_diag(cfg, opt)
+    res = farm_diag(cfg, opt, solver=timed_solver)
     torch.cuda.synchronize()
-    print(f"farm workers={a.workers} wall {time.perf_counter() - t:.4f} s states={res.states.size}", flush=True)
+    wall = time.perf_counter() - t
+    print(f"farm workers={a.workers} wall {wall:.4f} s states={res.states.size}", flush=True)
+    busy = sum(e["t1"] - e["t0"] for e in events)
+    first = min(e["t0"] for e in events) - t
+    last = max(e["t1"] for e in events) - t
+    print(f"  sector solves: sum {busy:.3f} s over {len(events)} (mean concurrency {busy / max(last - first, 1e-9):.2f}),"
+          f" first start {first * 1e3:.1f} ms, last end {last * 1e3:.1f} ms", flush=True)
+if a.timeline:
+    t0 = min(e["t0"] for e in events)
+    for e in events:
+        e["t0"] = round(e["t0"] - t0, 6)
+        e["t1"] = round(e["t1"] - t0, 6)
+    with open(a.timeline, "w") as f:
+        json.dump(events, f)

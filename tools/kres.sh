@@ -4,9 +4,21 @@
 set -eo pipefail
 T=$(mktemp -d)
 objcopy -O binary --only-section=.hip_fatbin "$1" "$T/fb.bin"
-/opt/rocm/lib/llvm/bin/clang-offload-bundler --unbundle --type=o --input="$T/fb.bin" \
-  --targets=hipv4-amdgcn-amd-amdhsa--gfx950 --output="$T/k.co"
-/opt/rocm/lib/llvm/bin/llvm-readelf --notes "$T/k.co" | python3 -c '
+# one offload bundle per translation unit: split at the bundle magic
+python3 - "$T" <<'PY'
+import sys
+d = sys.argv[1]
+b = open(d + "/fb.bin", "rb").read()
+mag = b"__CLANG_OFFLOAD_BUNDLE__"
+pos = [i for i in range(len(b)) if b.startswith(mag, i)]
+for k, i in enumerate(pos):
+    open("%s/fb%d.bin" % (d, k), "wb").write(b[i:pos[k + 1] if k + 1 < len(pos) else len(b)])
+PY
+for f in "$T"/fb[0-9]*.bin; do
+  /opt/rocm/lib/llvm/bin/clang-offload-bundler --unbundle --type=o --input="$f" \
+    --targets=hipv4-amdgcn-amd-amdhsa--gfx950 --output="${f%.bin}.co"
+done
+for f in "$T"/fb[0-9]*.co; do /opt/rocm/lib/llvm/bin/llvm-readelf --notes "$f"; done | python3 -c '
 import re, sys, subprocess
 pat = re.compile(sys.argv[1] if len(sys.argv) > 1 else ".")
 cur = {}
