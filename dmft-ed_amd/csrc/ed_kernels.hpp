@@ -783,27 +783,39 @@ __global__ void __launch_bounds__(kBlock) k_spmv_pk(const val_t<HC>* __restrict_
 // scalar loads.  Ops go in groups of kDirGroup with every gather of a group
 // issued before the group's terms are summed, in order, into the row: the
 // same products and additions as k_spmv, so H·v is bit-identical to the
-// stored kernel.  The diagonal is gen_row's own (gen_diag).  An op's kind is
-// scalar: down-level ops and pads skip the per-lane evaluation (uniform
-// branch); the group's LDS reads and gathers still issue back to back.  The
-// two directions of a hop on up levels are one op (kDirXor, build_direct):
-// ~half the per-lane evaluations of a normal-mode row.
+// stored kernel.  The diagonal is gen_row's own (gen_diag).  Targets come
+// from one formula (DirOp; a down-level op has no up bits in flip, so its
+// rank read is the lane's own rank); an op's kind is scalar, and only
+// up-level ops evaluate a per-lane condition and sign (uniform branch).  The
+// group's LDS reads and gathers issue back to back.  The two
+// directions of a hop on up levels are one op (kDirXor, build_direct): ~half
+// the per-lane evaluations of a normal-mode row.
 constexpr int kDirBlock = 1024;
 constexpr int kDirGroup = 4;
+// One op, evaluated the same way for every kind (no per-op branch):
+//   fires  = (m & req_mask) == req_val && popc(m & xm) == (kind has kDirXor)
+//   target = delta + rank[(m ^ flip) & up-mask]   (delta: first row of the
+//            target block; a down-level op has no up bits in flip, so this
+//            is the lane's own rank in the target block)
+//   sign   = (-1)^(popc(m & smask) + c0)          (down-level ops: smask 0,
+//            the block's sign resolved on the host into c0)
+// Pads: req_val = 1 with req_mask 0 (never fire).
 struct DirOp {
-  uint32_t req_mask, req_val, flip, smask;
-  int32_t delta;  // UNI: target row - own row; LANE: first row of the target block
-  int32_t kind;   // kDirLane | kDirC0 | kDirImSigned | kDirPad
-  double re, im;  // UNI: sign applied; LANE: before the sign
+  uint32_t req_mask, req_val, flip, smask, xm;
+  int32_t delta;
+  int32_t kind;   // kDirLane | kDirC0 | kDirImSigned | kDirPad | kDirXor
+  double re, im;  // before the sign
 };
 // kDirGroup ops field by field in 64-byte lines: one group is three
 // s_load_dwordx16 and one wait (op by op, the struct's fields came in
 // dependent scalar loads: ~70 round trips per chunk)
 struct __align__(64) DirGroup {
   uint32_t req_mask[kDirGroup], req_val[kDirGroup], flip[kDirGroup], smask[kDirGroup];
-  int32_t delta[kDirGroup], kind[kDirGroup], pad_[8];
+  int32_t delta[kDirGroup], kind[kDirGroup];
+  uint32_t xm[kDirGroup], pad_[4];
   double re[kDirGroup], im[kDirGroup];
 };
+static_assert(sizeof(DirGroup) == 192, "DirGroup: three 64-byte scalar loads");
 // kDirXor: merged hop pair, fires when exactly one of the two flip bits is set
 constexpr int kDirLane = 1, kDirC0 = 2, kDirImSigned = 4, kDirPad = 8, kDirXor = 16;
 struct DirChunk {
@@ -814,6 +826,18 @@ struct DirChunk {
   int32_t op0, nop;  // the block's ops: [op0, op0 + nop), nop a multiple of kDirGroup
   int32_t pad[2];
 };
+
+// element e of a vector through a raw buffer resource (byte offset e*sizeof)
+template <bool VC>
+__device__ __forceinline__ val_t<VC> ld_rsrc(__amdgpu_buffer_rsrc_t r, int e) {
+  if constexpr (VC) {
+    const auto q = __builtin_amdgcn_raw_buffer_load_b128(r, e * 16, 0, 0);
+    return __builtin_bit_cast(double2, q);
+  } else {
+    const auto q = __builtin_amdgcn_raw_buffer_load_b64(r, e * 8, 0, 0);
+    return __builtin_bit_cast(double, q);
+  }
+}
 
 __device__ __forceinline__ double flip_sign(double v, uint32_t neg) {
   return __longlong_as_double(__double_as_longlong(v) ^ ((long long)neg << 63));
@@ -869,6 +893,9 @@ __global__ void __launch_bounds__(kDirBlock) k_direct(const EdModel* __restrict_
     cend = nchunk;
     cstep = gridDim.x * (kDirBlock / 64);
   }
+  // gathers through a buffer resource: 32-bit element offsets (one VALU op
+  // per gather instead of a 64-bit address)
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, 0x7fffffff, 0x00020000);
   double part = 0.0;
   for (; c < cend; c += cstep) {
     const DirChunk ch = chunks[c];
@@ -885,37 +912,41 @@ __global__ void __launch_bounds__(kDirBlock) k_direct(const EdModel* __restrict_
     const int g1 = (ch.op0 + ch.nop) / kDirGroup;
     for (int gi = ch.op0 / kDirGroup; gi < g1; gi++) {
       const DirGroup G = grp[gi];
-      int tg[kDirGroup];
-      bool vd[kDirGroup];
-      H hv[kDirGroup];
       int rk[kDirGroup];
 #pragma unroll
       for (int j = 0; j < kDirGroup; j++) rk[j] = srank[(m ^ G.flip[j]) & mask];
+      // the four rank reads are issued here, not sunk under each op's
+      // condition (the compiler otherwise branches on EXEC per op)
+      asm volatile("" ::"v"(rk[0]), "v"(rk[1]), "v"(rk[2]), "v"(rk[3]));
+      int tg[kDirGroup];
+      bool vd[kDirGroup];
+      H hv[kDirGroup];
 #pragma unroll
       for (int j = 0; j < kDirGroup; j++) {
-        const int kind = G.kind[j];  // scalar: the branches below are uniform
-        if (kind & kDirLane) {
-          bool f = (m & G.req_mask[j]) == G.req_val[j];
-          if (kind & kDirXor) f = f & (__builtin_popcount(m & G.flip[j]) == 1);
-          const uint32_t neg = (uint32_t)(__builtin_popcount(m & G.smask[j]) + (kind >> 1)) & 1u;
-          vd[j] = f;
-          tg[j] = f ? G.delta[j] + rk[j] : row;
-          if constexpr (HC)
-            hv[j] = make_double2(flip_sign(G.re[j], neg), (kind & kDirImSigned) ? flip_sign(G.im[j], neg) : G.im[j]);
-          else
-            hv[j] = flip_sign(G.re[j], neg);
-        } else {  // down-level op (signed value, row offset) or pad (never fires)
-          vd[j] = !(kind & kDirPad);
-          tg[j] = row + G.delta[j];
-          hv[j] = mk<HC>(G.re[j], G.im[j]);
+        const uint32_t kind = (uint32_t)G.kind[j];  // scalar: the branch is uniform
+        bool f;
+        uint32_t neg;
+        if (kind & kDirLane) {  // per-lane condition and Jordan-Wigner sign
+          f = ((m & G.req_mask[j]) == G.req_val[j]) &
+              ((uint32_t)__builtin_popcount(m & G.xm[j]) == ((kind >> 4) & 1u));
+          neg = (uint32_t)(__builtin_popcount(m & G.smask[j]) + (kind >> 1)) & 1u;
+        } else {  // down-level op (fires, block sign in c0) or pad (never)
+          f = !(kind & kDirPad);
+          neg = (kind >> 1) & 1u;
         }
+        vd[j] = f;
+        tg[j] = f ? G.delta[j] + rk[j] : row;
+        if constexpr (HC)
+          hv[j] = make_double2(flip_sign(G.re[j], neg), (kind & kDirImSigned) ? flip_sign(G.im[j], neg) : G.im[j]);
+        else
+          hv[j] = flip_sign(G.re[j], neg);
       }
       V g[kDirGroup];
 #pragma unroll
-      for (int j = 0; j < kDirGroup; j++) g[j] = x[tg[j]];
+      for (int j = 0; j < kDirGroup; j++) g[j] = ld_rsrc<VC>(xr, tg[j]);
 #pragma unroll
       for (int j = 0; j < kDirGroup; j++)
-        if (vd[j]) acc = add(acc, mul(hv[j], g[j]));
+        acc = vd[j] ? add(acc, mul(hv[j], g[j])) : acc;  // a select, not an EXEC branch
     }
     if (on) part += epi.row((int64_t)row - row0, acc, xi);
   }

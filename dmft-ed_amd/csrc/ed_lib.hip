@@ -452,6 +452,7 @@ static bool dir_merge(DirOp& a, const DirOp& b, uint32_t nst) {
   a.req_mask &= ~fl;
   a.req_val &= ~fl;
   a.smask &= ~fl;
+  a.xm = fl;
   a.kind = (a.kind & ~kDirC0) | (pa ? kDirC0 : 0) | kDirXor;
   return true;
 }
@@ -460,14 +461,9 @@ static bool dir_merge(DirOp& a, const DirOp& b, uint32_t nst) {
 // fires?, target row, sign.
 static bool dir_apply(const DirOp& o, uint32_t m, uint32_t mask, int64_t row, const std::vector<uint32_t>& rank,
                       int64_t* tgt, double* sg) {
-  if (o.kind & kDirPad) return false;
-  if (!(o.kind & kDirLane)) {
-    *tgt = row + o.delta;
-    *sg = 1.0;
-    return true;
-  }
-  bool f = (m & o.req_mask) == o.req_val;
-  if (o.kind & kDirXor) f = f && __builtin_popcount(m & o.flip) == 1;
+  (void)row;
+  const bool f = (m & o.req_mask) == o.req_val &&
+                 (uint32_t)__builtin_popcount(m & o.xm) == (uint32_t)((o.kind & kDirXor) ? 1 : 0);
   if (!f) return false;
   *tgt = o.delta + (int64_t)rank[(m ^ o.flip) & mask];
   *sg = ((__builtin_popcount(m & o.smask) + ((o.kind & kDirC0) ? 1 : 0)) & 1) ? -1.0 : 1.0;
@@ -493,8 +489,8 @@ static int direct_ops_check(const ed_sector* s, const std::vector<DirOp>& ops, c
         double sg;
         if (!dir_apply(ops[k], m, mask, row, T.rank, &tg, &sg)) continue;
         const DirOp& o = ops[k];
-        const double re = (o.kind & kDirLane) ? o.re * sg : o.re;
-        const double im = (o.kind & kDirLane) && (o.kind & kDirImSigned) ? o.im * sg : o.im;
+        const double re = o.re * sg;
+        const double im = (o.kind & kDirImSigned) ? o.im * sg : o.im;
         if (q >= ref.k.size() || table_index(T, ref.k[q]) != tg || !same_bits(ref.re[q], re) ||
             !same_bits(ref.im[q], im))
           return fail(ED_ERR_STATE, "direct op lists differ from gen_row (row " + std::to_string(row) + ")");
@@ -530,12 +526,14 @@ static int build_direct(ed_sector* s) {
       const bool uni = ((c.req_mask | c.flip | c.smask) & (nst - 1)) == 0;
       DirOp o{};
       if (uni) {
+        // no up bits: always fires in this block, the lane's own rank in the
+        // target block, the block's Jordan-Wigner sign in c0
         if (off2 < 0) return fail(ED_ERR_STATE, "direct: a down-level term leaves the sector");
-        const double sg = ((__builtin_popcount(mdw & c.smask) + c.c0) & 1) ? -1.0 : 1.0;
-        o.delta = (int32_t)(off2 - T.off[idw]);
-        o.kind = 0;
-        o.re = c.re * sg;
-        o.im = c.im_signed ? c.im * sg : c.im;
+        const int neg = (__builtin_popcount(mdw & c.smask) + c.c0) & 1;
+        o.delta = off2;
+        o.kind = (neg ? kDirC0 : 0) | (c.im_signed ? kDirImSigned : 0);
+        o.re = c.re;
+        o.im = c.im;
       } else {
         if (off2 < 0) continue;  // no up pattern can reach an empty block
         o.req_mask = c.req_mask;
@@ -555,6 +553,7 @@ static int build_direct(ed_sector* s) {
     }
     while ((ops.size() - op0) % kDirGroup) {
       DirOp o{};
+      o.req_val = 1;  // (m & 0) != 1: never fires
       o.kind = kDirPad;
       ops.push_back(o);
     }
@@ -583,6 +582,7 @@ static int build_direct(ed_sector* s) {
     G.smask[j] = ops[q].smask;
     G.delta[j] = ops[q].delta;
     G.kind[j] = ops[q].kind;
+    G.xm[j] = ops[q].xm;
     G.re[j] = ops[q].re;
     G.im[j] = ops[q].im;
   }
