@@ -48,6 +48,7 @@ for e in "${ENTRIES[@]}"; do
   done
   python3 "$R/tools/traffic_json.py" "$PROF/${name}_traffic.json" "$pat" "$OUT/pmc_${name}_FETCH_SIZE" \
     "$OUT/pmc_${name}_WRITE_SIZE" "spmv_probe.py $args" > /dev/null || { echo "traffic $name failed"; exit 1; }
+  mkdir -p "$R/profiles/$TAG" && cp "$PROF/${name}_traffic.json" "$R/profiles/$TAG/"  # for a bench.py later in the same call
   echo "profile $name ok"
 done
 find "$OUT" -name "*kernel_trace.csv" -size +2M -delete
