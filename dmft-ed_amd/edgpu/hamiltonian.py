@@ -196,8 +196,15 @@ class Sector:
         return float(egs[0]), out, int(n.value)
 
     def lanc_run(self, niter: int, v0_dev=None, real: Optional[bool] = None):
-        """Fixed-length device Lanczos (benchmark): returns (alpha, beta, ms)."""
+        """Fixed-length device Lanczos (benchmark): returns (alpha, beta, ms).
+        The vector type follows `real`, else the start vector's dtype (a
+        complex tensor runs complex(8) vectors), else the sector's."""
+        if real is None and v0_dev is not None:
+            real = not v0_dev.is_complex()
         vt = 0 if (self.real if real is None else real) else 1
+        if v0_dev is not None:
+            if v0_dev.is_complex() != (vt == 1) or v0_dev.numel() != self.dim or not v0_dev.is_contiguous():
+                raise ValueError("lanc_run: v0_dev must be a contiguous length-dim vector of the run's type")
         a = np.zeros(niter)
         b = np.zeros(niter)
         ms = ctypes.c_float()
