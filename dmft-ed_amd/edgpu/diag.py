@@ -54,6 +54,9 @@ class DiagOptions:
     # sectors solved concurrently on one GPU (host threads, one HIP stream per
     # sector; ctypes releases the GIL): small sectors are launch-latency bound
     workers: int = 8
+    # ED_OPT_* kernel alternatives (Sector.set_options names) for every sector
+    # of the diagonalisation (A/B runs; the defaults are the measured best)
+    kernel_options: Tuple[str, ...] = ()
 
 
 @dataclass
@@ -123,7 +126,8 @@ def solve_sector(cfg: EDConfig, sec: SectorId, opt: DiagOptions, device: int = 0
     real = cfg.is_real()
     q = (sec.q1, sec.q2)
     if not lanc_solve:
-        with Sector(cfg, sec.q1, sec.q2, stored=True, real=real, device=device) as S:
+        with Sector(cfg, sec.q1, sec.q2, stored=True, real=real, device=device,
+                    options=opt.kernel_options) as S:
             rp, cols, vals = S.dump_csr()
         H = np.zeros((dim, dim), dtype=np.complex128)
         rows = np.repeat(np.arange(dim), np.diff(rp))
@@ -133,7 +137,8 @@ def solve_sector(cfg: EDConfig, sec: SectorId, opt: DiagOptions, device: int = 0
         w, v = np.linalg.eigh(H)
         vec = v[:, :neigen] if opt.keep_vectors else None
         return SectorResult(sec.isector, q, dim, w, neigen, vec, "dense")
-    with Sector(cfg, sec.q1, sec.q2, stored=True, real=real, device=device) as S:
+    with Sector(cfg, sec.q1, sec.q2, stored=True, real=real, device=device,
+                options=opt.kernel_options) as S:
         if opt.lanc_method == "lanczos":
             e0, vec, _ = S.lanc_eigh(nitermax=nitermax, threshold=opt.lanc_tolerance,
                                      v0=_start_vector(dim, not real), vector=opt.keep_vectors,

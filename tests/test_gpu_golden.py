@@ -26,15 +26,19 @@ def _load(name):
         return json.load(fh)
 
 
-@pytest.mark.parametrize("bath", ["flat", "random"])
-def test_c4_all_sectors_match_fixture(bath):
+@pytest.mark.parametrize("bath,kopts", [("flat", ()), ("random", ()), ("random", ("trlan_unfused",))],
+                         ids=["flat", "random", "random-unfused"])
+def test_c4_all_sectors_match_fixture(bath, kopts):
+    """All 169 configs[3] sectors through the farm against the dense fixture
+    (1e-10 of |E0|); also with the always-two-pass CGS2 (ED_OPT_TRLAN_UNFUSED,
+    DiagOptions.kernel_options) against the default DGKS-conditional pass."""
     from edgpu.diag import DiagOptions
     from edgpu.farm import farm_diag
     from golden.golden_configs import c4_config
 
     gold = _load(f"c4_diag_{bath}.json")
     cfg = c4_config(bath)
-    res = farm_diag(cfg, DiagOptions())
+    res = farm_diag(cfg, DiagOptions(kernel_options=kopts))
     assert len(res.eigenvalues) == len(gold["sectors"]) == 169
     scale = abs(gold["E0"])
     worst = 0.0

@@ -61,7 +61,7 @@ if a.serial_stats:
         json.dump(dict(config="configs[3] random bath, Lanczos sectors, one thread", options=list(opts),
                        totals=tot, sectors=rows), f, indent=1)
 
-opt = DiagOptions(workers=a.workers)
+opt = DiagOptions(workers=a.workers, kernel_options=opts)
 import threading  # noqa: E402
 
 from edgpu.diag import solve_sector  # noqa: E402
