@@ -1964,6 +1964,7 @@ struct Trlan {
   unsigned int* bar = nullptr;   // [0] arrival counter, [1] abort word
   unsigned int bar_count = 0;    // counter value after the last launch
   unsigned int abort_h = 0;      // abort word read back with alpha/beta
+  double* hp = nullptr;          // pinned staging (trlan_pinned)
   std::vector<void*> mine;
   std::vector<std::pair<int, hipGraphExec_t>> graphs;
   int nhv = 0;
@@ -2142,6 +2143,20 @@ struct Trlan {
   }
 };
 
+// Pinned host staging of the per-restart copies (alpha/beta down, the
+// projected eigenvectors up): pageable copies go through the runtime's
+// staging buffer, a CPU copy and an extra wait each, three per restart.  One
+// buffer per host thread, allocated on first use and kept (a farm worker
+// reuses it for every sector; freeing pinned memory can synchronise the
+// device under the other workers' streams).
+static constexpr int kPinnedDoubles = 2 * (64 + 8) + 64 * 64 + 16;
+static double* trlan_pinned() {
+  static thread_local double* buf = nullptr;
+  if (!buf && hipHostMalloc((void**)&buf, kPinnedDoubles * sizeof(double), hipHostMallocDefault) != hipSuccess)
+    buf = nullptr;
+  return buf;
+}
+
 // blocks of the O(dim) Krylov sweeps
 static constexpr int kTrlanGridCap = 1024;
 // persistent sweeps (k_trl_sweep): sector size limit and rows per workgroup
@@ -2169,9 +2184,14 @@ static int trlan_core(Trlan<VC>& T, int k0, int nev, int maxit, double tol, cons
   else if (seed == 0) hipLaunchKernelGGL(k_default_start, dim3(grid_for(nd)), dim3(kBlock), 0, st, (double*)T.w, nd);
   else hipLaunchKernelGGL(k_hash_vec, dim3(grid_for(nd)), dim3(kBlock), 0, st, (double*)T.w, nd, seed);
   CK(T.orth(k0, T.w, -1));  // CGS2 against the locked columns; the norm -> beta[m]
-  double b0 = 0.0;
-  HIPCK(hipMemcpyAsync(&b0, T.beta + m, sizeof(double), hipMemcpyDeviceToHost, st));
+  double* const hp = T.hp;  // pinned: [0, 72) alpha, [72, 144) beta, [144, ...) Z, last: scalars
+  double* const hal = hp;
+  double* const hbe = hp + 72;
+  double* const hZ = hp + 144;
+  double* const hs = hp + kPinnedDoubles - 8;
+  HIPCK(hipMemcpyAsync(hs, T.beta + m, sizeof(double), hipMemcpyDeviceToHost, st));
   HIPCK(hipStreamSynchronize(st));
+  const double b0 = hs[0];
   if (!(b0 > 0.0)) return fail(ED_ERR_ARG, "zero start vector");
   hipLaunchKernelGGL(k_scale_into<VC>, dim3(g), dim3(kBlock), 0, st, T.w, T.col(T.Vb, k0), T.beta + m, dim);
 
@@ -2183,9 +2203,11 @@ static int trlan_core(Trlan<VC>& T, int k0, int nev, int maxit, double tol, cons
     int j0 = jstart;
     for (;;) {  // expansion j0..m-1, restarted past an invariant subspace
       CK(T.sweep(j0));
-      HIPCK(hipMemcpyAsync(al.data(), T.alpha, m * sizeof(double), hipMemcpyDeviceToHost, st));
-      HIPCK(hipMemcpyAsync(be.data(), T.beta, m * sizeof(double), hipMemcpyDeviceToHost, st));
+      HIPCK(hipMemcpyAsync(hal, T.alpha, m * sizeof(double), hipMemcpyDeviceToHost, st));
+      HIPCK(hipMemcpyAsync(hbe, T.beta, m * sizeof(double), hipMemcpyDeviceToHost, st));
       HIPCK(hipStreamSynchronize(st));
+      std::copy(hal, hal + m, al.begin());
+      std::copy(hbe, hbe + m, be.begin());
       if (T.abort_h) return fail(ED_ERR_HIP, "persistent Krylov sweep: grid barrier timed out");
       int jb = -1;
       for (int j = j0; j < m; j++) {
@@ -2219,7 +2241,9 @@ static int trlan_core(Trlan<VC>& T, int k0, int nev, int maxit, double tol, cons
     if (conv == nev || it == maxit - 1 || m == dim) break;
     // thick restart: keep nkeep Ritz vectors + the residual direction
     const int nkeep = std::max(nev, std::min(ma - 2, nev + (ma - nev) / 2));
-    HIPCK(hipMemcpyAsync(T.Y, Z.data(), (size_t)ma * ma * sizeof(double), hipMemcpyHostToDevice, st));
+    // (the previous restart's upload of hZ completed at this sweep's sync)
+    std::copy(Z.begin(), Z.begin() + (size_t)ma * ma, hZ);
+    HIPCK(hipMemcpyAsync(T.Y, hZ, (size_t)ma * ma * sizeof(double), hipMemcpyHostToDevice, st));
     CK(T.rotate(k0, ma, nkeep, g));
     hipLaunchKernelGGL(k_scale_into<VC>, dim3(g), dim3(kBlock), 0, st, T.w, T.col(T.Vb, k0 + nkeep),
                        T.beta + (m - 1), dim);
@@ -2254,6 +2278,8 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
   T.st = s->stream;
   T.dim = s->dim;
   T.G = (int)std::min<int64_t>(grid_for(s->dim), kTrlanGridCap);
+  T.hp = trlan_pinned();
+  if (!T.hp) return fail(ED_ERR_OOM, "pinned host staging buffer");
   T.fused = !(s->opts & ED_OPT_TRLAN_UNFUSED);
   if (s->opts & ED_OPT_TRLAN_NOFOLD) T.kFinFoldG = 0;
   T.graphs_on = !(s->opts & ED_OPT_NO_GRAPH);
@@ -2299,7 +2325,8 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
   CK(trlan_core(T, 0, nev, maxit, tol, v0, 0, theta, Z, &conv));
   // Ritz vectors -> Vb[0, nev): the result vectors live there from here on
   // (locked columns of the deflated solves)
-  HIPCK(hipMemcpyAsync(T.Y, Z.data(), (size_t)m * m * sizeof(double), hipMemcpyHostToDevice, st));
+  std::copy(Z.begin(), Z.begin() + (size_t)m * m, T.hp + 144);
+  HIPCK(hipMemcpyAsync(T.Y, T.hp + 144, (size_t)m * m * sizeof(double), hipMemcpyHostToDevice, st));
   CK(T.rotate(0, m, nev, g));
   std::vector<double> ev(theta.begin(), theta.begin() + nev);
   if (verify && conv == nev) {
@@ -2326,7 +2353,8 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
       // a missed eigenvalue: its Ritz vector -> w, then insert in order
       // (drop the current largest)
       const int ma2 = T.m - nev;
-      HIPCK(hipMemcpyAsync(T.Y, Z2.data(), (size_t)ma2 * sizeof(double), hipMemcpyHostToDevice, st));
+      std::copy(Z2.begin(), Z2.begin() + ma2, T.hp + 144);
+      HIPCK(hipMemcpyAsync(T.Y, T.hp + 144, (size_t)ma2 * sizeof(double), hipMemcpyHostToDevice, st));
       hipLaunchKernelGGL(k_rotate<VC>, dim3(std::min(g, 2048)), dim3(kBlock), (size_t)ma2 * sizeof(double), st,
                          T.col(T.Vb, nev), ma2, T.Y, ma2, 1, T.w, dim);
       HIPCK(hipGetLastError());
