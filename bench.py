@@ -372,8 +372,10 @@ def roofline_sweep(Sector, make_config):
         td, tdsrc = _traffic(f"direct_{name}_traffic.json")
         row["direct_generic"] = {"ms_per_hxv": round(msd, 4),
                                  "frac_16dim": round(16 * dim / (msd * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                 "own_bytes": 24 * dim,  # v read, Hv written, diagonal vector read
+                                 "frac_own": round(24 * dim / (msd * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                                  "traffic": td, "traffic_source": tdsrc,
-                                 "kernel": "k_direct (wave per 64-row chunk, op lists, LDS rank tables)"}
+                                 "kernel": "k_direct (wave per 64-row chunk, op lists, LDS rank tables, diagonal vector from k_gen_diag)"}
         out[name] = row
     out["workloads"] = {"n28b": "Norb=2 Nbath=6 (Nlevels=28) (7,7) sector, random bath, real(8)",
                         "c4_66": "configs[3] Norb=2 Nbath=5 half-filled (6,6) sector, random bath, real(8)",
@@ -534,8 +536,10 @@ def main():
             _, _, msd = measure_hxv(Sector, cfg28, (7, 7), 20, path=1)
             td, tdsrc = _traffic("direct_n28_traffic.json")
             kron["direct_generic"] = {"ms_per_hxv": round(msd, 4),
-                                      "kernel": "k_direct (wave per 64-row chunk, op lists, LDS rank tables)",
+                                      "kernel": "k_direct (wave per 64-row chunk, op lists, LDS rank tables, diagonal vector from k_gen_diag)",
                                       "frac_16dim": round(Bk / (msd * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                      "own_bytes": 24 * dimk,  # v read, Hv written, diagonal vector read
+                                      "frac_own": round(24 * dimk / (msd * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                                       "traffic": td, "traffic_source": tdsrc}
             infc = {}
             _, _, msc = measure_hxv(Sector, cfg28, (7, 7), 20, path=0, info=infc, cplx=True)

@@ -325,6 +325,38 @@ struct EpiStore {
   __device__ __forceinline__ void finish(double) {}
 };
 
+// Thick-restart Lanczos step j past a restart (Trlan::step, ed_lib.hip):
+// the three-term part of the recurrence is applied as H v_j is stored, with
+// the spectral shift sigma = alpha_{j-1},
+//   w = (H - sigma) v_j - beta_{j-1} v_{j-1}
+// (alpha_j = sigma + <v_j, w>, k_coef_scale).  The Gram-Schmidt pass then
+// meets only the remainder: ARPACK's DGKS test (||w'|| > 0.717 ||w||, which
+// bounds the growth of the basis' orthogonality error) passes whenever
+// |alpha_j - alpha_{j-1}| < 0.97 beta_j, and the second pass over the basis
+// is skipped.  On the raw w = H v_j the test can never pass (w carries
+// beta_{j-1} v_{j-1} and alpha_j v_j: ||w'|| / ||w|| < 1/sqrt(2)).
+template <bool VC>
+struct EpiTrlLoc {
+  using V = val_t<VC>;
+  V* hv;
+  const V* vprev;        // v_{j-1}
+  const double* sig;     // &alpha[j-1]
+  const double* bprev;   // &beta[j-1]
+  double s = 0.0, b = 0.0;
+  V* scratch() const { return hv; }
+  __device__ __forceinline__ bool skip() const { return false; }
+  __device__ __forceinline__ void prepare() {
+    s = *sig;
+    b = *bprev;
+  }
+  __device__ __forceinline__ double row(int64_t i, V acc, V xi) {
+    hv[i] = sub(sub(acc, scl(s, xi)), scl(b, vprev[i]));
+    return 0.0;
+  }
+  template <int NT = kBlock>
+  __device__ __forceinline__ void finish(double) {}
+};
+
 // Device scalars of one Lanczos run.
 struct LancState {
   double beta;    // b of the previous iteration (normalisation of R)
@@ -783,7 +815,10 @@ __global__ void __launch_bounds__(kBlock) k_spmv_pk(const val_t<HC>* __restrict_
 // scalar loads.  Ops go in groups of kDirGroup with every gather of a group
 // issued before the group's terms are summed, in order, into the row: the
 // same products and additions as k_spmv, so H·v is bit-identical to the
-// stored kernel.  The diagonal is gen_row's own (gen_diag).  Targets come
+// stored kernel.  The diagonal is gen_row's own (gen_diag), evaluated once
+// per sector by k_gen_diag into a vector (8 or 16 B per row): re-running
+// gen_diag's loops (~30 dependent f64 adds at Nlevels=28, half-rate f64
+// VALU) in every H·v was a quarter of the kernel's instructions.  Targets come
 // from one formula (DirOp; a down-level op has no up bits in flip, so its
 // rank read is the lane's own rank); an op's kind is scalar, and only
 // up-level ops evaluate a per-lane condition and sign (uniform branch).  The
@@ -843,8 +878,23 @@ __device__ __forceinline__ double flip_sign(double v, uint32_t neg) {
   return __longlong_as_double(__double_as_longlong(v) ^ ((long long)neg << 63));
 }
 
+// Diagonal of every row of a matrix-free sector: gen_diag, the value the
+// stored build puts in its diagonal slot (k_fill), so k_direct stays
+// bit-identical to k_spmv.
+template <bool HC>
+__global__ void __launch_bounds__(kBlock) k_gen_diag(const EdModel* __restrict__ Mp,
+                                                     const uint32_t* __restrict__ map, int64_t n,
+                                                     val_t<HC>* __restrict__ out) {
+  const EdModel& M = *Mp;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    double re, im;
+    gen_diag(M, map[i], &re, &im);
+    out[i] = mk<HC>(re, im);
+  }
+}
+
 template <bool HC, bool VC, bool PATLDS, class Epi>
-__global__ void __launch_bounds__(kDirBlock) k_direct(const EdModel* __restrict__ Mp,
+__global__ void __launch_bounds__(kDirBlock) k_direct(const val_t<HC>* __restrict__ ddiag,
                                                       const DirChunk* __restrict__ chunks, int nchunk,
                                                       const DirGroup* __restrict__ grp,
                                                       const uint16_t* __restrict__ rank_g,
@@ -870,11 +920,6 @@ __global__ void __launch_bounds__(kDirBlock) k_direct(const EdModel* __restrict_
       if (PATLDS) spat[q] = pat_g[q];
     }
   }
-  // the model constants in LDS: gen_diag's loops read them as broadcast LDS
-  // loads (from the scalar cache every loop iteration waited on its loads)
-  __shared__ EdModel M;
-  for (int q = threadIdx.x; q < (int)(sizeof(EdModel) / 4); q += kDirBlock)
-    ((uint32_t*)&M)[q] = ((const uint32_t*)Mp)[q];
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // chunk data and ops: scalar loads
@@ -905,10 +950,8 @@ __global__ void __launch_bounds__(kDirBlock) k_direct(const EdModel* __restrict_
     if constexpr (PATLDS) up = spat[ch.pat0 + (on ? lane : 0)];
     else up = map[row] & mask;
     const uint32_t m = up | (ch.idw << ns);
-    double dre, dim_;
-    gen_diag(M, m, &dre, &dim_);
     const V xi = x[row];
-    V acc = add(vzero<V>(), mul(mk<HC>(dre, dim_), xi));
+    V acc = add(vzero<V>(), mul(ddiag[row - row0], xi));
     const int g1 = (ch.op0 + ch.nop) / kDirGroup;
     for (int gi = ch.op0 / kDirGroup; gi < g1; gi++) {
       const DirGroup G = grp[gi];

@@ -108,6 +108,7 @@ struct ed_sector {
   int ndchunk = 0;
   DirGroup* d_dops = nullptr;
   uint16_t *d_rank16 = nullptr, *d_pat16 = nullptr;
+  void* d_ddiag = nullptr;   // gen_diag of the sector object's rows (k_gen_diag)
   bool dir_patlds = false;
   int dir_lds = 0, dir_grid = 0;
   // matrix-free, Kronecker form
@@ -597,6 +598,17 @@ static int build_direct(ed_sector* s) {
   CK(upload(s, &s->d_dops, groups));
   CK(upload(s, &s->d_rank16, rk));
   CK(upload(s, &s->d_pat16, pt));
+  // the rows' diagonal, once (k_direct reads it instead of running gen_diag)
+  CK(dalloc(s, &s->d_ddiag, (size_t)std::max<int64_t>(s->nrows, 1) * (s->hc ? 16 : 8)));
+  if (s->nrows > 0) {
+    if (s->hc)
+      hipLaunchKernelGGL(k_gen_diag<true>, dim3(grid_for(s->nrows)), dim3(kBlock), 0, s->stream, s->Md,
+                         s->d_map + s->row0, s->nrows, (double2*)s->d_ddiag);
+    else
+      hipLaunchKernelGGL(k_gen_diag<false>, dim3(grid_for(s->nrows)), dim3(kBlock), 0, s->stream, s->Md,
+                         s->d_map + s->row0, s->nrows, (double*)s->d_ddiag);
+    HIPCK(hipGetLastError());
+  }
   // both tables in LDS up to Ns = 15 (128 KB); at Ns = 16 the rank table
   // alone (128 KB), the row's own pattern then read from H%map
   s->dir_patlds = 4 * (int64_t)rk.size() <= 128 * 1024;
@@ -627,7 +639,8 @@ static int launch_direct(ed_sector* s, const void* x, Epi epi, hipStream_t st) {
     (void)hipGetLastError();  // not sticky for later launches
     return fail(ED_ERR_HIP, std::string("k_direct LDS attribute -> ") + hipGetErrorString(ae));
   }
-  hipLaunchKernelGGL(fn, dim3(s->dir_grid), dim3(kDirBlock), s->dir_lds, st, s->Md, s->d_dchunk, s->ndchunk,
+  hipLaunchKernelGGL(fn, dim3(s->dir_grid), dim3(kDirBlock), s->dir_lds, st, (const val_t<HC>*)s->d_ddiag,
+                     s->d_dchunk, s->ndchunk,
                      s->d_dops, s->d_rank16, s->d_pat16, s->d_map, s->T.ns, (const V*)x, s->row0, epi);
   return ED_OK;
 }
@@ -1956,6 +1969,7 @@ struct Trlan {
   // (every block re-reads G x ncol partials; 0 with ED_OPT_TRLAN_NOFOLD: A/B)
   int kFinFoldG = 128;
   bool graphs_on = true;  // false (ED_OPT_NO_GRAPH): sweeps launched directly
+  bool solo = true;       // false (ED_OPT_TRLAN_NOSOLO): multi-kernel CGS on small sectors too (A/B)
   double *Y = nullptr, *npart = nullptr, *alpha = nullptr, *beta = nullptr;
   double *npA = nullptr, *npB = nullptr;  // |w|^2 partials before / after the first CGS pass (DGKS)
   // persistent sweep (k_trl_sweep): grid, ping-pong residuals, barrier words
@@ -1995,7 +2009,25 @@ struct Trlan {
 #undef ED_CGS
     return true;
   }
-  int orth(int ncol, V* x, int jn, V* out = nullptr) {
+  int orth(int ncol, V* x, int jn, V* out = nullptr, int shifted = 0) {
+    // small sectors: the whole CGS2 + alpha/beta + V_{j+1} in one workgroup
+    // (complex vectors: up to 16 columns; the 24/32-column forms spill)
+    if (fused && solo && ncol > 0 && dim <= kOrthSoloMaxDim && ncol <= (VC ? 16 : 32)) {
+      V* const o = (out && jn >= 0) ? out : nullptr;
+      const int js = jn >= 0 ? jn : m;  // beta[m]: scratch slot
+      const int nc = (ncol + 7) / 8 * 8;
+#define ED_OSOLO(NCV)                                                                                          \
+  hipLaunchKernelGGL((k_orth_solo<VC, NCV>), dim3(1), dim3(kOrthSoloBlock), 0, st, Vb, ncol, x, dim, coef,     \
+                     jn >= 0 ? alpha : nullptr, beta, jn, js, o, shifted)
+      if (nc <= 8) ED_OSOLO(8);
+      else if (nc <= 16) ED_OSOLO(16);
+      else if constexpr (!VC) {
+        if (nc <= 24) ED_OSOLO(24);
+        else ED_OSOLO(32);
+      }
+#undef ED_OSOLO
+      return ED_OK;
+    }
     // fused CGS: dots + |x|^2 | x -= V h1, dots, |x'|^2 | (DGKS: only if
     // |x'| <= 0.717 |x|) x -= V h2, |x''|^2 — V streamed 2x or 3x
     if (fused && ncol > 0 && cgs(ncol, nullptr, x, part, npA)) {
@@ -2014,10 +2046,10 @@ struct Trlan {
       }
       if (out && jn >= 0)  // + V_{j+1} = x / beta_j in the same launch
         hipLaunchKernelGGL(k_coef_scale<VC>, dim3(G), dim3(kBlock), 0, st, npart, G, coef, jn, alpha, beta,
-                           x, out, dim);
+                           x, out, dim, shifted);
       else
         hipLaunchKernelGGL(k_trl_coef, dim3(1), dim3(kBlock), 0, st, npart, G, coef, jn >= 0 ? jn : m,
-                           jn >= 0 ? alpha : nullptr, beta);
+                           jn >= 0 ? alpha : nullptr, beta, jn >= 0 ? shifted : 0);
       return ED_OK;
     }
     if (ncol == 0) {
@@ -2032,7 +2064,7 @@ struct Trlan {
                          pass == 1 ? npart : nullptr);
     }
     hipLaunchKernelGGL(k_trl_coef, dim3(1), dim3(kBlock), 0, st, npart, G, coef, jn >= 0 ? jn : m,
-                       jn >= 0 ? alpha : nullptr, beta);  // beta[m]: scratch slot
+                       jn >= 0 ? alpha : nullptr, beta, jn >= 0 ? shifted : 0);  // beta[m]: scratch slot
     if (out && jn >= 0)
       hipLaunchKernelGGL(k_scale_into<VC>, dim3(grid_for(dim)), dim3(kBlock), 0, st, x, out, beta + jn, dim);
     return ED_OK;
@@ -2055,12 +2087,23 @@ struct Trlan {
     HIPCK(hipGetLastError());
     return ED_OK;
   }
-  // Lanczos step j: w = H V_j, CGS2, alpha_j, beta_j; V_{j+1} = w / beta_j
-  int step(int j) {
+  // Lanczos step j: w = H V_j, CGS2, alpha_j, beta_j; V_{j+1} = w / beta_j.
+  // Past the sweep's first column (j > j0) the H·v applies the shifted
+  // three-term recurrence (EpiTrlLoc) so that the DGKS test can skip the
+  // second Gram-Schmidt pass; the first column after a restart couples to
+  // every kept Ritz vector and takes the plain product.
+  bool local = true;  // false (ED_OPT_TRLAN_NOLOCAL): plain w = H V_j every step (A/B)
+  int step(int j, int j0) {
     nhv++;
-    EpiStore<VC> e{w};
-    CK(launch_hxv<VC>(s, path, col(Vb, j), e, st));
-    CK(orth(j + 1, w, j, j + 1 < m ? col(Vb, j + 1) : nullptr));
+    const bool loc = local && j > j0;
+    if (loc) {
+      EpiTrlLoc<VC> e{w, col(Vb, j - 1), alpha + (j - 1), beta + (j - 1)};
+      CK(launch_hxv<VC>(s, path, col(Vb, j), e, st));
+    } else {
+      EpiStore<VC> e{w};
+      CK(launch_hxv<VC>(s, path, col(Vb, j), e, st));
+    }
+    CK(orth(j + 1, w, j, j + 1 < m ? col(Vb, j + 1) : nullptr, loc ? 1 : 0));
     return ED_OK;
   }
   template <bool HC, bool PK, int NC>
@@ -2123,7 +2166,7 @@ struct Trlan {
       hipGraph_t g;
       HIPCK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
       int rc = ED_OK;
-      for (int j = j0; j < m && rc == ED_OK; j++) rc = step(j);
+      for (int j = j0; j < m && rc == ED_OK; j++) rc = step(j, j0);
       hipError_t e2 = hipStreamEndCapture(st, &g);
       if (rc != ED_OK) return rc;
       HIPCK(e2);
@@ -2136,7 +2179,7 @@ struct Trlan {
       HIPCK(hipGraphLaunch(ge, st));
       nhv += n;
     } else {
-      for (int j = j0; j < m; j++) CK(step(j));
+      for (int j = j0; j < m; j++) CK(step(j, j0));
     }
     HIPCK(hipGetLastError());
     return ED_OK;
@@ -2283,6 +2326,8 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
   T.fused = !(s->opts & ED_OPT_TRLAN_UNFUSED);
   if (s->opts & ED_OPT_TRLAN_NOFOLD) T.kFinFoldG = 0;
   T.graphs_on = !(s->opts & ED_OPT_NO_GRAPH);
+  T.local = !(s->opts & ED_OPT_TRLAN_NOLOCAL);
+  T.solo = !(s->opts & ED_OPT_TRLAN_NOSOLO);
   const int64_t dim = s->dim;
   const int m = (int)std::min<int64_t>(ncv, dim);
   if (nev < 1 || nev >= m) return fail(ED_ERR_ARG, "need 1 <= nev < min(ncv, dim)");
@@ -2563,7 +2608,7 @@ int ed_sector_destroy(ed_sector* s) {
 
 int ed_sector_set_options(ed_sector* s, int32_t opts) {
   if (!s) return fail(ED_ERR_ARG, "null");
-  if (opts & ~0xfff) return fail(ED_ERR_ARG, "unknown ED_OPT_* bits");
+  if (opts & ~0x3fff) return fail(ED_ERR_ARG, "unknown ED_OPT_* bits");
   if (opts != s->opts) drop_graph(s);  // a captured recurrence bakes in the kernel choice
   s->opts = opts;
   return ED_OK;

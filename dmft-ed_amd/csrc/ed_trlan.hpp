@@ -137,13 +137,14 @@ __global__ void __launch_bounds__(kBlock) k_vaxpy(const val_t<VC>* __restrict__ 
 // beta[j] = ||w|| from the partials; alpha[j] = Re coef[j]
 static __global__ void __launch_bounds__(kBlock) k_trl_coef(const double* __restrict__ npart, int G,
                                                      const double2* __restrict__ coef, int j,
-                                                     double* __restrict__ alpha, double* __restrict__ beta) {
+                                                     double* __restrict__ alpha, double* __restrict__ beta,
+                                                     int shifted = 0) {
   double t = 0.0;
   for (int b = threadIdx.x; b < G; b += kBlock) t += npart[b];
   t = block_sum(t);
   if (threadIdx.x == 0) {
     beta[j] = sqrt(t);
-    if (alpha) alpha[j] = coef[j].x;
+    if (alpha) alpha[j] = shifted ? alpha[j - 1] + coef[j].x : coef[j].x;  // (EpiTrlLoc)
   }
 }
 
@@ -218,14 +219,16 @@ __global__ void __launch_bounds__(kBlock) k_coef_scale(const double* __restrict_
                                                        const double2* __restrict__ coef, int j,
                                                        double* __restrict__ alpha, double* __restrict__ beta,
                                                        const val_t<VC>* __restrict__ x,
-                                                       val_t<VC>* __restrict__ out, int64_t dim) {
+                                                       val_t<VC>* __restrict__ out, int64_t dim,
+                                                       int shifted = 0) {
   double t = 0.0;
   for (int b = threadIdx.x; b < G; b += kBlock) t += npart[b];
   t = block_sum(t);
   const double nrm = sqrt(t);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     beta[j] = nrm;
-    if (alpha) alpha[j] = coef[j].x;
+    // shifted step (EpiTrlLoc): alpha_j = alpha_{j-1} + <v_j, w>
+    if (alpha) alpha[j] = shifted ? alpha[j - 1] + coef[j].x : coef[j].x;
   }
   const double inv = nrm > 0.0 ? 1.0 / nrm : 0.0;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < dim; i += (int64_t)gridDim.x * kBlock)
@@ -351,6 +354,130 @@ __global__ void __launch_bounds__(kBlock) k_cgs(const val_t<VC>* __restrict__ V,
 #pragma unroll
     for (int w = 0; w < NW; w++) r = r + red[w][NR - 1];
     npart[blockIdx.x] = r;
+  }
+}
+
+// ------------------------------------------------------------------------
+// Whole orthogonalisation of one Krylov step in ONE workgroup (sectors up to
+// kOrthSoloMaxDim rows).  The multi-kernel form is three k_cgs launches and a
+// k_coef_scale (each a few microseconds of launch and latency on a sector
+// of a few hundred rows: ~30 of the ~36 us a small-sector step took).  Here
+// the block does CGS pass 1 (dots, |x|^2), pass 2 (x -= V h1, dots, |x'|^2),
+// the DGKS test, the conditional pass 3 (x -= V h2, |x''|^2), alpha/beta and
+// V_{j+1} = x / beta with block reductions between the passes: a Krylov step
+// is the H·v and this launch.  Same coefficients, same test, same semantics
+// as Trlan::orth's fused sweeps (coef = h1, + h2 when the second pass runs;
+// beta[jslot] = |x|; alpha[jn] when jn >= 0, shifted by alpha[jn-1] after an
+// EpiTrlLoc product).
+constexpr int kOrthSoloBlock = 512;
+constexpr int64_t kOrthSoloMaxDim = 4096;
+
+template <bool VC, int NC>
+__global__ void __launch_bounds__(kOrthSoloBlock) k_orth_solo(const val_t<VC>* __restrict__ V, int ncol,
+                                                              val_t<VC>* __restrict__ x, int64_t dim,
+                                                              double2* __restrict__ coef, double* __restrict__ alpha,
+                                                              double* __restrict__ beta, int jn, int jslot,
+                                                              val_t<VC>* __restrict__ out, int shifted) {
+  using Vt = val_t<VC>;
+  constexpr int NT = kOrthSoloBlock, NW = NT / 64;
+  constexpr int NR = (VC ? 2 * NC : NC) + 1;  // partial slots: re[NC] | im[NC] | norm
+  __shared__ double red[NW][NR];
+  __shared__ double tot[NR];
+  __shared__ double2 h1[NC], h2[NC];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  double are[NC], aim[VC ? NC : 1];
+  // block sums (fixed order): are/aim (first nc columns) and n2 -> tot
+  auto reduce = [&](int nc, double n2) {
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+      if (c >= nc) continue;  // uniform
+      const double r = wave_sum_dpp(are[c]);
+      if (lane == 63) red[wv][c] = r;
+      if constexpr (VC) {
+        const double q = wave_sum_dpp(aim[c]);
+        if (lane == 63) red[wv][NC + c] = q;
+      }
+    }
+    const double r = wave_sum_dpp(n2);
+    if (lane == 63) red[wv][NR - 1] = r;
+    __syncthreads();
+    if (t < NR) {
+      double a = 0.0;
+#pragma unroll
+      for (int w = 0; w < NW; w++) a = a + red[w][t];
+      tot[t] = a;
+    }
+    __syncthreads();
+  };
+  auto zero = [&]() {
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+      are[c] = 0.0;
+      if constexpr (VC) aim[c] = 0.0;
+    }
+  };
+  // x -= V h (h in LDS); optional dots of the result; returns |x|^2 partial
+  auto pass = [&](const double2* h, bool dots) {
+    double n2 = 0.0;
+    for (int64_t i = t; i < dim; i += NT) {
+      Vt v[NC];
+#pragma unroll
+      for (int c = 0; c < NC; c++) v[c] = c < ncol ? V[(int64_t)c * dim + i] : vzero<Vt>();
+      Vt xi = x[i];
+      if (h) {
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+          if (c >= ncol) continue;  // uniform
+          if constexpr (VC) {
+            xi.x -= v[c].x * h[c].x - v[c].y * h[c].y;
+            xi.y -= v[c].x * h[c].y + v[c].y * h[c].x;
+          } else {
+            xi -= v[c] * h[c].x;
+          }
+        }
+        x[i] = xi;
+      }
+      if (dots) {
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+          const double2 d = cdotc(v[c], xi);
+          are[c] += d.x;
+          if constexpr (VC) aim[c] += d.y;
+        }
+      }
+      n2 += redot(xi, xi);
+    }
+    return n2;
+  };
+  // pass 1: h1 = V^H x, |x|^2
+  zero();
+  reduce(ncol, pass(nullptr, true));
+  const double nA = tot[NR - 1];
+  if (t < ncol) h1[t] = make_double2(tot[t], VC ? tot[NC + t] : 0.0);
+  __syncthreads();
+  // pass 2: x -= V h1; h2 = V^H x, |x'|^2
+  zero();
+  reduce(ncol, pass(h1, true));
+  const double nB = tot[NR - 1];
+  if (t < ncol) h2[t] = make_double2(tot[t], VC ? tot[NC + t] : 0.0);
+  __syncthreads();
+  double nF = nB;
+  const bool second = !(nB > kDgks2 * nA);  // ARPACK's DGKS test (block-uniform)
+  if (second) {
+    zero();
+    reduce(0, pass(h2, false));
+    nF = tot[NR - 1];
+  }
+  if (t < ncol) {
+    const double2 c = second ? make_double2(h1[t].x + h2[t].x, h1[t].y + h2[t].y) : h1[t];
+    coef[t] = c;
+    if (t == jn && alpha) alpha[jn] = shifted ? alpha[jn - 1] + c.x : c.x;
+  }
+  const double b = sqrt(nF);
+  if (t == 0) beta[jslot] = b;
+  if (out) {
+    const double inv = b > 0.0 ? 1.0 / b : 0.0;
+    for (int64_t i = t; i < dim; i += NT) out[i] = scl(inv, x[i]);
   }
 }
 

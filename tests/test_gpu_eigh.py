@@ -107,3 +107,17 @@ def test_eigh_persistent_sweep_solo_small():
     assert 2 * NCV < H.shape[0] <= 2048
     with Sector(cfg, 3, 3, stored=True, real=True, options=("trlan_psweep",)) as S:
         _check(S, H, True)
+
+
+@pytest.mark.parametrize("opts", [("trlan_nolocal",), ("trlan_nosolo",), ("trlan_nolocal", "trlan_nosolo")],
+                         ids=["nolocal", "nosolo", "plain"])
+@pytest.mark.parametrize("real", [True, False], ids=["real", "complex"])
+def test_eigh_step_variants(opts, real):
+    """The thick-restart step's alternatives against dense diagonalisation:
+    without the shifted three-term H·v epilogue (ED_OPT_TRLAN_NOLOCAL), with
+    the multi-kernel CGS on a small sector instead of the one-workgroup
+    orthogonalisation (ED_OPT_TRLAN_NOSOLO), and both (the round-2 step)."""
+    cfg = CASES[0][1]()
+    H = _oracle_H(cfg, (3, 3))   # dim 3,136: inside the one-workgroup range
+    with Sector(cfg, 3, 3, stored=True, real=True, options=opts) as S:
+        _check(S, H, True, vt_real=real)

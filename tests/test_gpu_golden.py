@@ -26,8 +26,9 @@ def _load(name):
         return json.load(fh)
 
 
-@pytest.mark.parametrize("bath,kopts", [("flat", ()), ("random", ()), ("random", ("trlan_unfused",))],
-                         ids=["flat", "random", "random-unfused"])
+@pytest.mark.parametrize("bath,kopts", [("flat", ()), ("random", ()), ("random", ("trlan_unfused",)),
+                                        ("random", ("trlan_nolocal", "trlan_nosolo"))],
+                         ids=["flat", "random", "random-unfused", "random-plain-step"])
 def test_c4_all_sectors_match_fixture(bath, kopts):
     """All 169 configs[3] sectors through the farm against the dense fixture
     (1e-10 of |E0|); also with the always-two-pass CGS2 (ED_OPT_TRLAN_UNFUSED,
