@@ -1494,7 +1494,9 @@ static int64_t persist_vrows(const ed_sector* s, int mode, int vc = 0) {
   switch (mode) {
     case 2: return (int64_t)kPRegBlock * s->preg_rpt;
     case 3: return (int64_t)kPRegBlock * s->kreg_rpt;
-    case 4: return vc ? (int64_t)kPBlock * s->pkr_rpt_c : (int64_t)kPRegBlock * s->pkr_rpt;
+    case 4:
+      return (vc && (s->opts & ED_OPT_PKRON_C1024)) ? (int64_t)kPBlock * s->pkr_rpt_c
+                                                    : (int64_t)kPRegBlock * s->pkr_rpt;
     default: return (int64_t)kPBlock * persist_rpt01(s->dim);
   }
 }
@@ -1513,7 +1515,8 @@ static int persist_mode(ed_sector* s, int vc, int path) {
   if (!(o & (ED_OPT_NO_PKRON | ED_OPT_NO_PREG)) &&
       ((path == 0 && !(o & ED_OPT_PERSIST_STORED) && build_pkron_stored(s) > 0) ||
        (path == 2 && build_pkron_direct(s) > 0)) &&
-      (vc == 0 || s->pkr_rpt_c > 0) && persist_lds(s, vc, 4) <= kLdsBudget)
+      (vc == 0 || ((s->opts & ED_OPT_PKRON_C1024) ? s->pkr_rpt_c > 0 : pkr_fits_c512(s->pkr_E, s->pkr_rpt))) &&
+      persist_lds(s, vc, 4) <= kLdsBudget)
     return 4;
   // stored: MODE 2 (ELL entries in registers; c2 4.6 us/step) by default.
   // MODE 0 streams the matrix from L2 through one CU (~40-50 GB/s) and is
@@ -1595,6 +1598,7 @@ static PersistGeom persist_geom(const ed_sector* s) {
   g.pkr_E = s->pkr_E;
   g.pkr_rpt = s->pkr_rpt;
   g.pkr_rpt_c = s->pkr_rpt_c;
+  g.pkr_c1024 = (s->opts & ED_OPT_PKRON_C1024) ? 1 : 0;
   return g;
 }
 
@@ -2608,7 +2612,7 @@ int ed_sector_destroy(ed_sector* s) {
 
 int ed_sector_set_options(ed_sector* s, int32_t opts) {
   if (!s) return fail(ED_ERR_ARG, "null");
-  if (opts & ~0x3fff) return fail(ED_ERR_ARG, "unknown ED_OPT_* bits");
+  if (opts & ~0xffff) return fail(ED_ERR_ARG, "unknown ED_OPT_* bits");
   if (opts != s->opts) drop_graph(s);  // a captured recurrence bakes in the kernel choice
   s->opts = opts;
   return ED_OK;

@@ -271,12 +271,17 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
   // one iw broadcast) instead of registers, whose budget the complex w and
   // p take.
   constexpr bool KR = MODE == 4;
-  constexpr bool KRV = KR && VC;
+  // complex vectors: KRV = the 1024-thread layout (values and diagonal read
+  // from LDS); KRC = the 512-thread layout (up-hop values and diagonal in
+  // registers as for real vectors, down-hop values broadcast from LDS,
+  // p = v_{k-1} in global memory)
+  constexpr bool KRV = KR && VC && NT == kPBlock;
+  constexpr bool KRC = KR && VC && NT != kPBlock;
   int ucol[KR ? E : 1];
-  double uval[(KR && !VC) ? E : 1];
+  double uval[(KR && !KRV) ? E : 1];
   int dcol[KR ? RPT * E : 1];
   double dval[(KR && !VC) ? RPT * E : 1];
-  double dgr[(KR && !VC) ? RPT : 1];
+  double dgr[(KR && !KRV) ? RPT : 1];
   const double* sdv = nullptr;   // KRV: down-hop values [e * dd + iw]
   const double* suv = nullptr;   // KRV: up-hop values [e * du + iu] (reordered lists)
   const double* sdg = nullptr;   // KRV: diagonal [VROWS] (padding rows 0)
@@ -286,8 +291,9 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
     const bool act = tid < G * du;
     const int g = act ? tid / du : 0;
     giw = g;
-    if constexpr (KRV) {
-      // LDS: vector | diagonal | down-hop values
+    if constexpr (KR && VC) {
+      // LDS: vector | diagonal | down-hop values | up-hop values (KRC reads
+      // only the down-hop values)
       double* tg = (double*)(smem + (((int64_t)VROWS * sizeof(V) + 15) & ~(int64_t)15));
       for (int x = tid; x < VROWS; x += NT) {
         double d = 0.0;
@@ -323,7 +329,7 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
 #pragma unroll
       for (int e = 0; e < E; e++) {
         const bool ok = okr && e < a.kdegd;
-        if constexpr (KRV) {
+        if constexpr (KR && VC) {
           // padding slots gather the row's own (zero) padding entry, valid
           // rows beyond their degree a zero table value
           dcol[r * E + e] = (ok ? a.kdwc[e * dd + iw] * du + q.iu : (okr ? 0 : PROW(r))) * (int)sizeof(V);
@@ -352,7 +358,7 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
   // rows only, read once and written once per step, L2-resident): it frees
   // 4 VGPRs per row for the ELL words.  P is allocated with >= NT*RPT rows
   // (p_rows, ed_lib.hip) so padding slots load and store without a guard.
-  constexpr bool PG = REG && VC;
+  constexpr bool PG = (REG || KRC) && VC;
   // real vectors keep their own rows of r_k in registers; complex ones
   // re-read them from LDS (register budget of the ELL words)
   // (MODE 4 at 10 rows per thread reads them from LDS with the gathers: the
@@ -519,7 +525,7 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
 #pragma unroll
           for (int e = 0; e < E; e++) acc = fmac(acc, uval[e], *(const V*)(rb + ucol[e]));
         }
-        if constexpr (KRV) {
+        if constexpr (KR && VC) {
           const int iwc = min(giw + (NT / a.kdu) * r, a.kdd - 1);
 #pragma unroll
           for (int e = 0; e < E; e++)

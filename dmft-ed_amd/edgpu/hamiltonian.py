@@ -87,7 +87,7 @@ class Sector:
         """Select kernel alternatives by name (ED_OPT_*: no_persist,
         persist_stored, no_preg, no_pkron, fused_step, split_simple, no_batch,
         eigh_no_verify, trlan_unfused, trlan_nofold, trlan_psweep, no_graph,
-        trlan_nolocal, trlan_nosolo); no names
+        trlan_nolocal, trlan_nosolo, pkron_c1024); no names
         restores the defaults."""
         bits = 0
         for n in names:

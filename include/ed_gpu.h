@@ -82,7 +82,8 @@ extern "C" {
 #define ED_OPT_TRLAN_PSWEEP   0x400 /* eigh: one persistent launch per expansion sweep (opt-in) */
 #define ED_OPT_NO_GRAPH       0x800 /* eigh: Krylov sweeps launched directly, not as hipGraphs  */
 #define ED_OPT_TRLAN_NOLOCAL  0x1000 /* eigh: plain w = H v_j (no shifted three-term step)     */
-#define ED_OPT_TRLAN_NOSOLO   0x2000 /* eigh: multi-kernel CGS also on sectors <= 4096 rows     */
+#define ED_OPT_TRLAN_NOSOLO   0x2000 /* eigh: multi-kernel CGS also on sectors <= 2048 rows     */
+#define ED_OPT_PKRON_C1024    0x8000 /* Lanczos MODE 4, complex vectors: 1024-thread LDS layout  */
 
 /* status codes */
 #define ED_OK              0

@@ -117,7 +117,10 @@ def test_eigh_step_variants(opts, real):
     without the shifted three-term H·v epilogue (ED_OPT_TRLAN_NOLOCAL), with
     the multi-kernel CGS on a small sector instead of the one-workgroup
     orthogonalisation (ED_OPT_TRLAN_NOSOLO), and both (the round-2 step)."""
-    cfg = CASES[0][1]()
-    H = _oracle_H(cfg, (3, 3))   # dim 3,136: inside the one-workgroup range
-    with Sector(cfg, 3, 3, stored=True, real=True, options=opts) as S:
+    from edgpu.params import make_config
+
+    cfg = make_config(Norb=1, Nbath=6, bath="random", seed=5)
+    H = _oracle_H(cfg, (3, 4))   # dim 35 x 35 = 1,225: inside the one-workgroup range (<= 2,048)
+    assert 2 * NCV < H.shape[0] <= 2048
+    with Sector(cfg, 3, 4, stored=True, real=True, options=opts) as S:
         _check(S, H, True, vt_real=real)

@@ -52,6 +52,7 @@ def test_two_pass_bit_identical(name, factory, sectors):
     (dict(Norb=1, Nbath=7), (4, 4)),                                     # configs[1] sector
     (dict(Norb=2, Nbath=5, bath="random", seed=20251015), (6, 6)),       # configs[3] largest
     (dict(Norb=2, Nbath=4, bath="random", seed=4), (3, 6)),              # du != dd
+    (dict(Norb=1, Nbath=6, bath="random", seed=6), (3, 4)),              # odd DimUp (35)
 ])
 def test_two_pass_real_vectors_and_lanczos(cfg_kw, q):
     from edgpu.params import make_config
@@ -74,3 +75,4 @@ def test_two_pass_real_vectors_and_lanczos(cfg_kw, q):
         assert n1 == n2 == 24
         np.testing.assert_allclose(a1, a2, rtol=1e-12, atol=1e-12)
         np.testing.assert_allclose(b1, b2, rtol=1e-12, atol=1e-12)
+

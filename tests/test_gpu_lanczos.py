@@ -139,11 +139,13 @@ def test_c4_half_filled_ground_state_pin():
             assert abs(np.linalg.norm(vec) - 1.0) < 1e-10
 
 
+@pytest.mark.parametrize("layout", [(), ("pkron_c1024",)], ids=["c512", "c1024"])
 @pytest.mark.parametrize("direct", [False, True], ids=["stored", "direct"])
-def test_complex_vectors_kronecker_register_layout(direct):
+def test_complex_vectors_kronecker_register_layout(direct, layout):
     """The reference's arithmetic — complex(8) vectors — on a real H through
-    the Kronecker register layout (persistent MODE 4, 1024-thread complex
-    form): alpha/beta (first 15 steps) and E0 against the oracle's complex
+    the Kronecker register layout (persistent MODE 4; the 512-thread register
+    form, default, and the 1024-thread LDS form, ED_OPT_PKRON_C1024):
+    alpha/beta (first 15 steps) and E0 against the oracle's complex
     recurrence at 1e-10, and 40 steps against the multi-kernel one at 1e-9."""
     from edgpu.hamiltonian import Sector
     from cases import c2
@@ -155,7 +157,7 @@ def test_complex_vectors_kronecker_register_layout(direct):
     v0 = start_vector(len(hmap))
     ar, br, nr = lanc_tridiag(csr, v0, 60)
     kw = dict(stored=False, direct=True) if direct else dict(stored=True)
-    with Sector(cfg, 4, 4, real=True, **kw) as S:
+    with Sector(cfg, 4, 4, real=True, options=layout, **kw) as S:
         assert S.lanc_mode(real=False) == 4
         a, b, n = S.lanc_tridiag(v0, 60, real=False)
         assert n == nr == 60
@@ -171,14 +173,15 @@ def test_complex_vectors_kronecker_register_layout(direct):
     np.testing.assert_allclose(b[:40], b2[:40], rtol=1e-9, atol=1e-11)
 
 
-def test_complex_vectors_batched_mode4():
-    """Batched complex runs (one 1024-thread workgroup per start vector) give
-    each run's single-launch alpha/beta."""
+@pytest.mark.parametrize("layout", [(), ("pkron_c1024",)], ids=["c512", "c1024"])
+def test_complex_vectors_batched_mode4(layout):
+    """Batched complex runs (one workgroup per start vector, both MODE 4
+    complex layouts) give each run's single-launch alpha/beta."""
     from edgpu.gf import _tridiag_batch
     from edgpu.hamiltonian import Sector
     from cases import c2
 
-    with Sector(c2(), 4, 4, real=True, stored=True) as S:
+    with Sector(c2(), 4, 4, real=True, stored=True, options=layout) as S:
         assert S.lanc_mode(real=False) == 4
         i = torch.arange(1, S.dim + 1, dtype=torch.float64, device="cuda:0")
         seeds = torch.stack([torch.complex(torch.sin(k * i), torch.cos(3 * k * i)) for k in (1, 2, 3)])

@@ -31,6 +31,7 @@ ap.add_argument("--path", type=int, default=0)
 ap.add_argument("--complex", action="store_true", help="complex(8) H values (and vectors)")
 ap.add_argument("--cvec", action="store_true", help="real H, complex vectors")
 ap.add_argument("--iters", type=int, default=20)
+ap.add_argument("--options", default="", help="comma-separated ED_OPT_* names")
 a = ap.parse_args()
 if a.sector == "c4r":   # bench.py's configs[3] parameters (Uloc=(2,2,0), Ust=1, Jh=0.5), (6,6)
     from golden.golden_configs import c4_config
@@ -39,7 +40,8 @@ else:
     kw, q = SECTORS[a.sector]
     cfg = make_config(bath="random", seed=20251015, **kw)
 real = not a.complex
-with Sector(cfg, q[0], q[1], stored=(a.path == 0), direct=(a.path != 0), real=real) as S:
+opts = tuple(o for o in a.options.split(",") if o)
+with Sector(cfg, q[0], q[1], stored=(a.path == 0), direct=(a.path != 0), real=real, options=opts) as S:
     dt = torch.float64 if (real and not a.cvec) else torch.complex128
     i = torch.arange(1, S.dim + 1, dtype=torch.float64, device="cuda")
     x = torch.sin(i) if dt == torch.float64 else torch.complex(torch.sin(i), torch.cos(3 * i))
