@@ -291,7 +291,7 @@ def bench_batched(S, v0, niter, last_alpha, ks=(256, 1024), cplx=False):
                        "alpha_seed0_rel_dev": dev}
     out["note"] = ("K start vectors on the configs[1] sector, one workgroup each, one launch "
                    "(the headline value is ONE recurrence on one CU)" +
-                   ("; complex(8) vectors on the real(8) stored H (MODE 4, 1024 threads per run)" if cplx else ""))
+                   ("; complex(8) vectors on the real(8) stored H (MODE 4, 512-thread register layout per run)" if cplx else ""))
     return out
 
 
