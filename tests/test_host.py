@@ -83,6 +83,25 @@ def test_library_exports_every_header_symbol():
         assert hasattr(lib, d)
 
 
+def test_option_names_match_header_bits():
+    """Every ED_OPT_* bit of include/ed_gpu.h has its Python name in
+    edgpu._lib.OPTIONS (Sector(options=...) / DiagOptions.kernel_options) with
+    the same value, and the library accepts exactly those bits."""
+    from edgpu._lib import OPTIONS
+
+    bits = {m.group(1).lower(): int(m.group(2), 16)
+            for m in re.finditer(r"#define\s+ED_OPT_(\w+)\s+(0x[0-9a-fA-F]+)", open(HEADER).read())}
+    assert bits == OPTIONS
+    assert len(set(bits.values())) == len(bits)
+    mask = 0
+    for v in bits.values():
+        assert v & (v - 1) == 0  # one bit each
+        mask |= v
+    src = open(os.path.join(ROOT, "dmft-ed_amd", "csrc", "ed_lib.hip")).read()
+    m = re.search(r"if \(opts & ~(0x[0-9a-fA-F]+)\) return fail\(ED_ERR_ARG", src)
+    assert m and int(m.group(1), 16) >= mask and (int(m.group(1), 16) + 1) & int(m.group(1), 16) == 0
+
+
 def test_fortran_shim_compiles_and_binds():
     """The Fortran module builds and references every bound C symbol it declares."""
     d = os.path.join(ROOT, "dmft-ed_amd", "fortran")
