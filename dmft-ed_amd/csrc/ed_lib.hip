@@ -2100,6 +2100,33 @@ struct Trlan {
   int step(int j, int j0) {
     nhv++;
     const bool loc = local && j > j0;
+    // small packed stored sectors, real vectors: the whole step in one workgroup
+    if constexpr (!VC) {
+      if (solo && fused && path == 0 && s->d_words && !s->hc && s->row0 == 0 && s->nrows == dim &&
+          dim <= kOrthSoloMaxDim && j + 1 <= 32) {
+        StepSoloArgs a;
+        a.diag = (const double*)s->d_diag;
+        a.sptr = s->d_sptr;
+        a.words = s->d_words;
+        a.dict = (const double*)s->d_pdict;
+        a.Vb = (const double*)Vb;
+        a.x = (double*)w;
+        a.out = j + 1 < m ? (double*)col(Vb, j + 1) : nullptr;
+        a.coef = coef;
+        a.alpha = alpha;
+        a.beta = beta;
+        a.dim = dim;
+        a.j = j;
+        a.shifted = loc ? 1 : 0;
+        const int nc = (j + 1 + 7) / 8 * 8;
+        if (nc <= 8) hipLaunchKernelGGL(k_step_solo<8>, dim3(1), dim3(kOrthSoloBlock), 0, st, a);
+        else if (nc <= 16) hipLaunchKernelGGL(k_step_solo<16>, dim3(1), dim3(kOrthSoloBlock), 0, st, a);
+        else if (nc <= 24) hipLaunchKernelGGL(k_step_solo<24>, dim3(1), dim3(kOrthSoloBlock), 0, st, a);
+        else hipLaunchKernelGGL(k_step_solo<32>, dim3(1), dim3(kOrthSoloBlock), 0, st, a);
+        HIPCK(hipGetLastError());
+        return ED_OK;
+      }
+    }
     if (loc) {
       EpiTrlLoc<VC> e{w, col(Vb, j - 1), alpha + (j - 1), beta + (j - 1)};
       CK(launch_hxv<VC>(s, path, col(Vb, j), e, st));

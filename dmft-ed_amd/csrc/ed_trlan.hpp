@@ -373,11 +373,11 @@ constexpr int kOrthSoloBlock = 512;
 constexpr int64_t kOrthSoloMaxDim = 2048;  // measured: dim 2,640 35 us per step solo, 31 multi-kernel
 
 template <bool VC, int NC>
-__global__ void __launch_bounds__(kOrthSoloBlock) k_orth_solo(const val_t<VC>* __restrict__ V, int ncol,
-                                                              val_t<VC>* __restrict__ x, int64_t dim,
-                                                              double2* __restrict__ coef, double* __restrict__ alpha,
-                                                              double* __restrict__ beta, int jn, int jslot,
-                                                              val_t<VC>* __restrict__ out, int shifted) {
+__device__ __forceinline__ void orth_solo_body(const val_t<VC>* __restrict__ V, int ncol,
+                                               val_t<VC>* __restrict__ x, int64_t dim,
+                                               double2* __restrict__ coef, double* __restrict__ alpha,
+                                               double* __restrict__ beta, int jn, int jslot,
+                                               val_t<VC>* __restrict__ out, int shifted) {
   using Vt = val_t<VC>;
   constexpr int NT = kOrthSoloBlock, NW = NT / 64;
   constexpr int NR = (VC ? 2 * NC : NC) + 1;  // partial slots: re[NC] | im[NC] | norm
@@ -479,6 +479,73 @@ __global__ void __launch_bounds__(kOrthSoloBlock) k_orth_solo(const val_t<VC>* _
     const double inv = b > 0.0 ? 1.0 / b : 0.0;
     for (int64_t i = t; i < dim; i += NT) out[i] = scl(inv, x[i]);
   }
+}
+
+template <bool VC, int NC>
+__global__ void __launch_bounds__(kOrthSoloBlock) k_orth_solo(const val_t<VC>* __restrict__ V, int ncol,
+                                                              val_t<VC>* __restrict__ x, int64_t dim,
+                                                              double2* __restrict__ coef, double* __restrict__ alpha,
+                                                              double* __restrict__ beta, int jn, int jslot,
+                                                              val_t<VC>* __restrict__ out, int shifted) {
+  orth_solo_body<VC, NC>(V, ncol, x, dim, coef, alpha, beta, jn, jslot, out, shifted);
+}
+
+// A whole Krylov step of a small stored sector in ONE workgroup (real
+// vectors, packed SELL words): v_j staged in LDS, H v_j gathered from LDS
+// with the shifted three-term epilogue (EpiTrlLoc's arithmetic when
+// shifted), then orth_solo_body.  The sweep is one launch per step instead
+// of two (the H·v grid and k_orth_solo).  Same per-row sums as k_spmv_pk.
+struct StepSoloArgs {
+  const double* diag;
+  const int64_t* sptr;
+  const uint32_t* words;
+  const double* dict;  // 256 entries
+  const double* Vb;    // basis, column c at Vb + c*dim
+  double* x;           // w (the step's residual)
+  double* out;         // V_{j+1} = w / beta_j, or null (last column of the sweep)
+  double2* coef;
+  double* alpha;
+  double* beta;
+  int64_t dim;
+  int j, shifted;      // column j; shifted: w = (H - alpha_{j-1}) v_j - beta_{j-1} v_{j-1}
+};
+
+template <int NC>
+__global__ void __launch_bounds__(kOrthSoloBlock) k_step_solo(const StepSoloArgs a) {
+  constexpr int NT = kOrthSoloBlock;
+  __shared__ double vl[kOrthSoloMaxDim];
+  __shared__ double sdict[256];
+  const int t = threadIdx.x;
+  const int64_t dim = a.dim;
+  const int j = a.j;
+  const double* vj = a.Vb + (int64_t)j * dim;
+  for (int64_t i = t; i < dim; i += NT) vl[i] = vj[i];
+  if (t < 256) sdict[t] = a.dict[t];
+  double sg = 0.0, bp = 0.0;
+  if (a.shifted) {
+    sg = a.alpha[j - 1];
+    bp = a.beta[j - 1];
+  }
+  __syncthreads();
+  const double* vprev = a.shifted ? a.Vb + (int64_t)(j - 1) * dim : nullptr;
+  for (int64_t i = t; i < dim; i += NT) {
+    const int64_t sl = i >> 6, s0 = a.sptr[sl];
+    const int w = (int)((a.sptr[sl + 1] - s0) >> 6);
+    const uint32_t* wp = a.words + s0 + (i & 63);
+    const double xi = vl[i];
+    double acc = 0.0 + a.diag[i] * xi;
+    for (int k0 = 0; k0 < w; k0 += kChunk) {
+      uint32_t c[kChunk];
+#pragma unroll
+      for (int k = 0; k < kChunk; k++) c[k] = (k0 + k < w) ? wp[64 * (k0 + k)] : (uint32_t)i;
+#pragma unroll
+      for (int k = 0; k < kChunk; k++)
+        if (k0 + k < w) acc = acc + sdict[c[k] >> kPackShift] * vl[c[k] & kPackColMask];
+    }
+    a.x[i] = a.shifted ? (acc - sg * xi) - bp * vprev[i] : acc;
+  }
+  // (each thread's orthogonalisation passes read back only its own rows of x)
+  orth_solo_body<false, NC>(a.Vb, j + 1, a.x, dim, a.coef, a.alpha, a.beta, j, j, a.out, a.shifted);
 }
 
 // ------------------------------------------------------------------------
