@@ -16,8 +16,9 @@ device matrix, sit in registers — DESIGN.md §1).  Beside it:
   * direct_iters_per_s: configs[2], matrix-free tables (MODE 4 from the hop
     tables);
   * complex_iters_per_s: complex(8) vectors (the reference's arithmetic) on the
-    real(8) stored values of the same H (persistent MODE 4, 1024-thread complex
-    form); complex_h_iters_per_s: complex(8) H values and vectors (MODE 2);
+    real(8) stored values of the same H (persistent MODE 4, 512-thread complex
+    register layout by default); complex_h_iters_per_s: complex(8) H values and
+    vectors (MODE 2);
   * validation: the lowest Ritz value of the last timed run's tridiagonal
     against the committed oracle E0 (tests/golden/c2_e0.json) at 1e-10.
 Sections (rank 0 prints, all ranks take part):
@@ -242,10 +243,16 @@ def bench_split(dist, world, dev, iters=10):
         ds.hxv(x)
     dt, _ = _timed(dist, lambda: [ds.hxv(x) for _ in range(iters)])
     ds.close()
-    return {"ms_per_hxv": round(dt / iters * 1e3, 4), "n_gpus": world, "scaling": "strong",
+    if dist:
+        import torch.distributed as tdist
+        backend = tdist.get_backend()
+        how = "RCCL" if backend == "nccl" else backend
+    else:
+        how = "one rank: no exchange"
+    return {"ms_per_hxv": round(dt / iters * 1e3, 4), "n_gpus": world, "scaling": "strong", "backend": how,
             "dim": ds.du * ds.dd, "local_rows": nw,
             "workload": "Nlevels=28 Norb=1 Nbath=13 (7,7) sector split by down rows; Kronecker rows/cols "
-                        "kernels + 2 all_to_all exchanges per H·v (RCCL; strip layout, no transposes)"}
+                        f"kernels + 2 all_to_all exchanges per H·v ({how}; strip layout, no transposes)"}
 
 
 def _lanc_rate(S, niter, v0, reps=5, options=()):
@@ -385,6 +392,65 @@ def roofline_sweep(Sector, make_config):
     return out
 
 
+def spawn_ranks(n, argv):
+    """`--gpus N` without an external launcher: start N ranks (one process per
+    GPU) with torch.distributed.run as a CHILD process and return its exit
+    code.  Called before anything touches the GPU (importing torch and
+    counting devices do not), and never by exec: the parent only waits."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC (the box's driver)
+    return subprocess.run(cmd, env=env).returncode
+
+
+def rank_env(args):
+    """(world, rank, local) of this process; checks that the launch matches
+    --gpus (a driver run of `--gpus 8` must measure 8 ranks, not one)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    if not (0 <= rank < world):
+        raise SystemExit(f"bench.py: RANK={rank} outside WORLD_SIZE={world}")
+    return world, rank, local
+
+
+def launch_check(args):
+    """`--launch-check`: the N-rank flow without a GPU (CPU test): every rank
+    joins a gloo group, the barrier-bracketed max-over-ranks timing runs on a
+    CPU stand-in step, rank 0 prints the line with n_gpus = world."""
+    import torch.distributed as tdist
+
+    world, rank, local = rank_env(args)
+    if world > 1:
+        tdist.init_process_group("gloo")
+    seen = torch.tensor([float(rank), float(local)], dtype=torch.float64)
+    allv = [torch.zeros(2, dtype=torch.float64) for _ in range(world)]
+    if world > 1:
+        tdist.all_gather(allv, seen)
+    else:
+        allv = [seen]
+    t0 = time.perf_counter()
+    if world > 1:
+        tdist.barrier()
+    dt = torch.tensor([time.perf_counter() - t0 + 1e-3 * (rank + 1)], dtype=torch.float64)
+    if world > 1:
+        tdist.all_reduce(dt, op=tdist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "ranks": [int(v[0]) for v in allv],
+                          "local_ranks": [int(v[1]) for v in allv], "max_dt": float(dt.item())}))
+    if world > 1:
+        tdist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -394,28 +460,36 @@ def main():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-farm", action="store_true", help="skip the configs[3]/[4] sections")
+    ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    if args.launch_check:
+        return launch_check(args)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = rank_env(args)
     dist = world > 1
+    # rehearsal switches (not used by the driver): ED_BENCH_BACKEND=gloo and
+    # ED_BENCH_ONE_DEVICE=1 run N ranks on one GPU to exercise the N>1 flow
+    one_device = bool(os.environ.get("ED_BENCH_ONE_DEVICE"))
+    backend = os.environ.get("ED_BENCH_BACKEND", "nccl") if dist else None
+    if one_device:
+        local = 0
+    ndev = torch.cuda.device_count()
+    if local >= ndev:
+        raise SystemExit(f"bench.py: rank {rank} wants GPU {local} but {ndev} are visible")
+    torch.cuda.set_device(local)
     if dist:
         import torch.distributed as tdist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        # rehearsal switches (not used by the driver): ED_BENCH_BACKEND=gloo and
-        # ED_BENCH_ONE_DEVICE=1 run N ranks on one GPU to exercise the N>1 flow
-        if os.environ.get("ED_BENCH_ONE_DEVICE"):
-            local = 0
-        torch.cuda.set_device(local)
-        backend = os.environ.get("ED_BENCH_BACKEND", "nccl")
         if backend == "nccl":
             tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             tdist.init_process_group(backend)
-    else:
-        torch.cuda.set_device(0)
+        assert tdist.get_world_size() == args.gpus
     dev = torch.cuda.current_device()
 
     from edgpu.hamiltonian import Sector

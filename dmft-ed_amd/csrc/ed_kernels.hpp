@@ -862,14 +862,18 @@ struct DirChunk {
   int32_t pad[2];
 };
 
-// element e of a vector through a raw buffer resource (byte offset e*sizeof)
+// element e of a vector through a raw buffer resource: the byte offset
+// e*sizeof is formed in 32-bit unsigned arithmetic and the resource spans
+// 4 GiB, so the host admits k_direct only for vectors of < 2^32 bytes
+// (kDirMaxVecBytes; launch_direct refuses larger ones)
+constexpr uint64_t kDirMaxVecBytes = 0xffffffffull;
 template <bool VC>
 __device__ __forceinline__ val_t<VC> ld_rsrc(__amdgpu_buffer_rsrc_t r, int e) {
   if constexpr (VC) {
-    const auto q = __builtin_amdgcn_raw_buffer_load_b128(r, e * 16, 0, 0);
+    const auto q = __builtin_amdgcn_raw_buffer_load_b128(r, (int)((uint32_t)e * 16u), 0, 0);
     return __builtin_bit_cast(double2, q);
   } else {
-    const auto q = __builtin_amdgcn_raw_buffer_load_b64(r, e * 8, 0, 0);
+    const auto q = __builtin_amdgcn_raw_buffer_load_b64(r, (int)((uint32_t)e * 8u), 0, 0);
     return __builtin_bit_cast(double, q);
   }
 }
@@ -940,7 +944,7 @@ __global__ void __launch_bounds__(kDirBlock) k_direct(const val_t<HC>* __restric
   }
   // gathers through a buffer resource: 32-bit element offsets (one VALU op
   // per gather instead of a 64-bit address)
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)0xffffffffu, 0x00020000);
   double part = 0.0;
   for (; c < cend; c += cstep) {
     const DirChunk ch = chunks[c];

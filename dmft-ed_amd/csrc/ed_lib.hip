@@ -620,9 +620,24 @@ static int build_direct(ed_sector* s) {
   return ED_OK;
 }
 
+// the k_direct tables on first use of path 1 (build_direct), ordered before
+// the caller's stream by a sync of the sector's stream
+static int ensure_direct(ed_sector* s, int path) {
+  if (path != 1 || s->d_dchunk || s->nrows == 0) return ED_OK;
+  if (!(s->flags & ED_DIRECT)) return fail(ED_ERR_ARG, "generic matrix-free path needs ED_DIRECT");
+  CK(build_direct(s));
+  HIPCK(hipStreamSynchronize(s->stream));
+  return ED_OK;
+}
+
 template <bool HC, bool VC, bool PL, class Epi>
 static int launch_direct(ed_sector* s, const void* x, Epi epi, hipStream_t st) {
   using V = val_t<VC>;
+  // the gathers address x through a 4 GiB buffer resource with 32-bit byte
+  // offsets (ld_rsrc): a longer vector would read zeros past the range
+  if ((uint64_t)s->dim * sizeof(V) > kDirMaxVecBytes)
+    return fail(ED_ERR_UNSUPPORTED, "k_direct: vector of " + std::to_string(s->dim) +
+                                        " elements exceeds the 4 GiB gather range (use the stored or Kronecker path)");
   auto fn = k_direct<HC, VC, PL, Epi>;
   // dynamic LDS beyond 64 KB: allow what the 160 KB leave next to the
   // function's static LDS (the epilogue's reduction slots)
@@ -2609,8 +2624,12 @@ static int sector_create(const ed_params* p, int32_t q1, int32_t q2, int32_t fla
   // Kronecker form: normal mode without Jx/Jp terms (no term moves both spins)
   s->kron = (flags & ED_DIRECT) && s->Mh.mode == ED_MODE_NORMAL && !s->Mh.jhflag && nrows == s->dim;
   if ((flags & ED_STORED) && nrows > 0) TRY(build_stored(s));
-  if ((flags & ED_DIRECT) && nrows > 0) TRY(build_direct(s));
   if (s->kron) TRY(build_kron(s));
+  // k_direct tables: built here only when the generic matrix-free kernel is
+  // the sector's default H·v; otherwise on the first explicit path-1 request
+  // (ensure_direct), so stored, Kronecker and GF source sectors keep their
+  // build cost and failure modes
+  if ((flags & ED_DIRECT) && nrows > 0 && resolve_path(s, -1) == 1) TRY(build_direct(s));
   if (hipStreamSynchronize(s->stream) != hipSuccess) {
     sector_free(s);
     return fail(ED_ERR_HIP, "sector build");
@@ -2637,9 +2656,15 @@ int ed_sector_destroy(ed_sector* s) {
   return ED_OK;
 }
 
+// every defined ED_OPT_* bit (include/ed_gpu.h); any other bit is refused
+static constexpr int32_t kOptKnown =
+    ED_OPT_NO_PERSIST | ED_OPT_PERSIST_STORED | ED_OPT_NO_PREG | ED_OPT_NO_PKRON | ED_OPT_FUSED_STEP |
+    ED_OPT_SPLIT_SIMPLE | ED_OPT_NO_BATCH | ED_OPT_EIGH_NO_VERIFY | ED_OPT_TRLAN_UNFUSED | ED_OPT_TRLAN_NOFOLD |
+    ED_OPT_TRLAN_PSWEEP | ED_OPT_NO_GRAPH | ED_OPT_TRLAN_NOLOCAL | ED_OPT_TRLAN_NOSOLO | ED_OPT_PKRON_C1024;
+
 int ed_sector_set_options(ed_sector* s, int32_t opts) {
   if (!s) return fail(ED_ERR_ARG, "null");
-  if (opts & ~0xffff) return fail(ED_ERR_ARG, "unknown ED_OPT_* bits");
+  if (opts & ~kOptKnown) return fail(ED_ERR_ARG, "unknown ED_OPT_* bits");
   if (opts != s->opts) drop_graph(s);  // a captured recurrence bakes in the kernel choice
   s->opts = opts;
   return ED_OK;
@@ -2674,6 +2699,7 @@ int ed_sector_hxv_dev_path(ed_sector* s, int32_t path, int32_t vtype, const void
   int pth = resolve_path(s, path);
   if (pth < 0) return fail(ED_ERR_ARG, "H·v path not available for this sector");
   HIPCK(hipSetDevice(s->device));
+  CK(ensure_direct(s, pth));
   hipStream_t st = (hipStream_t)stream;
   if (vtype == 1) {
     EpiStore<true> e{(double2*)hv};

@@ -98,8 +98,10 @@ def test_option_names_match_header_bits():
         assert v & (v - 1) == 0  # one bit each
         mask |= v
     src = open(os.path.join(ROOT, "dmft-ed_amd", "csrc", "ed_lib.hip")).read()
-    m = re.search(r"if \(opts & ~(0x[0-9a-fA-F]+)\) return fail\(ED_ERR_ARG", src)
-    assert m and int(m.group(1), 16) >= mask and (int(m.group(1), 16) + 1) & int(m.group(1), 16) == 0
+    assert re.search(r"if \(opts & ~kOptKnown\) return fail\(ED_ERR_ARG", src)
+    m = re.search(r"kOptKnown =([^;]+);", src)
+    names = re.findall(r"ED_OPT_(\w+)", m.group(1))
+    assert {n.lower() for n in names} == set(bits) and len(names) == len(bits)  # exactly the defined bits
 
 
 def test_fortran_shim_compiles_and_binds():

@@ -57,5 +57,14 @@ with Sector(cfg, q[0], q[1], stored=(a.path == 0), direct=(a.path != 0), real=re
     e1.record(st)
     e1.synchronize()
     ms = e0.elapsed_time(e1) / a.iters
+    # the same launches bracketed one by one (what a per-dispatch trace sees)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.iters)]
+    for b, e in ev:
+        b.record(st)
+        S.hxv_dev(x, y, path=a.path, stream=st)
+        e.record(st)
+    ev[-1][1].synchronize()
+    each = sorted(b.elapsed_time(e) for b, e in ev)
+    print(f"per-launch events: mean {sum(each) / len(each):.5f} min {each[0]:.5f} median {each[len(each) // 2]:.5f} ms")
     print(f"sector={a.sector} dim={S.dim} nnz={S.nnz} padded={S.info.padded} path={a.path} "
           f"real={real} cvec={a.cvec} packed={S.info.packed} ndict={S.info.npdict} ms/launch={ms:.5f}")
