@@ -904,7 +904,8 @@ __global__ void __launch_bounds__(kDirBlock) k_direct(const val_t<HC>* __restric
                                                       const uint16_t* __restrict__ rank_g,
                                                       const uint16_t* __restrict__ pat_g,
                                                       const uint32_t* __restrict__ map, int ns,
-                                                      const val_t<VC>* __restrict__ x, int64_t row0, Epi epi) {
+                                                      const val_t<VC>* __restrict__ x, int64_t xdim, int64_t row0,
+                                                      Epi epi) {
   using V = val_t<VC>;
   using H = val_t<HC>;
   if (epi.skip()) return;
@@ -943,8 +944,14 @@ __global__ void __launch_bounds__(kDirBlock) k_direct(const val_t<HC>* __restric
     cstep = gridDim.x * (kDirBlock / 64);
   }
   // gathers through a buffer resource: 32-bit element offsets (one VALU op
-  // per gather instead of a 64-bit address)
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)0xffffffffu, 0x00020000);
+  // per gather instead of a 64-bit address).  The resource spans exactly the
+  // sector vector, so a lane whose op does not fire gathers element xdim:
+  // out of range, the load returns 0 without touching the cache (the lanes
+  // of an op that fires on half of them used to fetch their own row: the L1
+  // tag lookups of those lines were ~40 % of the kernel's, nonSU2 N26)
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)x, (short)0, (int)(uint32_t)((uint64_t)xdim * sizeof(V)), 0x00020000);
+  const int oob = (int)xdim;
   double part = 0.0;
   for (; c < cend; c += cstep) {
     const DirChunk ch = chunks[c];
@@ -982,7 +989,7 @@ __global__ void __launch_bounds__(kDirBlock) k_direct(const val_t<HC>* __restric
           neg = (kind >> 1) & 1u;
         }
         vd[j] = f;
-        tg[j] = f ? G.delta[j] + rk[j] : row;
+        tg[j] = f ? G.delta[j] + rk[j] : oob;
         if constexpr (HC)
           hv[j] = make_double2(flip_sign(G.re[j], neg), (kind & kDirImSigned) ? flip_sign(G.im[j], neg) : G.im[j]);
         else

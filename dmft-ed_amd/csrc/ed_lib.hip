@@ -656,7 +656,7 @@ static int launch_direct(ed_sector* s, const void* x, Epi epi, hipStream_t st) {
   }
   hipLaunchKernelGGL(fn, dim3(s->dir_grid), dim3(kDirBlock), s->dir_lds, st, (const val_t<HC>*)s->d_ddiag,
                      s->d_dchunk, s->ndchunk,
-                     s->d_dops, s->d_rank16, s->d_pat16, s->d_map, s->T.ns, (const V*)x, s->row0, epi);
+                     s->d_dops, s->d_rank16, s->d_pat16, s->d_map, s->T.ns, (const V*)x, s->dim, s->row0, epi);
   return ED_OK;
 }
 
