@@ -807,52 +807,56 @@ __global__ void __launch_bounds__(kBlock) k_spmv_pk(const val_t<HC>* __restrict_
 //     block are the same for every lane, resolved on the host into a row
 //     offset and a signed value — one coalesced gather, no per-lane work;
 //   - LANE ops (terms touching up levels): condition, target pattern and
-//     Jordan-Wigner sign per lane by bit masks and popc, target row
-//     off[idw'] (block-uniform, from the op) + rank of the target up pattern
-//     (LDS table).
+//     Jordan-Wigner sign per lane from the lane's up pattern (bit masks and
+//     popc), target row off[idw'] (block-uniform, from the op) + rank of the
+//     target up pattern (LDS table); the part of the sign that depends on
+//     the block's down bits and the string's constant are folded into the
+//     op's value on the host.
 // The rank table (16-bit, 2^Ns entries) and the up patterns of every class
 // (16-bit, 2^Ns) are staged in LDS once per workgroup; ops are read with
-// scalar loads.  Ops go in groups of kDirGroup with every gather of a group
-// issued before the group's terms are summed, in order, into the row: the
-// same products and additions as k_spmv, so H·v is bit-identical to the
-// stored kernel.  The diagonal is gen_row's own (gen_diag), evaluated once
-// per sector by k_gen_diag into a vector (8 or 16 B per row): re-running
-// gen_diag's loops (~30 dependent f64 adds at Nlevels=28, half-rate f64
-// VALU) in every H·v was a quarter of the kernel's instructions.  Targets come
-// from one formula (DirOp; a down-level op has no up bits in flip, so its
-// rank read is the lane's own rank); an op's kind is scalar, and only
-// up-level ops evaluate a per-lane condition and sign (uniform branch).  The
-// group's LDS reads and gathers issue back to back.  The two
-// directions of a hop on up levels are one op (kDirXor, build_direct): ~half
-// the per-lane evaluations of a normal-mode row.
+// scalar loads.  Ops go in groups of kDirGroup whose UNI/LANE pattern is a
+// compile-time case (DirGroup::lanes selects one of 16 specialised bodies:
+// no per-op scalar branch, a UNI op costs one address add and the product);
+// every gather of a group is issued before the group is summed, in order,
+// into the row: the same products and additions as k_spmv (a lane whose op
+// does not fire gathers out of range, reads 0 and adds a zero product), so
+// H·v equals the stored kernel's.  The diagonal is gen_row's own (gen_diag),
+// evaluated once per sector by k_gen_diag into a vector (8 or 16 B per row).
+// The two directions of a hop on up levels are one op (kDirXor, build_direct):
+// ~half the per-lane evaluations of a normal-mode row.
+// Round-4 counters (nonSU2 N26, tools/r4_call1.sh): the kernel issued ~20
+// VALU and ~22 SALU instructions per op (per-op kind branches, per-lane
+// selects and sign assembly) and was issue-bound, not L1-bound.
 constexpr int kDirBlock = 1024;
 constexpr int kDirGroup = 4;
-// One op, evaluated the same way for every kind (no per-op branch):
+// Host form of one op (build_direct), before it is folded into a DirGroup:
 //   fires  = (m & req_mask) == req_val && popc(m & xm) == (kind has kDirXor)
-//   target = delta + rank[(m ^ flip) & up-mask]   (delta: first row of the
-//            target block; a down-level op has no up bits in flip, so this
-//            is the lane's own rank in the target block)
-//   sign   = (-1)^(popc(m & smask) + c0)          (down-level ops: smask 0,
-//            the block's sign resolved on the host into c0)
-// Pads: req_val = 1 with req_mask 0 (never fire).
+//   target = delta + rank[(m ^ flip) & up-mask]
+//   sign   = (-1)^(popc(m & smask) + c0)
 struct DirOp {
   uint32_t req_mask, req_val, flip, smask, xm;
   int32_t delta;
   int32_t kind;   // kDirLane | kDirC0 | kDirImSigned | kDirPad | kDirXor
   double re, im;  // before the sign
 };
-// kDirGroup ops field by field in 64-byte lines: one group is three
-// s_load_dwordx16 and one wait (op by op, the struct's fields came in
-// dependent scalar loads: ~70 round trips per chunk)
+// kDirXor: merged hop pair, fires when exactly one of the two flip bits is set
+constexpr int kDirLane = 1, kDirC0 = 2, kDirImSigned = 4, kDirPad = 8, kDirXor = 16;
+// kDirGroup ops field by field in 64-byte lines (three s_load_dwordx16).
+// Fields act on the lane's UP pattern u only (the block's down bits are
+// resolved on the host):
+//   LANE op j: fires = (u & cmask) == cval && popc(u & xm) == xv
+//              target = delta + rank[u ^ flipu], value = (re, im) * (-1)^popc(u & smasku)
+//              (the imaginary part signed only where bit j of imsig is set)
+//   UNI op j:  target = delta + rank[u] (the lane's own rank), value (re, im)
+//   pads:      UNI ops of value 0 on the row's own block
 struct __align__(64) DirGroup {
-  uint32_t req_mask[kDirGroup], req_val[kDirGroup], flip[kDirGroup], smask[kDirGroup];
-  int32_t delta[kDirGroup], kind[kDirGroup];
-  uint32_t xm[kDirGroup], pad_[4];
+  uint32_t cmask[kDirGroup], cval[kDirGroup], flipu[kDirGroup], smasku[kDirGroup];
+  int32_t delta[kDirGroup];
+  uint32_t xm[kDirGroup], xv[kDirGroup];
+  uint32_t lanes, imsig, pad_[2];  // lanes: bit j = op j is a LANE op
   double re[kDirGroup], im[kDirGroup];
 };
 static_assert(sizeof(DirGroup) == 192, "DirGroup: three 64-byte scalar loads");
-// kDirXor: merged hop pair, fires when exactly one of the two flip bits is set
-constexpr int kDirLane = 1, kDirC0 = 2, kDirImSigned = 4, kDirPad = 8, kDirXor = 16;
 struct DirChunk {
   int32_t row;    // row of lane 0
   uint32_t idw;   // down pattern of the block
@@ -862,18 +866,18 @@ struct DirChunk {
   int32_t pad[2];
 };
 
-// element e of a vector through a raw buffer resource: the byte offset
-// e*sizeof is formed in 32-bit unsigned arithmetic and the resource spans
-// 4 GiB, so the host admits k_direct only for vectors of < 2^32 bytes
-// (kDirMaxVecBytes; launch_direct refuses larger ones)
+// element gathers through a raw buffer resource: byte offsets in 32-bit
+// unsigned arithmetic over a resource of exactly the vector's bytes, so the
+// host admits k_direct only for vectors of < 2^32 bytes (kDirMaxVecBytes;
+// launch_direct refuses larger ones); an offset at or past the end reads 0
 constexpr uint64_t kDirMaxVecBytes = 0xffffffffull;
 template <bool VC>
-__device__ __forceinline__ val_t<VC> ld_rsrc(__amdgpu_buffer_rsrc_t r, int e) {
+__device__ __forceinline__ val_t<VC> ld_rsrc_b(__amdgpu_buffer_rsrc_t r, uint32_t byte) {
   if constexpr (VC) {
-    const auto q = __builtin_amdgcn_raw_buffer_load_b128(r, (int)((uint32_t)e * 16u), 0, 0);
+    const auto q = __builtin_amdgcn_raw_buffer_load_b128(r, (int)byte, 0, 0);
     return __builtin_bit_cast(double2, q);
   } else {
-    const auto q = __builtin_amdgcn_raw_buffer_load_b64(r, (int)((uint32_t)e * 8u), 0, 0);
+    const auto q = __builtin_amdgcn_raw_buffer_load_b64(r, (int)byte, 0, 0);
     return __builtin_bit_cast(double, q);
   }
 }
@@ -897,6 +901,57 @@ __global__ void __launch_bounds__(kBlock) k_gen_diag(const EdModel* __restrict__
   }
 }
 
+// One op group with UNI/LANE pattern M (bit j: op j is a LANE op), summed
+// into acc in op order.  ownb: the lane's own rank in bytes; oobb: the byte
+// offset past the vector (gathers there read 0).
+template <int M, bool HC, bool VC>
+__device__ __forceinline__ void dir_group(const DirGroup& G, uint32_t up, uint32_t ownb, uint32_t oobb,
+                                          const uint16_t* __restrict__ srank, __amdgpu_buffer_rsrc_t xr,
+                                          val_t<VC>& acc) {
+  using V = val_t<VC>;
+  using H = val_t<HC>;
+  constexpr uint32_t lsz = VC ? 4u : 3u;
+  uint32_t rk[kDirGroup];
+#pragma unroll
+  for (int j = 0; j < kDirGroup; j++)
+    if ((M >> j) & 1) rk[j] = srank[up ^ G.flipu[j]];
+  // real H on real vectors: the lane's sign goes onto the gathered value
+  // ((-g) h == g (-h) bit for bit), which keeps h a scalar operand
+  constexpr bool GSIGN = !HC && !VC;
+  uint32_t off[kDirGroup], neg[kDirGroup];
+  H h[kDirGroup];
+#pragma unroll
+  for (int j = 0; j < kDirGroup; j++) {
+    const uint32_t base = (uint32_t)G.delta[j] << lsz;  // scalar
+    neg[j] = 0;
+    if ((M >> j) & 1) {
+      const bool f = ((up & G.cmask[j]) == G.cval[j]) & ((uint32_t)__builtin_popcount(up & G.xm[j]) == G.xv[j]);
+      neg[j] = (uint32_t)__builtin_popcount(up & G.smasku[j]) & 1u;
+      off[j] = f ? base + (rk[j] << lsz) : oobb;
+      if constexpr (HC)
+        h[j] = make_double2(flip_sign(G.re[j], neg[j]),
+                            ((G.imsig >> j) & 1u) ? flip_sign(G.im[j], neg[j]) : G.im[j]);
+      else if constexpr (GSIGN)
+        h[j] = G.re[j];
+      else
+        h[j] = flip_sign(G.re[j], neg[j]);
+    } else {
+      off[j] = base + ownb;
+      h[j] = mk<HC>(G.re[j], G.im[j]);
+    }
+  }
+  V g[kDirGroup];
+#pragma unroll
+  for (int j = 0; j < kDirGroup; j++) g[j] = ld_rsrc_b<VC>(xr, off[j]);
+#pragma unroll
+  for (int j = 0; j < kDirGroup; j++) {
+    if constexpr (GSIGN) {
+      if ((M >> j) & 1) g[j] = flip_sign(g[j], neg[j]);
+    }
+    acc = add(acc, mul(h[j], g[j]));
+  }
+}
+
 template <bool HC, bool VC, bool PATLDS, class Epi>
 __global__ void __launch_bounds__(kDirBlock) k_direct(const val_t<HC>* __restrict__ ddiag,
                                                       const DirChunk* __restrict__ chunks, int nchunk,
@@ -907,7 +962,6 @@ __global__ void __launch_bounds__(kDirBlock) k_direct(const val_t<HC>* __restric
                                                       const val_t<VC>* __restrict__ x, int64_t xdim, int64_t row0,
                                                       Epi epi) {
   using V = val_t<VC>;
-  using H = val_t<HC>;
   if (epi.skip()) return;
   epi.prepare();
   extern __shared__ __align__(16) unsigned char smem[];
@@ -929,6 +983,7 @@ __global__ void __launch_bounds__(kDirBlock) k_direct(const val_t<HC>* __restric
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // chunk data and ops: scalar loads
   const uint32_t mask = (1u << ns) - 1u;
+  constexpr uint32_t lsz = VC ? 4u : 3u;
   // chunk schedule: with a grid of 8k blocks each XCD (blocks b = x mod 8)
   // walks one contiguous eighth of the chunks, so its L2 serves the gathers
   // neighbouring rows share
@@ -943,15 +998,9 @@ __global__ void __launch_bounds__(kDirBlock) k_direct(const val_t<HC>* __restric
     cend = nchunk;
     cstep = gridDim.x * (kDirBlock / 64);
   }
-  // gathers through a buffer resource: 32-bit element offsets (one VALU op
-  // per gather instead of a 64-bit address).  The resource spans exactly the
-  // sector vector, so a lane whose op does not fire gathers element xdim:
-  // out of range, the load returns 0 without touching the cache (the lanes
-  // of an op that fires on half of them used to fetch their own row: the L1
-  // tag lookups of those lines were ~40 % of the kernel's, nonSU2 N26)
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)x, (short)0, (int)(uint32_t)((uint64_t)xdim * sizeof(V)), 0x00020000);
-  const int oob = (int)xdim;
+  // the resource spans exactly the sector vector: offset oobb reads 0
+  const uint32_t oobb = (uint32_t)((uint64_t)xdim * sizeof(V));
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)oobb, 0x00020000);
   double part = 0.0;
   for (; c < cend; c += cstep) {
     const DirChunk ch = chunks[c];
@@ -960,47 +1009,20 @@ __global__ void __launch_bounds__(kDirBlock) k_direct(const val_t<HC>* __restric
     uint32_t up;
     if constexpr (PATLDS) up = spat[ch.pat0 + (on ? lane : 0)];
     else up = map[row] & mask;
-    const uint32_t m = up | (ch.idw << ns);
+    const uint32_t ownb = (uint32_t)srank[up] << lsz;
     const V xi = x[row];
     V acc = add(vzero<V>(), mul(ddiag[row - row0], xi));
     const int g1 = (ch.op0 + ch.nop) / kDirGroup;
     for (int gi = ch.op0 / kDirGroup; gi < g1; gi++) {
       const DirGroup G = grp[gi];
-      int rk[kDirGroup];
-#pragma unroll
-      for (int j = 0; j < kDirGroup; j++) rk[j] = srank[(m ^ G.flip[j]) & mask];
-      // the four rank reads are issued here, not sunk under each op's
-      // condition (the compiler otherwise branches on EXEC per op)
-      asm volatile("" ::"v"(rk[0]), "v"(rk[1]), "v"(rk[2]), "v"(rk[3]));
-      int tg[kDirGroup];
-      bool vd[kDirGroup];
-      H hv[kDirGroup];
-#pragma unroll
-      for (int j = 0; j < kDirGroup; j++) {
-        const uint32_t kind = (uint32_t)G.kind[j];  // scalar: the branch is uniform
-        bool f;
-        uint32_t neg;
-        if (kind & kDirLane) {  // per-lane condition and Jordan-Wigner sign
-          f = ((m & G.req_mask[j]) == G.req_val[j]) &
-              ((uint32_t)__builtin_popcount(m & G.xm[j]) == ((kind >> 4) & 1u));
-          neg = (uint32_t)(__builtin_popcount(m & G.smask[j]) + (kind >> 1)) & 1u;
-        } else {  // down-level op (fires, block sign in c0) or pad (never)
-          f = !(kind & kDirPad);
-          neg = (kind >> 1) & 1u;
-        }
-        vd[j] = f;
-        tg[j] = f ? G.delta[j] + rk[j] : oob;
-        if constexpr (HC)
-          hv[j] = make_double2(flip_sign(G.re[j], neg), (kind & kDirImSigned) ? flip_sign(G.im[j], neg) : G.im[j]);
-        else
-          hv[j] = flip_sign(G.re[j], neg);
+      switch (G.lanes) {  // scalar: one uniform jump per group
+#define ED_DIRG(M) \
+  case M: dir_group<M, HC, VC>(G, up, ownb, oobb, srank, xr, acc); break;
+        ED_DIRG(0) ED_DIRG(1) ED_DIRG(2) ED_DIRG(3) ED_DIRG(4) ED_DIRG(5) ED_DIRG(6) ED_DIRG(7)
+        ED_DIRG(8) ED_DIRG(9) ED_DIRG(10) ED_DIRG(11) ED_DIRG(12) ED_DIRG(13) ED_DIRG(14)
+        default: dir_group<15, HC, VC>(G, up, ownb, oobb, srank, xr, acc); break;
+#undef ED_DIRG
       }
-      V g[kDirGroup];
-#pragma unroll
-      for (int j = 0; j < kDirGroup; j++) g[j] = ld_rsrc<VC>(xr, tg[j]);
-#pragma unroll
-      for (int j = 0; j < kDirGroup; j++)
-        acc = vd[j] ? add(acc, mul(hv[j], g[j])) : acc;  // a select, not an EXEC branch
     }
     if (on) part += epi.row((int64_t)row - row0, acc, xi);
   }

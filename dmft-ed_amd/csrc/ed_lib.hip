@@ -458,40 +458,84 @@ static bool dir_merge(DirOp& a, const DirOp& b, uint32_t nst) {
   return true;
 }
 
-// The kernel's view of one op (host restatement of k_direct's evaluation):
-// fires?, target row, sign.
-static bool dir_apply(const DirOp& o, uint32_t m, uint32_t mask, int64_t row, const std::vector<uint32_t>& rank,
-                      int64_t* tgt, double* sg) {
-  (void)row;
-  const bool f = (m & o.req_mask) == o.req_val &&
-                 (uint32_t)__builtin_popcount(m & o.xm) == (uint32_t)((o.kind & kDirXor) ? 1 : 0);
+// Op q of a block (down pattern idw, first row own0) folded into slot j of
+// a kernel group: conditions, flip and string mask restricted to the up
+// pattern; the sign part fixed by the block's down bits and the string's
+// constant multiplied into the value (a sign flip: the same bits as the
+// reference's products by +-1).  Pads become UNI ops of value 0 on the
+// row's own entry.
+static void dir_fold(const DirOp& o, uint32_t idw, int ns, uint32_t nst, int64_t own0, DirGroup& G, int j) {
+  const uint32_t um = nst - 1, mdw = idw << ns;
+  G.cmask[j] = G.cval[j] = G.flipu[j] = G.smasku[j] = G.xm[j] = G.xv[j] = 0;
+  if (o.kind & kDirPad) {
+    G.delta[j] = (int32_t)own0;
+    G.re[j] = G.im[j] = 0.0;
+    return;
+  }
+  const bool ims = (o.kind & kDirImSigned) != 0;
+  int neg;
+  if (o.kind & kDirLane) {
+    G.lanes |= 1u << j;
+    G.cmask[j] = o.req_mask & um;
+    G.cval[j] = o.req_val & um;
+    G.flipu[j] = o.flip & um;
+    G.smasku[j] = o.smask & um;
+    G.xm[j] = o.xm & um;
+    G.xv[j] = (o.kind & kDirXor) ? 1u : 0u;
+    if (ims) G.imsig |= 1u << j;
+    neg = (__builtin_popcount(mdw & o.smask) + ((o.kind & kDirC0) ? 1 : 0)) & 1;
+  } else {
+    neg = (o.kind & kDirC0) ? 1 : 0;  // the block's whole sign (build_direct)
+  }
+  G.delta[j] = o.delta;
+  G.re[j] = neg ? -o.re : o.re;
+  G.im[j] = (neg && ims) ? -o.im : o.im;
+}
+
+// The kernel's view of op j of a group (host restatement of dir_group):
+// fires?, target row, value.
+static bool dir_eval(const DirGroup& G, int j, uint32_t up, const std::vector<uint32_t>& rank, int64_t* tgt,
+                     double* re, double* im) {
+  if (!((G.lanes >> j) & 1u)) {
+    *tgt = G.delta[j] + (int64_t)rank[up];
+    *re = G.re[j];
+    *im = G.im[j];
+    return true;
+  }
+  const bool f = (up & G.cmask[j]) == G.cval[j] && (uint32_t)__builtin_popcount(up & G.xm[j]) == G.xv[j];
   if (!f) return false;
-  *tgt = o.delta + (int64_t)rank[(m ^ o.flip) & mask];
-  *sg = ((__builtin_popcount(m & o.smask) + ((o.kind & kDirC0) ? 1 : 0)) & 1) ? -1.0 : 1.0;
+  const bool neg = (__builtin_popcount(up & G.smasku[j]) & 1) != 0;
+  *tgt = G.delta[j] + (int64_t)rank[up ^ G.flipu[j]];
+  *re = neg ? -G.re[j] : G.re[j];
+  *im = (neg && ((G.imsig >> j) & 1u)) ? -G.im[j] : G.im[j];
   return true;
 }
 
-// The final op lists against gen_row on sample rows: targets (through the
-// sector's index), value bits and order.
-static int direct_ops_check(const ed_sector* s, const std::vector<DirOp>& ops, const std::vector<DirChunk>& chunks) {
+// The final kernel groups against gen_row on sample rows: targets (through
+// the sector's index), value bits and order (pads: zero products only).
+static int direct_ops_check(const ed_sector* s, const std::vector<DirGroup>& groups, const std::vector<uint8_t>& pad,
+                            const std::vector<DirChunk>& chunks) {
   const SectorTables& T = s->T;
-  const uint32_t mask = T.nst - 1;
   const size_t step = std::max<size_t>(1, chunks.size() / 512);
   for (size_t ci = 0; ci < chunks.size(); ci += step) {
     const DirChunk& ch = chunks[ci];
     for (int l = 0; l < ch.n; l += std::max(1, ch.n / 8)) {
       const int64_t row = ch.row + l;
-      const uint32_t m = T.by_cls[ch.pat0 + l] | (ch.idw << T.ns);
+      const uint32_t up = T.by_cls[ch.pat0 + l];
+      const uint32_t m = up | (ch.idw << T.ns);
       RecAcc ref;
       gen_row(s->Mh, m, ref);
       size_t q = 0;
       for (int k = ch.op0; k < ch.op0 + ch.nop; k++) {
+        const DirGroup& G = groups[k / kDirGroup];
+        const int j = k % kDirGroup;
         int64_t tg;
-        double sg;
-        if (!dir_apply(ops[k], m, mask, row, T.rank, &tg, &sg)) continue;
-        const DirOp& o = ops[k];
-        const double re = o.re * sg;
-        const double im = (o.kind & kDirImSigned) ? o.im * sg : o.im;
+        double re, im;
+        if (!dir_eval(G, j, up, T.rank, &tg, &re, &im)) continue;
+        if (pad[k]) {
+          if (re != 0.0 || im != 0.0 || tg != row) return fail(ED_ERR_STATE, "direct: pad op is not a zero product");
+          continue;
+        }
         if (q >= ref.k.size() || table_index(T, ref.k[q]) != tg || !same_bits(ref.re[q], re) ||
             !same_bits(ref.im[q], im))
           return fail(ED_ERR_STATE, "direct op lists differ from gen_row (row " + std::to_string(row) + ")");
@@ -512,6 +556,7 @@ static int build_direct(ed_sector* s) {
   CK(direct_candidates_check(s, cands));
   std::vector<DirOp> ops;
   std::vector<DirChunk> chunks;
+  std::vector<std::pair<uint32_t, int64_t>> opblk;  // per op: (idw, first row) of its block
   const int64_t r0 = s->row0, r1 = s->row0 + s->nrows;
   for (size_t b = 0; b + 1 < T.blk_off.size(); b++) {
     const int64_t lo = std::max<int64_t>(T.blk_off[b], r0), hi = std::min<int64_t>(T.blk_off[b + 1], r1);
@@ -559,6 +604,7 @@ static int build_direct(ed_sector* s) {
       ops.push_back(o);
     }
     const int32_t nop = (int32_t)ops.size() - op0;
+    opblk.resize(ops.size(), std::make_pair(idw, T.blk_off[b]));
     const int64_t cls0 = T.cls_start[T.need_cls[idw]];
     for (int64_t r = lo; r < hi; r += 64) {
       DirChunk ch{};
@@ -571,22 +617,13 @@ static int build_direct(ed_sector* s) {
       chunks.push_back(ch);
     }
   }
-  CK(direct_ops_check(s, ops, chunks));
-  if (ops.empty()) ops.resize(kDirGroup);  // (valid pointer)
-  std::vector<DirGroup> groups(ops.size() / kDirGroup);
+  std::vector<DirGroup> groups(std::max<size_t>(ops.size() / kDirGroup, 1));  // (valid pointer)
+  std::vector<uint8_t> pad(ops.size(), 0);
   for (size_t q = 0; q < ops.size(); q++) {
-    DirGroup& G = groups[q / kDirGroup];
-    const int j = (int)(q % kDirGroup);
-    G.req_mask[j] = ops[q].req_mask;
-    G.req_val[j] = ops[q].req_val;
-    G.flip[j] = ops[q].flip;
-    G.smask[j] = ops[q].smask;
-    G.delta[j] = ops[q].delta;
-    G.kind[j] = ops[q].kind;
-    G.xm[j] = ops[q].xm;
-    G.re[j] = ops[q].re;
-    G.im[j] = ops[q].im;
+    dir_fold(ops[q], opblk[q].first, ns, nst, opblk[q].second, groups[q / kDirGroup], (int)(q % kDirGroup));
+    pad[q] = (ops[q].kind & kDirPad) ? 1 : 0;
   }
+  CK(direct_ops_check(s, groups, pad, chunks));
   std::vector<uint16_t> rk(std::max<uint32_t>(nst, 8), 0), pt(std::max<uint32_t>(nst, 8), 0);
   for (uint32_t x = 0; x < nst; x++) {
     rk[x] = (uint16_t)T.rank[x];
