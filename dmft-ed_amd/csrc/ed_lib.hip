@@ -2026,6 +2026,8 @@ struct Trlan {
   int kFinFoldG = 128;
   bool graphs_on = true;  // false (ED_OPT_NO_GRAPH): sweeps launched directly
   bool solo = true;       // false (ED_OPT_TRLAN_NOSOLO): multi-kernel CGS on small sectors too (A/B)
+  bool locupd = true;     // false (ED_OPT_TRLAN_FULLUPD): full CGS update every step (A/B)
+  int* lof = nullptr;     // device: the current step's update was local-only
   double *Y = nullptr, *npart = nullptr, *alpha = nullptr, *beta = nullptr;
   double *npA = nullptr, *npB = nullptr;  // |w|^2 partials before / after the first CGS pass (DGKS)
   // persistent sweep (k_trl_sweep): grid, ping-pong residuals, barrier words
@@ -2052,11 +2054,12 @@ struct Trlan {
   // with jn >= 0: alpha[jn], beta[jn] = ||x|| afterwards
   // one fused sweep (k_cgs) with the column group rounded up to 8/16/24/32
   bool cgs(int ncol, const double2* hin, V* x, double2* pt, double* np, const double2* pin = nullptr,
-           int add = 0, const double* dgA = nullptr, const double* dgB = nullptr) {
+           int add = 0, const double* dgA = nullptr, const double* dgB = nullptr, int* lf = nullptr,
+           const double* locA = nullptr) {
     const int nc = (ncol + 7) / 8 * 8;
 #define ED_CGS(NCV) \
   hipLaunchKernelGGL((k_cgs<VC, NCV>), dim3(G), dim3(kBlock), 0, st, Vb, ncol, hin, x, dim, pt, np, pin, G, \
-                     coef, add, dgA, dgB)
+                     coef, add, dgA, dgB, lf, locA)
     if (nc <= 8) ED_CGS(8);
     else if (nc <= 16) ED_CGS(16);
     else if (nc <= 24) ED_CGS(24);
@@ -2074,7 +2077,7 @@ struct Trlan {
       const int nc = (ncol + 7) / 8 * 8;
 #define ED_OSOLO(NCV)                                                                                          \
   hipLaunchKernelGGL((k_orth_solo<VC, NCV>), dim3(1), dim3(kOrthSoloBlock), 0, st, Vb, ncol, x, dim, coef,     \
-                     jn >= 0 ? alpha : nullptr, beta, jn, js, o, shifted)
+                     jn >= 0 ? alpha : nullptr, beta, jn, js, o, shifted, (shifted && locupd) ? 1 : 0)
       if (nc <= 8) ED_OSOLO(8);
       else if (nc <= 16) ED_OSOLO(16);
       else if constexpr (!VC) {
@@ -2087,18 +2090,22 @@ struct Trlan {
     // fused CGS: dots + |x|^2 | x -= V h1, dots, |x'|^2 | (DGKS: only if
     // |x'| <= 0.717 |x|) x -= V h2, |x''|^2 — V streamed 2x or 3x
     if (fused && ncol > 0 && cgs(ncol, nullptr, x, part, npA)) {
+      // shifted steps: the update may be local-only (cgs_loc_only, decided
+      // by the first update pass from the dots and recorded in *lof)
+      int* const lf = (shifted && locupd) ? lof : nullptr;
+      const double* const la = lf ? npA : nullptr;
       if (G <= kFinFoldG) {
         // small grids: each pass forms the previous pass's coefficients from
         // its partials (k_vdot_fin folded in: 5 launches per step, not 7)
-        cgs(ncol, nullptr, x, part2, npB, part, 0);
-        cgs(ncol, nullptr, x, nullptr, npart, part2, 1, npA, npB);
+        cgs(ncol, nullptr, x, part2, npB, part, 0, nullptr, nullptr, lf, la);
+        cgs(ncol, nullptr, x, nullptr, npart, part2, 1, npA, npB, lf);
       } else {
         hipLaunchKernelGGL(k_vdot_fin<VC>, dim3(ncol), dim3(kBlock), 0, st, part, G, h, coef, 0,
-                           (const double*)nullptr, (const double*)nullptr);
-        cgs(ncol, h, x, part2, npB);
+                           (const double*)nullptr, (const double*)nullptr, (const int*)nullptr);
+        cgs(ncol, h, x, part2, npB, nullptr, 0, nullptr, nullptr, lf, la);
         hipLaunchKernelGGL(k_vdot_fin<VC>, dim3(ncol), dim3(kBlock), 0, st, part2, G, h, coef, 1,
-                           (const double*)npA, (const double*)npB);
-        cgs(ncol, h, x, nullptr, npart, nullptr, 0, npA, npB);
+                           (const double*)npA, (const double*)npB, (const int*)lf);
+        cgs(ncol, h, x, nullptr, npart, nullptr, 0, npA, npB, lf);
       }
       if (out && jn >= 0)  // + V_{j+1} = x / beta_j in the same launch
         hipLaunchKernelGGL(k_coef_scale<VC>, dim3(G), dim3(kBlock), 0, st, npart, G, coef, jn, alpha, beta,
@@ -2115,7 +2122,7 @@ struct Trlan {
     for (int pass = 0; pass < 2 && ncol > 0; pass++) {
       hipLaunchKernelGGL(k_vdot_part<VC>, gp, dim3(kBlock), 0, st, Vb, ncol, x, dim, part);
       hipLaunchKernelGGL(k_vdot_fin<VC>, dim3(ncol), dim3(kBlock), 0, st, part, G, h, coef, pass,
-                         (const double*)nullptr, (const double*)nullptr);
+                         (const double*)nullptr, (const double*)nullptr, (const int*)nullptr);
       hipLaunchKernelGGL(k_vaxpy<VC>, dim3(G), dim3(kBlock), 0, st, Vb, ncol, h, x, dim,
                          pass == 1 ? npart : nullptr);
     }
@@ -2170,6 +2177,7 @@ struct Trlan {
         a.dim = dim;
         a.j = j;
         a.shifted = loc ? 1 : 0;
+        a.locupd = locupd ? 1 : 0;
         const int nc = (j + 1 + 7) / 8 * 8;
         if (nc <= 8) hipLaunchKernelGGL(k_step_solo<8>, dim3(1), dim3(kOrthSoloBlock), 0, st, a);
         else if (nc <= 16) hipLaunchKernelGGL(k_step_solo<16>, dim3(1), dim3(kOrthSoloBlock), 0, st, a);
@@ -2411,6 +2419,7 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
   T.graphs_on = !(s->opts & ED_OPT_NO_GRAPH);
   T.local = !(s->opts & ED_OPT_TRLAN_NOLOCAL);
   T.solo = !(s->opts & ED_OPT_TRLAN_NOSOLO);
+  T.locupd = !(s->opts & ED_OPT_TRLAN_FULLUPD);
   const int64_t dim = s->dim;
   const int m = (int)std::min<int64_t>(ncv, dim);
   if (nev < 1 || nev >= m) return fail(ED_ERR_ARG, "need 1 <= nev < min(ncv, dim)");
@@ -2431,6 +2440,7 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
   CK(T.alloc((void**)&T.npart, (size_t)T.G * sizeof(double)));
   CK(T.alloc((void**)&T.npA, (size_t)T.G * sizeof(double)));
   CK(T.alloc((void**)&T.npB, (size_t)T.G * sizeof(double)));
+  CK(T.alloc((void**)&T.lof, sizeof(int)));
   CK(T.alloc((void**)&T.alpha, (kTrlanMaxCols + 8) * sizeof(double)));
   CK(T.alloc((void**)&T.beta, (kTrlanMaxCols + 8) * sizeof(double)));
   CK(T.alloc((void**)&T.Y, (size_t)mcap * mcap * sizeof(double)));
@@ -2697,7 +2707,8 @@ int ed_sector_destroy(ed_sector* s) {
 static constexpr int32_t kOptKnown =
     ED_OPT_NO_PERSIST | ED_OPT_PERSIST_STORED | ED_OPT_NO_PREG | ED_OPT_NO_PKRON | ED_OPT_FUSED_STEP |
     ED_OPT_SPLIT_SIMPLE | ED_OPT_NO_BATCH | ED_OPT_EIGH_NO_VERIFY | ED_OPT_TRLAN_UNFUSED | ED_OPT_TRLAN_NOFOLD |
-    ED_OPT_TRLAN_PSWEEP | ED_OPT_NO_GRAPH | ED_OPT_TRLAN_NOLOCAL | ED_OPT_TRLAN_NOSOLO | ED_OPT_PKRON_C1024;
+    ED_OPT_TRLAN_PSWEEP | ED_OPT_NO_GRAPH | ED_OPT_TRLAN_NOLOCAL | ED_OPT_TRLAN_NOSOLO | ED_OPT_TRLAN_FULLUPD |
+    ED_OPT_PKRON_C1024;
 
 int ed_sector_set_options(ed_sector* s, int32_t opts) {
   if (!s) return fail(ED_ERR_ARG, "null");

@@ -53,6 +53,50 @@ __device__ __forceinline__ bool dgks_skip(const double* __restrict__ nA, const d
   return sk != 0;
 }
 
+// Local-only update.  After the shifted three-term step (EpiTrlLoc) the
+// first Gram-Schmidt pass finds w nearly orthogonal to every basis column
+// but the last two: the coefficients h_c, c < j-1, are rounding noise
+// (round-4 measurement on configs[3] sectors: 2-30 eps of |w| at the 90th
+// percentile, tools in DESIGN.md).  Subtracting V h over all j+1 columns
+// then streams V a second time to correct at noise level.  When
+//   |w - h_j v_j - h_{j-1} v_{j-1}|^2 = |w|^2 - |h_j|^2 - |h_{j-1}|^2 > 0.717^2 |w|^2
+// (no cancellation: ARPACK's DGKS bound) and every far |h_c| <= 64 eps of
+// that norm, the update subtracts the last two columns only and no second
+// pass is made; the measured far coefficients keep the decision honest (the
+// dots are always taken, so a basis that drifts gets the full update).
+constexpr double kCgsLocTol = 64.0 * 2.220446049250313e-16;
+__device__ __forceinline__ double wave_max_f64(double v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+  return v;
+}
+// Block-uniform decision from the first pass's coefficients h[0, ncol) and
+// its |w|^2 partials nA[0, G) (every block sums them in the same order).
+// Needs blockDim >= 64.
+__device__ __forceinline__ bool cgs_loc_only(const double2* __restrict__ h, int ncol,
+                                             const double* __restrict__ nA, int G) {
+  __shared__ int lo;
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    double a = 0.0, hl = 0.0, far = 0.0;
+    for (int i = lane; i < G; i += 64) a += nA[i];
+    for (int c = lane; c < ncol; c += 64) {
+      const double v = h[c].x * h[c].x + h[c].y * h[c].y;
+      if (c >= ncol - 2) hl += v;
+      else far = fmax(far, v);
+    }
+    a = wave_sum_dpp(a);
+    hl = wave_sum_dpp(hl);
+    far = wave_max_f64(far);
+    if (lane == 63) {
+      const double wl = a - hl;
+      lo = (wl > kDgks2 * a) && (far <= kCgsLocTol * kCgsLocTol * wl);
+    }
+  }
+  __syncthreads();
+  return lo != 0;
+}
+
 // part[c * G + blockIdx.x] (re, im) = partial <V_c, w>; blockIdx.y picks the
 // column chunk [8y, 8y+8) ∩ [0, ncol).
 template <bool VC>
@@ -88,7 +132,8 @@ template <bool VC>
 __global__ void __launch_bounds__(kBlock) k_vdot_fin(const double2* __restrict__ part, int G,
                                                      double2* __restrict__ h, double2* __restrict__ coef,
                                                      int add, const double* dgA = nullptr,
-                                                     const double* dgB = nullptr) {
+                                                     const double* dgB = nullptr, const int* lof = nullptr) {
+  if (lof && *lof) return;                     // local-only step: no second pass
   if (dgA && dgks_skip(dgA, dgB, G)) return;  // conditional second pass not needed
   const int c = blockIdx.x;
   double re = 0.0, im = 0.0;
@@ -250,14 +295,16 @@ __global__ void __launch_bounds__(kBlock) k_cgs(const val_t<VC>* __restrict__ V,
                                                 double2* __restrict__ part, double* __restrict__ npart,
                                                 const double2* __restrict__ pin = nullptr, int gin = 0,
                                                 double2* __restrict__ coef = nullptr, int add = 0,
-                                                const double* dgA = nullptr, const double* dgB = nullptr) {
+                                                const double* dgA = nullptr, const double* dgB = nullptr,
+                                                int* lof = nullptr, const double* locA = nullptr) {
   constexpr int NW = kBlock / 64;
   constexpr int NR = (VC ? 2 * NC : NC) + 1;  // partial slots per wave
   __shared__ double2 hs[NC];
   __shared__ double red[NW][NR];
   // conditional second pass (dgA != null): when the DGKS test says the first
-  // pass sufficed, the norm partials of w' (dgB) are this pass's result
-  if (dgA && dgks_skip(dgA, dgB, gridDim.x)) {
+  // pass sufficed, or the update was local-only (lof), the norm partials of
+  // w' (dgB) are this pass's result
+  if (dgA && ((lof && *lof) || dgks_skip(dgA, dgB, gridDim.x))) {
     if (threadIdx.x == 0) npart[blockIdx.x] = dgB[blockIdx.x];
     return;
   }
@@ -285,6 +332,18 @@ __global__ void __launch_bounds__(kBlock) k_cgs(const val_t<VC>* __restrict__ V,
     for (int c = threadIdx.x; c < ncol; c += kBlock) hs[c] = hin[c];
     __syncthreads();
   }
+  // first update pass of a fused step (locA = |w|^2 partials of the dots
+  // pass): local-only when the far coefficients are noise (cgs_loc_only);
+  // the decision goes to *lof for the passes after this one
+  int c0 = 0;
+  if (locA) {
+    const bool lo = cgs_loc_only(hs, ncol, locA, pin ? gin : (int)gridDim.x);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *lof = lo ? 1 : 0;
+    if (lo) {
+      c0 = ncol - 2;
+      part = nullptr;  // no second pass: no dots
+    }
+  }
   const bool upd = hin || pin;
   double are[NC], aim[VC ? NC : 1];
 #pragma unroll
@@ -296,12 +355,12 @@ __global__ void __launch_bounds__(kBlock) k_cgs(const val_t<VC>* __restrict__ V,
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < dim; i += (int64_t)gridDim.x * kBlock) {
     val_t<VC> v[NC];
 #pragma unroll
-    for (int c = 0; c < NC; c++) v[c] = c < ncol ? V[(int64_t)c * dim + i] : vzero<val_t<VC>>();
+    for (int c = 0; c < NC; c++) v[c] = (c >= c0 && c < ncol) ? V[(int64_t)c * dim + i] : vzero<val_t<VC>>();
     auto xi = x[i];
     if (upd) {
 #pragma unroll
       for (int c = 0; c < NC; c++) {
-        if (c >= ncol) continue;  // uniform
+        if (c < c0 || c >= ncol) continue;  // uniform
         if constexpr (VC) {
           xi.x -= v[c].x * hs[c].x - v[c].y * hs[c].y;
           xi.y -= v[c].x * hs[c].y + v[c].y * hs[c].x;
@@ -377,7 +436,7 @@ __device__ __forceinline__ void orth_solo_body(const val_t<VC>* __restrict__ V, 
                                                val_t<VC>* __restrict__ x, int64_t dim,
                                                double2* __restrict__ coef, double* __restrict__ alpha,
                                                double* __restrict__ beta, int jn, int jslot,
-                                               val_t<VC>* __restrict__ out, int shifted) {
+                                               val_t<VC>* __restrict__ out, int shifted, int locupd) {
   using Vt = val_t<VC>;
   constexpr int NT = kOrthSoloBlock, NW = NT / 64;
   constexpr int NR = (VC ? 2 * NC : NC) + 1;  // partial slots: re[NC] | im[NC] | norm
@@ -416,18 +475,18 @@ __device__ __forceinline__ void orth_solo_body(const val_t<VC>* __restrict__ V, 
       if constexpr (VC) aim[c] = 0.0;
     }
   };
-  // x -= V h (h in LDS); optional dots of the result; returns |x|^2 partial
-  auto pass = [&](const double2* h, bool dots) {
+  // x -= V[:, c0:ncol] h (h in LDS); optional dots of the result; returns |x|^2 partial
+  auto pass = [&](const double2* h, bool dots, int c0) {
     double n2 = 0.0;
     for (int64_t i = t; i < dim; i += NT) {
       Vt v[NC];
 #pragma unroll
-      for (int c = 0; c < NC; c++) v[c] = c < ncol ? V[(int64_t)c * dim + i] : vzero<Vt>();
+      for (int c = 0; c < NC; c++) v[c] = (c >= c0 && c < ncol) ? V[(int64_t)c * dim + i] : vzero<Vt>();
       Vt xi = x[i];
       if (h) {
 #pragma unroll
         for (int c = 0; c < NC; c++) {
-          if (c >= ncol) continue;  // uniform
+          if (c < c0 || c >= ncol) continue;  // uniform
           if constexpr (VC) {
             xi.x -= v[c].x * h[c].x - v[c].y * h[c].y;
             xi.y -= v[c].x * h[c].y + v[c].y * h[c].x;
@@ -451,22 +510,31 @@ __device__ __forceinline__ void orth_solo_body(const val_t<VC>* __restrict__ V, 
   };
   // pass 1: h1 = V^H x, |x|^2
   zero();
-  reduce(ncol, pass(nullptr, true));
+  reduce(ncol, pass(nullptr, true, 0));
   const double nA = tot[NR - 1];
   if (t < ncol) h1[t] = make_double2(tot[t], VC ? tot[NC + t] : 0.0);
   __syncthreads();
-  // pass 2: x -= V h1; h2 = V^H x, |x'|^2
-  zero();
-  reduce(ncol, pass(h1, true));
-  const double nB = tot[NR - 1];
-  if (t < ncol) h2[t] = make_double2(tot[t], VC ? tot[NC + t] : 0.0);
-  __syncthreads();
-  double nF = nB;
-  const bool second = !(nB > kDgks2 * nA);  // ARPACK's DGKS test (block-uniform)
-  if (second) {
+  double nF;
+  bool second = false;
+  if (locupd && cgs_loc_only(h1, ncol, tot + (NR - 1), 1)) {
+    // local-only update (kCgsLocTol): the last two columns, no second pass
     zero();
-    reduce(0, pass(h2, false));
+    reduce(0, pass(h1, false, ncol - 2));
     nF = tot[NR - 1];
+  } else {
+    // pass 2: x -= V h1; h2 = V^H x, |x'|^2
+    zero();
+    reduce(ncol, pass(h1, true, 0));
+    const double nB = tot[NR - 1];
+    if (t < ncol) h2[t] = make_double2(tot[t], VC ? tot[NC + t] : 0.0);
+    __syncthreads();
+    nF = nB;
+    second = !(nB > kDgks2 * nA);  // ARPACK's DGKS test (block-uniform)
+    if (second) {
+      zero();
+      reduce(0, pass(h2, false, 0));
+      nF = tot[NR - 1];
+    }
   }
   if (t < ncol) {
     const double2 c = second ? make_double2(h1[t].x + h2[t].x, h1[t].y + h2[t].y) : h1[t];
@@ -486,8 +554,9 @@ __global__ void __launch_bounds__(kOrthSoloBlock) k_orth_solo(const val_t<VC>* _
                                                               val_t<VC>* __restrict__ x, int64_t dim,
                                                               double2* __restrict__ coef, double* __restrict__ alpha,
                                                               double* __restrict__ beta, int jn, int jslot,
-                                                              val_t<VC>* __restrict__ out, int shifted) {
-  orth_solo_body<VC, NC>(V, ncol, x, dim, coef, alpha, beta, jn, jslot, out, shifted);
+                                                              val_t<VC>* __restrict__ out, int shifted,
+                                                              int locupd) {
+  orth_solo_body<VC, NC>(V, ncol, x, dim, coef, alpha, beta, jn, jslot, out, shifted, locupd);
 }
 
 // A whole Krylov step of a small stored sector in ONE workgroup (real
@@ -508,6 +577,7 @@ struct StepSoloArgs {
   double* beta;
   int64_t dim;
   int j, shifted;      // column j; shifted: w = (H - alpha_{j-1}) v_j - beta_{j-1} v_{j-1}
+  int locupd;          // local-only CGS update allowed (kCgsLocTol)
 };
 
 template <int NC>
@@ -545,7 +615,8 @@ __global__ void __launch_bounds__(kOrthSoloBlock) k_step_solo(const StepSoloArgs
     a.x[i] = a.shifted ? (acc - sg * xi) - bp * vprev[i] : acc;
   }
   // (each thread's orthogonalisation passes read back only its own rows of x)
-  orth_solo_body<false, NC>(a.Vb, j + 1, a.x, dim, a.coef, a.alpha, a.beta, j, j, a.out, a.shifted);
+  orth_solo_body<false, NC>(a.Vb, j + 1, a.x, dim, a.coef, a.alpha, a.beta, j, j, a.out, a.shifted,
+                            a.shifted && a.locupd);
 }
 
 // ------------------------------------------------------------------------

@@ -83,6 +83,7 @@ extern "C" {
 #define ED_OPT_NO_GRAPH       0x800 /* eigh: Krylov sweeps launched directly, not as hipGraphs  */
 #define ED_OPT_TRLAN_NOLOCAL  0x1000 /* eigh: plain w = H v_j (no shifted three-term step)     */
 #define ED_OPT_TRLAN_NOSOLO   0x2000 /* eigh: multi-kernel CGS also on sectors <= 2048 rows     */
+#define ED_OPT_TRLAN_FULLUPD  0x4000 /* eigh: full CGS update every step (no local-only update) */
 #define ED_OPT_PKRON_C1024    0x8000 /* Lanczos MODE 4, complex vectors: 1024-thread LDS layout  */
 
 /* status codes */
