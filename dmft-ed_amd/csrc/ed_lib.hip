@@ -444,6 +444,7 @@ static bool dir_merge(DirOp& a, const DirOp& b, uint32_t nst) {
       (a.kind & kDirImSigned) != (b.kind & kDirImSigned) || a.smask != b.smask)
     return false;
   if (a.req_mask != b.req_mask || (a.req_mask & fl) != fl) return false;
+  if ((a.req_mask & ~fl & (nst - 1)) != 0) return false;  // (the kernel's single condition form)
   if ((a.req_val & ~fl) != (b.req_val & ~fl)) return false;
   const uint32_t va = a.req_val & fl, vb = b.req_val & fl;
   if (__builtin_popcount(va) != 1 || (va ^ vb) != fl) return false;
@@ -476,12 +477,21 @@ static void dir_fold(const DirOp& o, uint32_t idw, int ns, uint32_t nst, int64_t
   int neg;
   if (o.kind & kDirLane) {
     G.lanes |= 1u << j;
-    G.cmask[j] = o.req_mask & um;
-    G.cval[j] = o.req_val & um;
+    // one condition form: popc((u ^ cval) & cmask) == xv — the op's bit
+    // conditions (xv = 0), or a merged hop pair's "exactly one of the two
+    // bits" (xv = 1; dir_merge leaves such an op no other up-bit condition)
+    G.xm[j] = o.xm & um;
+    if (o.kind & kDirXor) {
+      G.cmask[j] = o.xm & um;
+      G.cval[j] = 0;
+      G.xv[j] = 1;
+    } else {
+      G.cmask[j] = o.req_mask & um;
+      G.cval[j] = o.req_val & um;
+      G.xv[j] = 0;
+    }
     G.flipu[j] = o.flip & um;
     G.smasku[j] = o.smask & um;
-    G.xm[j] = o.xm & um;
-    G.xv[j] = (o.kind & kDirXor) ? 1u : 0u;
     if (ims) G.imsig |= 1u << j;
     neg = (__builtin_popcount(mdw & o.smask) + ((o.kind & kDirC0) ? 1 : 0)) & 1;
   } else {
@@ -502,7 +512,7 @@ static bool dir_eval(const DirGroup& G, int j, uint32_t up, const std::vector<ui
     *im = G.im[j];
     return true;
   }
-  const bool f = (up & G.cmask[j]) == G.cval[j] && (uint32_t)__builtin_popcount(up & G.xm[j]) == G.xv[j];
+  const bool f = (uint32_t)__builtin_popcount((up ^ G.cval[j]) & G.cmask[j]) == G.xv[j];
   if (!f) return false;
   const bool neg = (__builtin_popcount(up & G.smasku[j]) & 1) != 0;
   *tgt = G.delta[j] + (int64_t)rank[up ^ G.flipu[j]];
@@ -606,12 +616,12 @@ static int build_direct(ed_sector* s) {
     const int32_t nop = (int32_t)ops.size() - op0;
     opblk.resize(ops.size(), std::make_pair(idw, T.blk_off[b]));
     const int64_t cls0 = T.cls_start[T.need_cls[idw]];
-    for (int64_t r = lo; r < hi; r += 64) {
+    for (int64_t r = lo; r < hi; r += 64 * kDirRows) {
       DirChunk ch{};
       ch.row = (int32_t)r;
       ch.idw = idw;
       ch.pat0 = (int32_t)(cls0 + (r - T.blk_off[b]));
-      ch.n = (int32_t)std::min<int64_t>(64, hi - r);
+      ch.n = (int32_t)std::min<int64_t>(64 * kDirRows, hi - r);
       ch.op0 = op0;
       ch.nop = nop;
       chunks.push_back(ch);
@@ -675,7 +685,7 @@ static int launch_direct(ed_sector* s, const void* x, Epi epi, hipStream_t st) {
   if ((uint64_t)s->dim * sizeof(V) > kDirMaxVecBytes)
     return fail(ED_ERR_UNSUPPORTED, "k_direct: vector of " + std::to_string(s->dim) +
                                         " elements exceeds the 4 GiB gather range (use the stored or Kronecker path)");
-  auto fn = k_direct<HC, VC, PL, Epi>;
+  auto fn = k_direct<HC, VC, PL, VC ? kDirRows : 1, Epi>;
   // dynamic LDS beyond 64 KB: allow what the 160 KB leave next to the
   // function's static LDS (the epilogue's reduction slots)
   static std::once_flag attr;
@@ -2101,10 +2111,10 @@ struct Trlan {
         cgs(ncol, nullptr, x, nullptr, npart, part2, 1, npA, npB, lf);
       } else {
         hipLaunchKernelGGL(k_vdot_fin<VC>, dim3(ncol), dim3(kBlock), 0, st, part, G, h, coef, 0,
-                           (const double*)nullptr, (const double*)nullptr, (const int*)nullptr);
+                           (const double*)nullptr, (const double*)nullptr);
         cgs(ncol, h, x, part2, npB, nullptr, 0, nullptr, nullptr, lf, la);
         hipLaunchKernelGGL(k_vdot_fin<VC>, dim3(ncol), dim3(kBlock), 0, st, part2, G, h, coef, 1,
-                           (const double*)npA, (const double*)npB, (const int*)lf);
+                           (const double*)npA, (const double*)npB);
         cgs(ncol, h, x, nullptr, npart, nullptr, 0, npA, npB, lf);
       }
       if (out && jn >= 0)  // + V_{j+1} = x / beta_j in the same launch
@@ -2122,7 +2132,7 @@ struct Trlan {
     for (int pass = 0; pass < 2 && ncol > 0; pass++) {
       hipLaunchKernelGGL(k_vdot_part<VC>, gp, dim3(kBlock), 0, st, Vb, ncol, x, dim, part);
       hipLaunchKernelGGL(k_vdot_fin<VC>, dim3(ncol), dim3(kBlock), 0, st, part, G, h, coef, pass,
-                         (const double*)nullptr, (const double*)nullptr, (const int*)nullptr);
+                         (const double*)nullptr, (const double*)nullptr);
       hipLaunchKernelGGL(k_vaxpy<VC>, dim3(G), dim3(kBlock), 0, st, Vb, ncol, h, x, dim,
                          pass == 1 ? npart : nullptr);
     }

@@ -58,12 +58,13 @@ __device__ __forceinline__ bool dgks_skip(const double* __restrict__ nA, const d
 // but the last two: the coefficients h_c, c < j-1, are rounding noise
 // (round-4 measurement on configs[3] sectors: 2-30 eps of |w| at the 90th
 // percentile, tools in DESIGN.md).  Subtracting V h over all j+1 columns
-// then streams V a second time to correct at noise level.  When
-//   |w - h_j v_j - h_{j-1} v_{j-1}|^2 = |w|^2 - |h_j|^2 - |h_{j-1}|^2 > 0.717^2 |w|^2
-// (no cancellation: ARPACK's DGKS bound) and every far |h_c| <= 64 eps of
-// that norm, the update subtracts the last two columns only and no second
-// pass is made; the measured far coefficients keep the decision honest (the
-// dots are always taken, so a basis that drifts gets the full update).
+// then streams V a second time to correct at noise level.  When every far
+// |h_c| <= 64 eps of |w - h_j v_j - h_{j-1} v_{j-1}| (= sqrt(|w|^2 -
+// |h_j|^2 - |h_{j-1}|^2)), the update and the DGKS second pass act on the
+// last two columns only (the second pass still taken when the norm
+// dropped below 0.717 |w|); the measured far coefficients keep the decision
+// honest (the dots are always taken, so a basis that drifts gets the full
+// update).
 constexpr double kCgsLocTol = 64.0 * 2.220446049250313e-16;
 __device__ __forceinline__ double wave_max_f64(double v) {
 #pragma unroll
@@ -90,7 +91,7 @@ __device__ __forceinline__ bool cgs_loc_only(const double2* __restrict__ h, int 
     far = wave_max_f64(far);
     if (lane == 63) {
       const double wl = a - hl;
-      lo = (wl > kDgks2 * a) && (far <= kCgsLocTol * kCgsLocTol * wl);
+      lo = (wl > 0.0) && (far <= kCgsLocTol * kCgsLocTol * wl);
     }
   }
   __syncthreads();
@@ -132,8 +133,8 @@ template <bool VC>
 __global__ void __launch_bounds__(kBlock) k_vdot_fin(const double2* __restrict__ part, int G,
                                                      double2* __restrict__ h, double2* __restrict__ coef,
                                                      int add, const double* dgA = nullptr,
-                                                     const double* dgB = nullptr, const int* lof = nullptr) {
-  if (lof && *lof) return;                     // local-only step: no second pass
+                                                     const double* dgB = nullptr) {
+  // (a local-only step folds stale partials for its far columns: unused)
   if (dgA && dgks_skip(dgA, dgB, G)) return;  // conditional second pass not needed
   const int c = blockIdx.x;
   double re = 0.0, im = 0.0;
@@ -302,9 +303,8 @@ __global__ void __launch_bounds__(kBlock) k_cgs(const val_t<VC>* __restrict__ V,
   __shared__ double2 hs[NC];
   __shared__ double red[NW][NR];
   // conditional second pass (dgA != null): when the DGKS test says the first
-  // pass sufficed, or the update was local-only (lof), the norm partials of
-  // w' (dgB) are this pass's result
-  if (dgA && ((lof && *lof) || dgks_skip(dgA, dgB, gridDim.x))) {
+  // pass sufficed, the norm partials of w' (dgB) are this pass's result
+  if (dgA && dgks_skip(dgA, dgB, gridDim.x)) {
     if (threadIdx.x == 0) npart[blockIdx.x] = dgB[blockIdx.x];
     return;
   }
@@ -333,16 +333,16 @@ __global__ void __launch_bounds__(kBlock) k_cgs(const val_t<VC>* __restrict__ V,
     __syncthreads();
   }
   // first update pass of a fused step (locA = |w|^2 partials of the dots
-  // pass): local-only when the far coefficients are noise (cgs_loc_only);
-  // the decision goes to *lof for the passes after this one
+  // pass): local-only when the far coefficients are noise (cgs_loc_only),
+  // its dots then only for the last two columns; the decision goes to *lof
+  // for the second pass (the columns it updates)
   int c0 = 0;
   if (locA) {
     const bool lo = cgs_loc_only(hs, ncol, locA, pin ? gin : (int)gridDim.x);
     if (blockIdx.x == 0 && threadIdx.x == 0) *lof = lo ? 1 : 0;
-    if (lo) {
-      c0 = ncol - 2;
-      part = nullptr;  // no second pass: no dots
-    }
+    if (lo) c0 = ncol - 2;
+  } else if (lof && *lof) {
+    c0 = ncol - 2;
   }
   const bool upd = hin || pin;
   double are[NC], aim[VC ? NC : 1];
@@ -373,6 +373,7 @@ __global__ void __launch_bounds__(kBlock) k_cgs(const val_t<VC>* __restrict__ V,
     if (part) {
 #pragma unroll
       for (int c = 0; c < NC; c++) {
+        if (c < c0) continue;  // uniform (local-only: far dots unused)
         const double2 t = cdotc(v[c], xi);
         are[c] += t.x;
         if constexpr (VC) aim[c] += t.y;
@@ -384,7 +385,7 @@ __global__ void __launch_bounds__(kBlock) k_cgs(const val_t<VC>* __restrict__ V,
   if (part) {
 #pragma unroll
     for (int c = 0; c < NC; c++) {
-      if (c >= ncol) continue;  // uniform
+      if (c < c0 || c >= ncol) continue;  // uniform
       const double r = wave_sum_dpp(are[c]);
       if (lane == 63) red[wv][c] = r;
       if constexpr (VC) {
@@ -399,7 +400,7 @@ __global__ void __launch_bounds__(kBlock) k_cgs(const val_t<VC>* __restrict__ V,
   }
   __syncthreads();
   const int t = threadIdx.x;
-  if (part && t < ncol) {
+  if (part && t >= c0 && t < ncol) {
     double re = 0.0, im = 0.0;
 #pragma unroll
     for (int w = 0; w < NW; w++) {
@@ -514,27 +515,20 @@ __device__ __forceinline__ void orth_solo_body(const val_t<VC>* __restrict__ V, 
   const double nA = tot[NR - 1];
   if (t < ncol) h1[t] = make_double2(tot[t], VC ? tot[NC + t] : 0.0);
   __syncthreads();
-  double nF;
-  bool second = false;
-  if (locupd && cgs_loc_only(h1, ncol, tot + (NR - 1), 1)) {
-    // local-only update (kCgsLocTol): the last two columns, no second pass
+  // local-only update (kCgsLocTol): passes 2 and 3 on the last two columns
+  const int c0 = (locupd && cgs_loc_only(h1, ncol, tot + (NR - 1), 1)) ? ncol - 2 : 0;
+  // pass 2: x -= V h1; h2 = V^H x, |x'|^2
+  zero();
+  reduce(ncol, pass(h1, true, c0));
+  const double nB = tot[NR - 1];
+  if (t < ncol) h2[t] = make_double2(tot[t], VC ? tot[NC + t] : 0.0);  // (far: 0 when local-only)
+  __syncthreads();
+  double nF = nB;
+  const bool second = !(nB > kDgks2 * nA);  // ARPACK's DGKS test (block-uniform)
+  if (second) {
     zero();
-    reduce(0, pass(h1, false, ncol - 2));
+    reduce(0, pass(h2, false, c0));
     nF = tot[NR - 1];
-  } else {
-    // pass 2: x -= V h1; h2 = V^H x, |x'|^2
-    zero();
-    reduce(ncol, pass(h1, true, 0));
-    const double nB = tot[NR - 1];
-    if (t < ncol) h2[t] = make_double2(tot[t], VC ? tot[NC + t] : 0.0);
-    __syncthreads();
-    nF = nB;
-    second = !(nB > kDgks2 * nA);  // ARPACK's DGKS test (block-uniform)
-    if (second) {
-      zero();
-      reduce(0, pass(h2, false, 0));
-      nF = tot[NR - 1];
-    }
   }
   if (t < ncol) {
     const double2 c = second ? make_double2(h1[t].x + h2[t].x, h1[t].y + h2[t].y) : h1[t];

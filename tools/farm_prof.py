@@ -31,6 +31,7 @@ ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--serial-stats", default="")
 ap.add_argument("--options", default="", help="comma-separated ED_OPT_* names for every sector")
 ap.add_argument("--timeline", default="", help="write per-sector (start, end, thread, dim) of the last rep")
+ap.add_argument("--maps", default="", help="write the process's shared-object mappings (for symbolising a crash)")
 a = ap.parse_args()
 cfg = c4_config("random")
 opts = tuple(x for x in a.options.split(",") if x)
@@ -62,6 +63,26 @@ if a.serial_stats:
                        totals=tot, sectors=rows), f, indent=1)
 
 opt = DiagOptions(workers=a.workers, kernel_options=opts)
+if a.maps:
+    # every mapped shared object with its load base (the lowest start of its
+    # mappings) and the executable segment (start, file offset): native crash
+    # PCs map to (object, offset) for addr2line / llvm-symbolizer in the
+    # builder container (same image)
+    from edgpu import _lib as _edlib  # noqa: E402
+    _edlib.load()
+    objs = {}
+    with open("/proc/self/maps") as fh:
+        for ln in fh:
+            f = ln.split()
+            if len(f) < 6 or not f[5].startswith("/"):
+                continue
+            lo, hi = (int(x, 16) for x in f[0].split("-"))
+            o = objs.setdefault(f[5], {"base": lo, "exec": []})
+            o["base"] = min(o["base"], lo - int(f[2], 16))
+            if "x" in f[1]:
+                o["exec"].append([hex(lo), hex(hi), hex(int(f[2], 16))])
+    with open(a.maps, "w") as fh:
+        json.dump({k: {"base": hex(v["base"]), "exec": v["exec"]} for k, v in objs.items()}, fh, indent=1)
 import threading  # noqa: E402
 
 from edgpu.diag import solve_sector  # noqa: E402
