@@ -2421,7 +2421,7 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
   T.path = resolve_path(s, -1);
   T.st = s->stream;
   T.dim = s->dim;
-  T.G = (int)std::min<int64_t>(grid_for(s->dim), kTrlanGridCap);
+  T.G = (int)std::min<int64_t>(grid_for(s->dim), (s->opts & ED_OPT_TRLAN_G128) ? 128 : kTrlanGridCap);
   T.hp = trlan_pinned();
   if (!T.hp) return fail(ED_ERR_OOM, "pinned host staging buffer");
   T.fused = !(s->opts & ED_OPT_TRLAN_UNFUSED);
@@ -2718,7 +2718,7 @@ static constexpr int32_t kOptKnown =
     ED_OPT_NO_PERSIST | ED_OPT_PERSIST_STORED | ED_OPT_NO_PREG | ED_OPT_NO_PKRON | ED_OPT_FUSED_STEP |
     ED_OPT_SPLIT_SIMPLE | ED_OPT_NO_BATCH | ED_OPT_EIGH_NO_VERIFY | ED_OPT_TRLAN_UNFUSED | ED_OPT_TRLAN_NOFOLD |
     ED_OPT_TRLAN_PSWEEP | ED_OPT_NO_GRAPH | ED_OPT_TRLAN_NOLOCAL | ED_OPT_TRLAN_NOSOLO | ED_OPT_TRLAN_FULLUPD |
-    ED_OPT_PKRON_C1024;
+    ED_OPT_PKRON_C1024 | ED_OPT_TRLAN_G128;
 
 int ed_sector_set_options(ed_sector* s, int32_t opts) {
   if (!s) return fail(ED_ERR_ARG, "null");
