@@ -2078,7 +2078,9 @@ struct Trlan {
 #undef ED_CGS
     return true;
   }
-  int orth(int ncol, V* x, int jn, V* out = nullptr, int shifted = 0) {
+  // jc: the basis column of v_j when it is not column jn (probe_screen's
+  // rolling window; alpha/beta slot jn)
+  int orth(int ncol, V* x, int jn, V* out = nullptr, int shifted = 0, int jc = -1) {
     // small sectors: the whole CGS2 + alpha/beta + V_{j+1} in one workgroup
     // (complex vectors: up to 16 columns; the 24/32-column forms spill)
     if (fused && solo && ncol > 0 && dim <= kOrthSoloMaxDim && ncol <= (VC ? 16 : 32)) {
@@ -2087,7 +2089,7 @@ struct Trlan {
       const int nc = (ncol + 7) / 8 * 8;
 #define ED_OSOLO(NCV)                                                                                          \
   hipLaunchKernelGGL((k_orth_solo<VC, NCV>), dim3(1), dim3(kOrthSoloBlock), 0, st, Vb, ncol, x, dim, coef,     \
-                     jn >= 0 ? alpha : nullptr, beta, jn, js, o, shifted, (shifted && locupd) ? 1 : 0)
+                     jn >= 0 ? alpha : nullptr, beta, jn, js, o, shifted, (shifted && locupd) ? 1 : 0, jc)
       if (nc <= 8) ED_OSOLO(8);
       else if (nc <= 16) ED_OSOLO(16);
       else if constexpr (!VC) {
@@ -2119,10 +2121,10 @@ struct Trlan {
       }
       if (out && jn >= 0)  // + V_{j+1} = x / beta_j in the same launch
         hipLaunchKernelGGL(k_coef_scale<VC>, dim3(G), dim3(kBlock), 0, st, npart, G, coef, jn, alpha, beta,
-                           x, out, dim, shifted);
+                           x, out, dim, shifted, jc);
       else
         hipLaunchKernelGGL(k_trl_coef, dim3(1), dim3(kBlock), 0, st, npart, G, coef, jn >= 0 ? jn : m,
-                           jn >= 0 ? alpha : nullptr, beta, jn >= 0 ? shifted : 0);
+                           jn >= 0 ? alpha : nullptr, beta, jn >= 0 ? shifted : 0, jc);
       return ED_OK;
     }
     if (ncol == 0) {
@@ -2137,7 +2139,7 @@ struct Trlan {
                          pass == 1 ? npart : nullptr);
     }
     hipLaunchKernelGGL(k_trl_coef, dim3(1), dim3(kBlock), 0, st, npart, G, coef, jn >= 0 ? jn : m,
-                       jn >= 0 ? alpha : nullptr, beta, jn >= 0 ? shifted : 0);  // beta[m]: scratch slot
+                       jn >= 0 ? alpha : nullptr, beta, jn >= 0 ? shifted : 0, jc);  // beta[m]: scratch slot
     if (out && jn >= 0)
       hipLaunchKernelGGL(k_scale_into<VC>, dim3(grid_for(dim)), dim3(kBlock), 0, st, x, out, beta + jn, dim);
     return ED_OK;
@@ -2403,6 +2405,93 @@ static int trlan_core(Trlan<VC>& T, int k0, int nev, int maxit, double tol, cons
   return ED_OK;
 }
 
+// Screening solve of the degeneracy probe (trlan_run): is there an
+// eigenvalue of H below `cut` on the orthogonal complement of the locked
+// columns [0, k0)?  A plain Lanczos recurrence from a hash start vector,
+// without restarts and without keeping the Krylov basis: a rolling window of
+// two columns (k0, k0+1) behind the locked ones holds v_{k-1} and v_k, and
+// every step is orthogonalised against the locked columns and the window by
+// the fused CGS (local-only when the locked coefficients are noise) — so a
+// step streams k0 + 2 columns, not the k0 + 20 of the thick-restart probe,
+// and the Krylov dimension is not capped by a restart.  Every kScreenChunk
+// steps the host forms the lowest Ritz value theta of the tridiagonal and
+// its residual bound |beta_k s_k| (first-row QL of the reversed matrix,
+// ed_tridiag_poles).  *below = 1: theta < cut (a missed eigenvalue: the
+// thick-restart probe then finds its vector); 0: theta converged to `tol`
+// and >= cut (none); -1: undecided within maxsteps (thick-restart probe).
+constexpr int kScreenChunk = 10;
+constexpr int kScreenMaxSteps = 400;
+template <bool VC>
+static int probe_screen(Trlan<VC>& T, int k0, int maxsteps, double tol, double cut, uint64_t seed, int* below) {
+  using V = val_t<VC>;
+  const int64_t dim = T.dim;
+  hipStream_t st = T.st;
+  const int64_t nd = dim * (VC ? 2 : 1);
+  const int ca = k0, cb = k0 + 1;
+  *below = -1;
+  if (maxsteps < 2 || k0 + 2 > T.mcap) return ED_OK;
+  // the recurrence's alpha/beta in T.alpha/T.beta's place for the duration
+  double *pa = nullptr, *pb = nullptr;
+  const int na = std::max(maxsteps, T.m) + 2;
+  CK(T.alloc((void**)&pa, na * sizeof(double)));
+  CK(T.alloc((void**)&pb, na * sizeof(double)));
+  double* const sa = T.alpha;
+  double* const sb = T.beta;
+  struct Restore {
+    Trlan<VC>& t; double* a; double* b;
+    ~Restore() { t.alpha = a; t.beta = b; }
+  } restore{T, sa, sb};
+  T.alpha = pa;
+  T.beta = pb;
+  HIPCK(hipMemsetAsync(T.col(T.Vb, cb), 0, dim * sizeof(V), st));  // v_{-1} = 0
+  hipLaunchKernelGGL(k_hash_vec, dim3(grid_for(nd)), dim3(kBlock), 0, st, (double*)T.w, nd, seed);
+  CK(T.orth(k0, T.w, -1));  // against the locked columns; the norm -> beta[m]
+  hipLaunchKernelGGL(k_scale_into<VC>, dim3(grid_for(dim)), dim3(kBlock), 0, st, T.w, T.col(T.Vb, ca),
+                     T.beta + T.m, dim);
+  HIPCK(hipGetLastError());
+  double* const hp = T.hp;  // pinned staging: alpha | beta of one chunk
+  std::vector<double> al, be;
+  for (int k0s = 0; k0s < maxsteps; k0s += kScreenChunk) {
+    const int k1 = std::min(maxsteps, k0s + kScreenChunk);
+    for (int k = k0s; k < k1; k++) {
+      const int cur = (k & 1) ? cb : ca, prv = (k & 1) ? ca : cb;
+      T.nhv++;
+      if (k == 0) {
+        EpiStore<VC> e{T.w};
+        CK(launch_hxv<VC>(T.s, T.path, T.col(T.Vb, cur), e, st));
+      } else {
+        EpiTrlLoc<VC> e{T.w, T.col(T.Vb, prv), pa + (k - 1), pb + (k - 1)};
+        CK(launch_hxv<VC>(T.s, T.path, T.col(T.Vb, cur), e, st));
+      }
+      // alpha slot k, basis column cur; v_{k+1} = w / beta_k -> the window's other column
+      CK(T.orth(k0 + 2, T.w, k, T.col(T.Vb, prv), k > 0 ? 1 : 0, cur));
+    }
+    const int n = k1 - k0s;
+    HIPCK(hipMemcpyAsync(hp, pa + k0s, n * sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPCK(hipMemcpyAsync(hp + 72, pb + k0s, n * sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPCK(hipStreamSynchronize(st));
+    al.insert(al.end(), hp, hp + n);
+    be.insert(be.end(), hp + 72, hp + 72 + n);
+    // lowest Ritz value and the last component of its vector: the reversed
+    // tridiagonal's first components
+    const int K = (int)al.size();
+    std::vector<double> ar(K), br(K, 0.0), E(K), z2(K), z1(K);
+    for (int i = 0; i < K; i++) ar[i] = al[K - 1 - i];
+    for (int i = 1; i < K; i++) br[i] = be[K - 1 - i];
+    if (ed_tridiag_poles(K, ar.data(), br.data(), E.data(), z2.data(), z1.data()) != ED_OK) return ED_OK;
+    const double theta = E[0], resid = fabs(be[K - 1] * z1[0]);
+    if (theta < cut) {
+      *below = 1;
+      return ED_OK;
+    }
+    if (resid <= tol * std::max(3.6e-11, fabs(theta)) || be[K - 1] < 1e-13 * (fabs(theta) + 1e-300)) {
+      *below = 0;
+      return ED_OK;
+    }
+  }
+  return ED_OK;
+}
+
 // sp_eigh replacement.  A single-vector Krylov method (ARPACK as much as this
 // one) sees one direction of each degenerate eigenspace — the other copies
 // only through rounding — so the lowest nev of a degenerate spectrum can come
@@ -2491,6 +2580,15 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
       constexpr double kProbeTol = 1e-5;  // 1e-3 misses copies; 1e-4 and 1e-5 find them
       const double tprobe = std::max(tol, kProbeTol);
       const double cut = ev[nev - 1] - 1e-9 * std::max(1.0, fabs(ev[nev - 1]));
+      if (!(s->opts & ED_OPT_EIGH_FULLPROBE)) {
+        // cheap screen first: a plain Lanczos run on the complement decides
+        // most sectors (no missed eigenvalue); the thick-restart probe below
+        // runs only when it finds one or cannot decide
+        int scr = -1;
+        CK(probe_screen(T, nev, (int)std::min<int64_t>(dim - nev, kScreenMaxSteps), tprobe, cut, 3000 + round,
+                        &scr));
+        if (scr == 0) break;
+      }
       CK(trlan_core(T, nev, 1, maxit, tprobe, nullptr, 1000 + round, th2, Z2, &c2));
       if (!(c2 == 1 && th2[0] < cut)) break;
       if (tprobe > tol) {
@@ -2718,7 +2816,7 @@ static constexpr int32_t kOptKnown =
     ED_OPT_NO_PERSIST | ED_OPT_PERSIST_STORED | ED_OPT_NO_PREG | ED_OPT_NO_PKRON | ED_OPT_FUSED_STEP |
     ED_OPT_SPLIT_SIMPLE | ED_OPT_NO_BATCH | ED_OPT_EIGH_NO_VERIFY | ED_OPT_TRLAN_UNFUSED | ED_OPT_TRLAN_NOFOLD |
     ED_OPT_TRLAN_PSWEEP | ED_OPT_NO_GRAPH | ED_OPT_TRLAN_NOLOCAL | ED_OPT_TRLAN_NOSOLO | ED_OPT_TRLAN_FULLUPD |
-    ED_OPT_PKRON_C1024 | ED_OPT_TRLAN_G128;
+    ED_OPT_PKRON_C1024 | ED_OPT_TRLAN_G128 | ED_OPT_EIGH_FULLPROBE;
 
 int ed_sector_set_options(ed_sector* s, int32_t opts) {
   if (!s) return fail(ED_ERR_ARG, "null");

@@ -181,16 +181,19 @@ __global__ void __launch_bounds__(kBlock) k_vaxpy(const val_t<VC>* __restrict__ 
 }
 
 // beta[j] = ||w|| from the partials; alpha[j] = Re coef[j]
+// (jc: the basis column of v_j when it differs from the alpha/beta slot j —
+// the rolling two-column window of probe_screen)
 static __global__ void __launch_bounds__(kBlock) k_trl_coef(const double* __restrict__ npart, int G,
                                                      const double2* __restrict__ coef, int j,
                                                      double* __restrict__ alpha, double* __restrict__ beta,
-                                                     int shifted = 0) {
+                                                     int shifted = 0, int jc = -1) {
   double t = 0.0;
   for (int b = threadIdx.x; b < G; b += kBlock) t += npart[b];
   t = block_sum(t);
   if (threadIdx.x == 0) {
     beta[j] = sqrt(t);
-    if (alpha) alpha[j] = shifted ? alpha[j - 1] + coef[j].x : coef[j].x;  // (EpiTrlLoc)
+    const int c = jc >= 0 ? jc : j;
+    if (alpha) alpha[j] = shifted ? alpha[j - 1] + coef[c].x : coef[c].x;  // (EpiTrlLoc)
   }
 }
 
@@ -266,7 +269,7 @@ __global__ void __launch_bounds__(kBlock) k_coef_scale(const double* __restrict_
                                                        double* __restrict__ alpha, double* __restrict__ beta,
                                                        const val_t<VC>* __restrict__ x,
                                                        val_t<VC>* __restrict__ out, int64_t dim,
-                                                       int shifted = 0) {
+                                                       int shifted = 0, int jc = -1) {
   double t = 0.0;
   for (int b = threadIdx.x; b < G; b += kBlock) t += npart[b];
   t = block_sum(t);
@@ -274,7 +277,8 @@ __global__ void __launch_bounds__(kBlock) k_coef_scale(const double* __restrict_
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     beta[j] = nrm;
     // shifted step (EpiTrlLoc): alpha_j = alpha_{j-1} + <v_j, w>
-    if (alpha) alpha[j] = shifted ? alpha[j - 1] + coef[j].x : coef[j].x;
+    const int c = jc >= 0 ? jc : j;
+    if (alpha) alpha[j] = shifted ? alpha[j - 1] + coef[c].x : coef[c].x;
   }
   const double inv = nrm > 0.0 ? 1.0 / nrm : 0.0;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < dim; i += (int64_t)gridDim.x * kBlock)
@@ -437,8 +441,10 @@ __device__ __forceinline__ void orth_solo_body(const val_t<VC>* __restrict__ V, 
                                                val_t<VC>* __restrict__ x, int64_t dim,
                                                double2* __restrict__ coef, double* __restrict__ alpha,
                                                double* __restrict__ beta, int jn, int jslot,
-                                               val_t<VC>* __restrict__ out, int shifted, int locupd) {
+                                               val_t<VC>* __restrict__ out, int shifted, int locupd,
+                                               int jc = -1) {
   using Vt = val_t<VC>;
+  if (jc < 0) jc = jn;  // basis column of v_j (alpha slot jn)
   constexpr int NT = kOrthSoloBlock, NW = NT / 64;
   constexpr int NR = (VC ? 2 * NC : NC) + 1;  // partial slots: re[NC] | im[NC] | norm
   __shared__ double red[NW][NR];
@@ -533,7 +539,7 @@ __device__ __forceinline__ void orth_solo_body(const val_t<VC>* __restrict__ V, 
   if (t < ncol) {
     const double2 c = second ? make_double2(h1[t].x + h2[t].x, h1[t].y + h2[t].y) : h1[t];
     coef[t] = c;
-    if (t == jn && alpha) alpha[jn] = shifted ? alpha[jn - 1] + c.x : c.x;
+    if (t == jc && jn >= 0 && alpha) alpha[jn] = shifted ? alpha[jn - 1] + c.x : c.x;
   }
   const double b = sqrt(nF);
   if (t == 0) beta[jslot] = b;
@@ -549,8 +555,8 @@ __global__ void __launch_bounds__(kOrthSoloBlock) k_orth_solo(const val_t<VC>* _
                                                               double2* __restrict__ coef, double* __restrict__ alpha,
                                                               double* __restrict__ beta, int jn, int jslot,
                                                               val_t<VC>* __restrict__ out, int shifted,
-                                                              int locupd) {
-  orth_solo_body<VC, NC>(V, ncol, x, dim, coef, alpha, beta, jn, jslot, out, shifted, locupd);
+                                                              int locupd, int jc) {
+  orth_solo_body<VC, NC>(V, ncol, x, dim, coef, alpha, beta, jn, jslot, out, shifted, locupd, jc);
 }
 
 // A whole Krylov step of a small stored sector in ONE workgroup (real

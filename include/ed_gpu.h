@@ -86,6 +86,7 @@ extern "C" {
 #define ED_OPT_TRLAN_FULLUPD  0x4000 /* eigh: full CGS update every step (no local-only update) */
 #define ED_OPT_PKRON_C1024    0x8000 /* Lanczos MODE 4, complex vectors: 1024-thread LDS layout  */
 #define ED_OPT_TRLAN_G128    0x10000 /* eigh: Krylov sweeps on <= 128 blocks (coefficients folded) */
+#define ED_OPT_EIGH_FULLPROBE 0x20000 /* eigh: degeneracy probe without the plain-Lanczos screen */
 
 /* status codes */
 #define ED_OK              0
