@@ -829,7 +829,7 @@ __global__ void __launch_bounds__(kBlock) k_spmv_pk(const val_t<HC>* __restrict_
 // selects and sign assembly) and was issue-bound, not L1-bound.
 constexpr int kDirBlock = 1024;
 constexpr int kDirGroup = 4;
-constexpr int kDirRows = 2;  // a chunk is up to 64 * kDirRows rows of one block
+constexpr int kDirRows = 2;  // complex vectors: chunks of up to 64 * kDirRows rows (two per lane)
 // Host form of one op (build_direct), before it is folded into a DirGroup:
 //   fires  = (m & req_mask) == req_val && popc(m & xm) == (kind has kDirXor)
 //   target = delta + rank[(m ^ flip) & up-mask]
@@ -864,7 +864,7 @@ struct DirChunk {
   int32_t row;    // row of lane 0
   uint32_t idw;   // down pattern of the block
   int32_t pat0;   // index of lane 0's up pattern in the by-class table
-  int32_t n;      // rows in the chunk (<= 64 * kDirRows)
+  int32_t n;      // rows in the chunk (<= 64 R)
   int32_t op0, nop;  // the block's ops: [op0, op0 + nop), nop a multiple of kDirGroup
   int32_t pad[2];
 };
@@ -969,10 +969,10 @@ __device__ __forceinline__ void dir_group(const DirGroup& G, const uint32_t* up,
     }
 }
 
-// R: rows of a chunk each lane holds at once (R = kDirRows: the whole chunk
-// in one pass over the ops, their scalar data shared; R = 1: the chunk's
-// halves one after the other — real vectors, measured faster: nonSU2 N26
-// 0.279 against 0.292 ms; complex vectors take R = 2: 0.378 against 0.435)
+// R: rows per lane (chunks of up to 64 R rows; one pass over the ops serves
+// the R rows, their scalar data shared).  Real vectors R = 1: nonSU2 N26
+// 0.279 against 0.292 ms with R = 2; complex vectors R = 2: 0.378 against
+// 0.435 ms.  The host keeps a chunk list for each.
 template <bool HC, bool VC, bool PATLDS, int R, class Epi>
 __global__ void __launch_bounds__(kDirBlock) k_direct(const val_t<HC>* __restrict__ ddiag,
                                                       const DirChunk* __restrict__ chunks, int nchunk,
@@ -1024,40 +1024,37 @@ __global__ void __launch_bounds__(kDirBlock) k_direct(const val_t<HC>* __restric
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)oobb, 0x00020000);
   double part = 0.0;
   for (; c < cend; c += cstep) {
-    const DirChunk ch = chunks[c];
-    for (int h0 = 0; h0 < kDirRows; h0 += R) {  // lane holds rows ch.row + 64 (h0 + r) + lane
-      uint32_t up[R], ownb[R];
-      int row[R];
-      bool on[R];
-      V xi[R], acc[R];
+    const DirChunk ch = chunks[c];  // up to 64 R rows; lane holds rows ch.row + 64 r + lane
+    uint32_t up[R], ownb[R];
+    int row[R];
+    bool on[R];
+    V xi[R], acc[R];
 #pragma unroll
-      for (int r = 0; r < R; r++) {
-        const int l = lane + 64 * (h0 + r);
-        on[r] = l < ch.n;
-        row[r] = ch.row + (on[r] ? l : 0);
-        if constexpr (PATLDS) up[r] = spat[ch.pat0 + (on[r] ? l : 0)];
-        else up[r] = map[row[r]] & mask;
-        ownb[r] = (uint32_t)srank[up[r]] << lsz;
-        xi[r] = x[row[r]];
-        acc[r] = add(vzero<V>(), mul(ddiag[row[r] - row0], xi[r]));
-      }
-      const int g1 = (ch.op0 + ch.nop) / kDirGroup;
-      for (int gi = ch.op0 / kDirGroup; gi < g1; gi++) {
-        const DirGroup G = grp[gi];
-        switch (G.lanes) {  // scalar: one uniform jump per group
+    for (int r = 0; r < R; r++) {
+      const int l = lane + 64 * r;
+      on[r] = l < ch.n;
+      row[r] = ch.row + (on[r] ? l : 0);
+      if constexpr (PATLDS) up[r] = spat[ch.pat0 + (on[r] ? l : 0)];
+      else up[r] = map[row[r]] & mask;
+      ownb[r] = (uint32_t)srank[up[r]] << lsz;
+      xi[r] = x[row[r]];
+      acc[r] = add(vzero<V>(), mul(ddiag[row[r] - row0], xi[r]));
+    }
+    const int g1 = (ch.op0 + ch.nop) / kDirGroup;
+    for (int gi = ch.op0 / kDirGroup; gi < g1; gi++) {
+      const DirGroup G = grp[gi];
+      switch (G.lanes) {  // scalar: one uniform jump per group
 #define ED_DIRG(M) \
   case M: dir_group<M, HC, VC, R>(G, up, ownb, oobb, srank, xr, acc); break;
-          ED_DIRG(0) ED_DIRG(1) ED_DIRG(2) ED_DIRG(3) ED_DIRG(4) ED_DIRG(5) ED_DIRG(6) ED_DIRG(7)
-          ED_DIRG(8) ED_DIRG(9) ED_DIRG(10) ED_DIRG(11) ED_DIRG(12) ED_DIRG(13) ED_DIRG(14)
-          default: dir_group<15, HC, VC, R>(G, up, ownb, oobb, srank, xr, acc); break;
+        ED_DIRG(0) ED_DIRG(1) ED_DIRG(2) ED_DIRG(3) ED_DIRG(4) ED_DIRG(5) ED_DIRG(6) ED_DIRG(7)
+        ED_DIRG(8) ED_DIRG(9) ED_DIRG(10) ED_DIRG(11) ED_DIRG(12) ED_DIRG(13) ED_DIRG(14)
+        default: dir_group<15, HC, VC, R>(G, up, ownb, oobb, srank, xr, acc); break;
 #undef ED_DIRG
-        }
       }
-#pragma unroll
-      for (int r = 0; r < R; r++)
-        if (on[r]) part += epi.row((int64_t)row[r] - row0, acc[r], xi[r]);
-      if (64 * (h0 + R) >= ch.n) break;  // (uniform) no row of the next half
     }
+#pragma unroll
+    for (int r = 0; r < R; r++)
+      if (on[r]) part += epi.row((int64_t)row[r] - row0, acc[r], xi[r]);
   }
   epi.template finish<kDirBlock>(part);
 }

@@ -104,8 +104,10 @@ struct ed_sector {
   void* d_pdict = nullptr;   // real(8) or complex(8) values (hc)
   int npdict = 0;
   // matrix-free, generic (k_direct): chunk list, per-block op lists, 16-bit tables
-  DirChunk* d_dchunk = nullptr;
+  DirChunk* d_dchunk = nullptr;   // 64-row chunks (real vectors)
   int ndchunk = 0;
+  DirChunk* d_dchunk2 = nullptr;  // 128-row chunks (complex vectors, two rows per lane)
+  int ndchunk2 = 0;
   DirGroup* d_dops = nullptr;
   uint16_t *d_rank16 = nullptr, *d_pat16 = nullptr;
   void* d_ddiag = nullptr;   // gen_diag of the sector object's rows (k_gen_diag)
@@ -565,7 +567,7 @@ static int build_direct(ed_sector* s) {
   direct_candidates(s->Mh, cands);
   CK(direct_candidates_check(s, cands));
   std::vector<DirOp> ops;
-  std::vector<DirChunk> chunks;
+  std::vector<DirChunk> chunks, chunks2;  // 64- and 128-row chunks
   std::vector<std::pair<uint32_t, int64_t>> opblk;  // per op: (idw, first row) of its block
   const int64_t r0 = s->row0, r1 = s->row0 + s->nrows;
   for (size_t b = 0; b + 1 < T.blk_off.size(); b++) {
@@ -616,16 +618,17 @@ static int build_direct(ed_sector* s) {
     const int32_t nop = (int32_t)ops.size() - op0;
     opblk.resize(ops.size(), std::make_pair(idw, T.blk_off[b]));
     const int64_t cls0 = T.cls_start[T.need_cls[idw]];
-    for (int64_t r = lo; r < hi; r += 64 * kDirRows) {
-      DirChunk ch{};
-      ch.row = (int32_t)r;
-      ch.idw = idw;
-      ch.pat0 = (int32_t)(cls0 + (r - T.blk_off[b]));
-      ch.n = (int32_t)std::min<int64_t>(64 * kDirRows, hi - r);
-      ch.op0 = op0;
-      ch.nop = nop;
-      chunks.push_back(ch);
-    }
+    for (int rr = 0; rr < 2; rr++)
+      for (int64_t r = lo; r < hi; r += 64 << rr) {
+        DirChunk ch{};
+        ch.row = (int32_t)r;
+        ch.idw = idw;
+        ch.pat0 = (int32_t)(cls0 + (r - T.blk_off[b]));
+        ch.n = (int32_t)std::min<int64_t>(64 << rr, hi - r);
+        ch.op0 = op0;
+        ch.nop = nop;
+        (rr ? chunks2 : chunks).push_back(ch);
+      }
   }
   std::vector<DirGroup> groups(std::max<size_t>(ops.size() / kDirGroup, 1));  // (valid pointer)
   std::vector<uint8_t> pad(ops.size(), 0);
@@ -640,8 +643,11 @@ static int build_direct(ed_sector* s) {
     pt[x] = (uint16_t)T.by_cls[x];
   }
   s->ndchunk = (int)chunks.size();
+  s->ndchunk2 = (int)chunks2.size();
   if (chunks.empty()) chunks.resize(1);
+  if (chunks2.empty()) chunks2.resize(1);
   CK(upload(s, &s->d_dchunk, chunks));
+  CK(upload(s, &s->d_dchunk2, chunks2));
   CK(upload(s, &s->d_dops, groups));
   CK(upload(s, &s->d_rank16, rk));
   CK(upload(s, &s->d_pat16, pt));
@@ -685,7 +691,8 @@ static int launch_direct(ed_sector* s, const void* x, Epi epi, hipStream_t st) {
   if ((uint64_t)s->dim * sizeof(V) > kDirMaxVecBytes)
     return fail(ED_ERR_UNSUPPORTED, "k_direct: vector of " + std::to_string(s->dim) +
                                         " elements exceeds the 4 GiB gather range (use the stored or Kronecker path)");
-  auto fn = k_direct<HC, VC, PL, VC ? kDirRows : 1, Epi>;
+  constexpr int R = VC ? kDirRows : 1;
+  auto fn = k_direct<HC, VC, PL, R, Epi>;
   // dynamic LDS beyond 64 KB: allow what the 160 KB leave next to the
   // function's static LDS (the epilogue's reduction slots)
   static std::once_flag attr;
@@ -702,7 +709,7 @@ static int launch_direct(ed_sector* s, const void* x, Epi epi, hipStream_t st) {
     return fail(ED_ERR_HIP, std::string("k_direct LDS attribute -> ") + hipGetErrorString(ae));
   }
   hipLaunchKernelGGL(fn, dim3(s->dir_grid), dim3(kDirBlock), s->dir_lds, st, (const val_t<HC>*)s->d_ddiag,
-                     s->d_dchunk, s->ndchunk,
+                     R == 1 ? s->d_dchunk : s->d_dchunk2, R == 1 ? s->ndchunk : s->ndchunk2,
                      s->d_dops, s->d_rank16, s->d_pat16, s->d_map, s->T.ns, (const V*)x, s->dim, s->row0, epi);
   return ED_OK;
 }
@@ -1629,7 +1636,8 @@ static int persist_mode(ed_sector* s, int vc, int path) {
 static int64_t persist_lds(const ed_sector* s, int vc, int mode) {
   const int64_t vs = vc ? 16 : 8, vr = persist_vrows(s, mode, vc);
   int64_t lds = ((vr * vs + 15) & ~(int64_t)15);
-  if (mode == 4) return lds + (vc ? vr * 8 + (int64_t)s->pkr_E * (s->pkr_dd + s->pkr_du) * 8 : 0);
+  // (complex: + 16, the 512-thread form's gap between its two vector planes)
+  if (mode == 4) return lds + (vc ? 16 + vr * 8 + (int64_t)s->pkr_E * (s->pkr_dd + s->pkr_du) * 8 : 0);
   if (mode == 2) {
     const int64_t hs = s->hc ? 16 : 8;
     return lds + ((vr * 8 + 15) & ~(int64_t)15) + (((int64_t)s->ndict * hs + 15) & ~(int64_t)15);
@@ -2038,6 +2046,7 @@ struct Trlan {
   bool solo = true;       // false (ED_OPT_TRLAN_NOSOLO): multi-kernel CGS on small sectors too (A/B)
   bool locupd = true;     // false (ED_OPT_TRLAN_FULLUPD): full CGS update every step (A/B)
   int* lof = nullptr;     // device: the current step's update was local-only
+  unsigned int* fold_cnt = nullptr;  // device: k_cgs last-block fold counter (zero between passes), or null
   double *Y = nullptr, *npart = nullptr, *alpha = nullptr, *beta = nullptr;
   double *npA = nullptr, *npB = nullptr;  // |w|^2 partials before / after the first CGS pass (DGKS)
   // persistent sweep (k_trl_sweep): grid, ping-pong residuals, barrier words
@@ -2065,11 +2074,11 @@ struct Trlan {
   // one fused sweep (k_cgs) with the column group rounded up to 8/16/24/32
   bool cgs(int ncol, const double2* hin, V* x, double2* pt, double* np, const double2* pin = nullptr,
            int add = 0, const double* dgA = nullptr, const double* dgB = nullptr, int* lf = nullptr,
-           const double* locA = nullptr) {
+           const double* locA = nullptr, const CgsFold& fold = CgsFold{}) {
     const int nc = (ncol + 7) / 8 * 8;
 #define ED_CGS(NCV) \
   hipLaunchKernelGGL((k_cgs<VC, NCV>), dim3(G), dim3(kBlock), 0, st, Vb, ncol, hin, x, dim, pt, np, pin, G, \
-                     coef, add, dgA, dgB, lf, locA)
+                     coef, add, dgA, dgB, lf, locA, fold)
     if (nc <= 8) ED_CGS(8);
     else if (nc <= 16) ED_CGS(16);
     else if (nc <= 24) ED_CGS(24);
@@ -2101,7 +2110,9 @@ struct Trlan {
     }
     // fused CGS: dots + |x|^2 | x -= V h1, dots, |x'|^2 | (DGKS: only if
     // |x'| <= 0.717 |x|) x -= V h2, |x''|^2 — V streamed 2x or 3x
-    if (fused && ncol > 0 && cgs(ncol, nullptr, x, part, npA)) {
+    unsigned int* const fcnt = (G > kFinFoldG) ? fold_cnt : nullptr;
+    if (fused && ncol > 0 && cgs(ncol, nullptr, x, part, npA, nullptr, 0, nullptr, nullptr, nullptr, nullptr,
+                                 CgsFold{fcnt, h, coef, 0, nullptr})) {
       // shifted steps: the update may be local-only (cgs_loc_only, decided
       // by the first update pass from the dots and recorded in *lof)
       int* const lf = (shifted && locupd) ? lof : nullptr;
@@ -2111,6 +2122,13 @@ struct Trlan {
         // its partials (k_vdot_fin folded in: 5 launches per step, not 7)
         cgs(ncol, nullptr, x, part2, npB, part, 0, nullptr, nullptr, lf, la);
         cgs(ncol, nullptr, x, nullptr, npart, part2, 1, npA, npB, lf);
+      } else if (fcnt) {
+        // large grids: the last block of each pass folds its coefficients
+        // (cgs_fold_last; ED_OPT_TRLAN_VDOTFIN: the separate k_vdot_fin, A/B).
+        // Pass A's fold ran in the launch above (fold armed there).
+        CgsFold f2{fcnt, h, coef, 1, npA};
+        cgs(ncol, h, x, part2, npB, nullptr, 0, nullptr, nullptr, lf, la, f2);
+        cgs(ncol, h, x, nullptr, npart, nullptr, 0, npA, npB, lf);
       } else {
         hipLaunchKernelGGL(k_vdot_fin<VC>, dim3(ncol), dim3(kBlock), 0, st, part, G, h, coef, 0,
                            (const double*)nullptr, (const double*)nullptr);
@@ -2386,7 +2404,9 @@ static int trlan_core(Trlan<VC>& T, int k0, int nev, int maxit, double tol, cons
       if (fabs(beta * Z[(ma - 1) + (size_t)ma * i]) <= tol * std::max(eps23, fabs(theta[i]))) conv++;
     if (conv == nev || it == maxit - 1 || m == dim) break;
     // thick restart: keep nkeep Ritz vectors + the residual direction
-    const int nkeep = std::max(nev, std::min(ma - 2, nev + (ma - nev) / 2));
+    int nkeep = std::max(nev, std::min(ma - 2, nev + (ma - nev) / 2));
+    if (const char* ek = getenv("ED_TRLAN_KEEP"))  // A/B (tools/trlan_ab.py): nev + k kept
+      nkeep = std::max(nev, std::min(ma - 2, nev + atoi(ek)));
     // (the previous restart's upload of hZ completed at this sweep's sync)
     std::copy(Z.begin(), Z.begin() + (size_t)ma * ma, hZ);
     HIPCK(hipMemcpyAsync(T.Y, hZ, (size_t)ma * ma * sizeof(double), hipMemcpyHostToDevice, st));
@@ -2540,6 +2560,10 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
   CK(T.alloc((void**)&T.npA, (size_t)T.G * sizeof(double)));
   CK(T.alloc((void**)&T.npB, (size_t)T.G * sizeof(double)));
   CK(T.alloc((void**)&T.lof, sizeof(int)));
+  if (!(s->opts & ED_OPT_TRLAN_VDOTFIN)) {
+    CK(T.alloc((void**)&T.fold_cnt, sizeof(unsigned int)));
+    HIPCK(hipMemsetAsync(T.fold_cnt, 0, sizeof(unsigned int), T.st));
+  }
   CK(T.alloc((void**)&T.alpha, (kTrlanMaxCols + 8) * sizeof(double)));
   CK(T.alloc((void**)&T.beta, (kTrlanMaxCols + 8) * sizeof(double)));
   CK(T.alloc((void**)&T.Y, (size_t)mcap * mcap * sizeof(double)));
@@ -2815,7 +2839,7 @@ int ed_sector_destroy(ed_sector* s) {
 static constexpr int32_t kOptKnown =
     ED_OPT_NO_PERSIST | ED_OPT_PERSIST_STORED | ED_OPT_NO_PREG | ED_OPT_NO_PKRON | ED_OPT_FUSED_STEP |
     ED_OPT_SPLIT_SIMPLE | ED_OPT_NO_BATCH | ED_OPT_EIGH_NO_VERIFY | ED_OPT_TRLAN_UNFUSED | ED_OPT_TRLAN_NOFOLD |
-    ED_OPT_TRLAN_PSWEEP | ED_OPT_NO_GRAPH | ED_OPT_TRLAN_NOLOCAL | ED_OPT_TRLAN_NOSOLO | ED_OPT_TRLAN_FULLUPD |
+    ED_OPT_TRLAN_PSWEEP | ED_OPT_NO_GRAPH | ED_OPT_TRLAN_NOLOCAL | ED_OPT_TRLAN_NOSOLO | ED_OPT_TRLAN_FULLUPD | ED_OPT_TRLAN_VDOTFIN |
     ED_OPT_PKRON_C1024 | ED_OPT_TRLAN_G128 | ED_OPT_EIGH_FULLPROBE;
 
 int ed_sector_set_options(ed_sector* s, int32_t opts) {

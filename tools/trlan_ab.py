@@ -22,25 +22,38 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--opts", default="trlan_fullupd,eigh_no_verify")
 ap.add_argument("--sectors", default="6,6;5,6;4,5;3,4;2,3")
+ap.add_argument("--ncv", default="", help="comma list of ncv values (restart length) instead of the options")
+ap.add_argument("--keep", default="", help="comma list of ED_TRLAN_KEEP values (Ritz vectors kept beyond nev)")
 a = ap.parse_args()
 cfg = c4_config("random")
 opt = DiagOptions()
-variants = [("default", ())] + [(o, (o,)) for o in a.opts.split(",") if o]
+variants = [("default", (), None, None)]
+if a.ncv or a.keep:
+    for n in (a.ncv.split(",") if a.ncv else [None]):
+        for k in (a.keep.split(",") if a.keep else [None]):
+            variants.append((f"ncv={n} keep={k}", (), int(n) if n else None, k))
+else:
+    variants += [(o, (o,), None, None) for o in a.opts.split(",") if o]
 for q in a.sectors.split(";"):
     q1, q2 = (int(x) for x in q.split(","))
     with Sector(cfg, q1, q2, stored=True, real=True) as S:
         neigen, nitermax, nblock = lanczos_params(S.dim, opt)
         v0 = _start_vector(S.dim, False)
         ref = None
-        for name, o in variants:
+        for name, o, ncv, keep in variants:
             S.set_options(*o)
+            if keep is None:
+                os.environ.pop("ED_TRLAN_KEEP", None)
+            else:
+                os.environ["ED_TRLAN_KEEP"] = keep
             best, nhv = 1e9, 0
             for _ in range(a.reps):
                 torch.cuda.synchronize()
                 t = time.perf_counter()
-                w, _, _, nhv = S.eigh(neigen=neigen, ncv=min(nblock, 64), maxit=nitermax, v0=v0, vectors=False)
+                w, _, _, nhv = S.eigh(neigen=neigen, ncv=min(ncv or nblock, 64), maxit=nitermax, v0=v0, vectors=False)
                 best = min(best, time.perf_counter() - t)
             ref = w if ref is None else ref
             print(f"({q1},{q2}) dim {S.dim:7d} {name:15s} {best * 1e3:8.2f} ms  nhv {nhv:4d}  "
                   f"dE {np.max(np.abs(np.asarray(w) - ref)):.1e}", flush=True)
         S.set_options()
+        os.environ.pop("ED_TRLAN_KEEP", None)
