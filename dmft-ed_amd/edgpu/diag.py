@@ -57,6 +57,12 @@ class DiagOptions:
     # ED_OPT_* kernel alternatives (Sector.set_options names) for every sector
     # of the diagonalisation (A/B runs; the defaults are the measured best)
     kernel_options: Tuple[str, ...] = ()
+    # concurrent sectors' working sets (Krylov basis + stored H, estimated by
+    # `working_set_bytes`) are admitted up to this many MB, so that the bases
+    # being streamed by the Gram-Schmidt sweeps stay in the 256 MB Infinity
+    # Cache instead of evicting each other to HBM; a sector larger than the
+    # budget runs when nothing else big is in flight.  0: no limit.
+    cache_budget_mb: float = 0.0
 
 
 @dataclass
@@ -192,22 +198,73 @@ def retain_state_vectors(sl: StateList, results: Iterable[SectorResult],
     return StateList(list(sl.energies), list(sl.sectors), vecs)
 
 
+def working_set_bytes(cfg: EDConfig, sec: SectorId, opt: DiagOptions) -> float:
+    """Device bytes a sector's solve streams repeatedly: the Krylov basis
+    (Nblock columns), the packed stored H (4 B per element, ~1 + Norb*Nbath
+    per row) and the O(dim) vectors (diagonal, residual, scratch)."""
+    _, _, nblock = lanczos_params(sec.dim, opt)
+    vs = 8 if cfg.is_real() else 16
+    return float(sec.dim) * (nblock * vs + 4.0 * (1 + cfg.Norb * cfg.Nbath) + 4 * vs)
+
+
 def solve_many(cfg: EDConfig, secs: List[SectorId], opt: DiagOptions, device: int = 0,
                solver=None, cost=None) -> List[SectorResult]:
     """Solve a list of sectors on one GPU with `opt.workers` host threads,
     largest first; results in the order of `secs` (each sector's result does
-    not depend on the schedule)."""
+    not depend on the schedule).  With `opt.cache_budget_mb` a worker takes
+    the largest pending sector whose working set fits beside those in flight
+    (a sector larger than the budget only when nothing else big runs), else
+    waits for one to finish."""
     solver = solver or solve_sector
     if opt.workers <= 1 or len(secs) <= 1:
         return [solver(cfg, sec, opt, device) for sec in secs]
-    from concurrent.futures import ThreadPoolExecutor
+    import threading
 
     order = sorted(range(len(secs)), key=lambda i: -(cost(secs[i]) if cost else secs[i].dim))
+    budget = opt.cache_budget_mb * 1e6
+    # (sectors below 16 MB are not counted: they fit the cache beside anything)
+    ws = [working_set_bytes(cfg, s, opt) if budget > 0 else 0.0 for s in secs]
+    ws = [w if w >= 16e6 else 0.0 for w in ws]
     out: List[Optional[SectorResult]] = [None] * len(secs)
-    with ThreadPoolExecutor(max_workers=opt.workers) as ex:
-        futs = {i: ex.submit(solver, cfg, secs[i], opt, device) for i in order}
-        for i, f in futs.items():
-            out[i] = f.result()
+    err: List[BaseException] = []
+    pending = list(order)
+    used = [0.0]
+    cv = threading.Condition()
+
+    def take() -> Optional[int]:
+        with cv:
+            while pending and not err:
+                for k, i in enumerate(pending):
+                    if ws[i] == 0.0 or used[0] + ws[i] <= budget or used[0] == 0.0:
+                        used[0] += ws[i]
+                        return pending.pop(k)
+                cv.wait()
+            return None
+
+    def worker():
+        while True:
+            i = take()
+            if i is None:
+                return
+            try:
+                out[i] = solver(cfg, secs[i], opt, device)
+            except BaseException as e:  # noqa: BLE001 - re-raised by the caller
+                with cv:
+                    err.append(e)
+            finally:
+                with cv:
+                    used[0] -= ws[i]
+                    if used[0] < 1.0:
+                        used[0] = 0.0
+                    cv.notify_all()
+
+    threads = [threading.Thread(target=worker, daemon=True) for _ in range(min(opt.workers, len(secs)))]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    if err:
+        raise err[0]
     return out
 
 

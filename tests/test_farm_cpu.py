@@ -28,6 +28,43 @@ def test_lpt_partition_balances_c4():
             assert max(loads) / (sum(costs) / n) < 1.05   # ~8x achievable
 
 
+@pytest.mark.parametrize("budget_mb", [0.0, 300.0])
+def test_solve_many_cache_budget(budget_mb):
+    """solve_many's scheduler: results in input order whatever the schedule;
+    with a cache budget the working sets counted in flight never exceed it
+    except for one sector alone (configs[3], a sleeping fake solver)."""
+    import threading
+    import time
+
+    from edgpu.diag import SectorResult, solve_many, working_set_bytes
+
+    cfg = make_config(Norb=2, Nbath=5)
+    opt = DiagOptions(workers=8, cache_budget_mb=budget_mb)
+    secs = setup_pointers(cfg)
+    ws = {s.isector: working_set_bytes(cfg, s, opt) for s in secs}
+    lock = threading.Lock()
+    live, peaks = {}, []
+
+    def solver(c, sec, o, device):
+        w = ws[sec.isector] if ws[sec.isector] >= 16e6 else 0.0
+        with lock:
+            live[sec.isector] = w
+            peaks.append((sum(live.values()), sum(1 for v in live.values() if v > 0)))
+        time.sleep(1e-3 + 2e-11 * sec.dim)
+        with lock:
+            del live[sec.isector]
+        return SectorResult(sec.isector, (sec.q1, sec.q2), sec.dim, np.zeros(1), 1)
+
+    out = solve_many(cfg, secs, opt, solver=solver, cost=lambda s: sector_cost(cfg, s, opt))
+    assert [r.isector for r in out] == [s.isector for s in secs]
+    big = sum(1 for v in ws.values() if v >= 16e6)
+    assert big >= 4                                   # the test has something to schedule
+    if budget_mb > 0:
+        assert all(tot <= budget_mb * 1e6 or n == 1 for tot, n in peaks)
+    else:
+        assert max(n for _, n in peaks) > 1
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))

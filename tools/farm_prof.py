@@ -30,6 +30,7 @@ ap.add_argument("--workers", type=int, default=8)
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--serial-stats", default="")
 ap.add_argument("--options", default="", help="comma-separated ED_OPT_* names for every sector")
+ap.add_argument("--budget", type=float, default=None, help="DiagOptions.cache_budget_mb (default: the library default)")
 ap.add_argument("--timeline", default="", help="write per-sector (start, end, thread, dim) of the last rep")
 ap.add_argument("--maps", default="", help="write the process's shared-object mappings (for symbolising a crash)")
 a = ap.parse_args()
@@ -63,6 +64,8 @@ if a.serial_stats:
                        totals=tot, sectors=rows), f, indent=1)
 
 opt = DiagOptions(workers=a.workers, kernel_options=opts)
+if a.budget is not None:
+    opt.cache_budget_mb = a.budget
 if a.maps:
     # every mapped shared object with its load base (the lowest start of its
     # mappings) and the executable segment (start, file offset): native crash

@@ -12,5 +12,6 @@ bash tools/gpu_step.sh \
  "cvec:120:python3 $R/tools/cvec_probe.py" \
  "ncv:400:python3 $R/tools/trlan_ab.py --reps 2 --ncv 16,23,32,44 --keep 1,3,6,12" \
  "vdotfin:300:python3 $R/tools/trlan_ab.py --reps 3 --opts trlan_vdotfin" \
- "farm:200:python3 $R/tools/farm_prof.py --reps 3 && python3 $R/tools/farm_prof.py --reps 2 --options trlan_vdotfin"
+ "farm:200:python3 $R/tools/farm_prof.py --reps 3 && python3 $R/tools/farm_prof.py --reps 2 --options trlan_vdotfin" \
+ "budget:300:for b in 250 400 700; do python3 $R/tools/farm_prof.py --reps 2 --budget $b || exit 1; done"
 du -sh $O
