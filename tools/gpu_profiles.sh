@@ -40,6 +40,11 @@ for e in "${ENTRIES[@]}"; do
   grep ms/launch "$OUT/st_$name.log"
   f=$(find "$OUT/st_$name" -name "*kernel_stats.csv" | head -1)
   [ -n "$f" ] && cp "$f" "$PROF/${name}_kernel_stats.csv"
+  # steady-state per-launch durations (the probe's 3 warm-ups dropped): the
+  # figure bench.py's HIP-event average is compared with
+  t=$(find "$OUT/st_$name" -name "*kernel_trace.csv" | head -1)
+  [ -n "$t" ] && python3 "$R/tools/trace_summary.py" "$t" "$pat" 3 "$PROF/${name}_trace.json" \
+    --note "spmv_probe.py $args --iters 30: 3 warm-up + 60 launches" > /dev/null
   for c in FETCH_SIZE WRITE_SIZE; do
     ( cd /tmp && export TMPDIR=/tmp && \
       timeout -s KILL 120 rocprofv3 --pmc $c --kernel-trace -d "$OUT/pmc_${name}_$c" -o pmc --output-format csv -- \
@@ -49,6 +54,7 @@ for e in "${ENTRIES[@]}"; do
   python3 "$R/tools/traffic_json.py" "$PROF/${name}_traffic.json" "$pat" "$OUT/pmc_${name}_FETCH_SIZE" \
     "$OUT/pmc_${name}_WRITE_SIZE" "spmv_probe.py $args" > /dev/null || { echo "traffic $name failed"; exit 1; }
   mkdir -p "$R/profiles/$TAG" && cp "$PROF/${name}_traffic.json" "$R/profiles/$TAG/"  # for a bench.py later in the same call
+  [ -f "$PROF/${name}_trace.json" ] && cp "$PROF/${name}_trace.json" "$R/profiles/$TAG/"
   echo "profile $name ok"
 done
 find "$OUT" -name "*kernel_trace.csv" -size +2M -delete
