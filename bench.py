@@ -50,7 +50,7 @@ import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 GOLD = os.path.join(ROOT, "tests", "golden")
-PROFILES = os.path.join(ROOT, "profiles", "r3")
+PROFILES = [os.path.join(ROOT, "profiles", r) for r in ("r4", "r3")]  # newest summary first
 
 
 def spmv_bytes_real(nnz, dim):
@@ -304,14 +304,31 @@ def bench_batched(S, v0, niter, last_alpha, ks=(256, 1024), cplx=False):
 
 def _traffic(name):
     """Per-launch HBM-side bytes from a committed rocprofv3 summary
-    (profiles/r3/<name>.json: 2 x FETCH_SIZE + WRITE_SIZE, the gfx950 x2
-    calibrated for 4/8/16-B lane loads in profiles/r2/fetch_calib.json)."""
-    f = os.path.join(PROFILES, name)
-    if not os.path.exists(f):
-        return None, None
-    with open(f) as fh:
-        tj = json.load(fh)
-    return tj.get("traffic_bytes_per_launch"), f"profiles/r3/{name}"
+    (profiles/r4/<name>.json, else round 3's: 2 x FETCH_SIZE + WRITE_SIZE, the
+    gfx950 x2 calibrated for 4/8/16-B lane loads in profiles/r2/fetch_calib.json)."""
+    for d in PROFILES:
+        f = os.path.join(d, name)
+        if os.path.exists(f):
+            with open(f) as fh:
+                tj = json.load(fh)
+            return tj.get("traffic_bytes_per_launch"), os.path.relpath(f, ROOT)
+    return None, None
+
+
+def _profile_ms(name):
+    """Steady-state per-launch duration of the same kernel on the same sector
+    from a committed rocprofv3 kernel trace (profiles/r4/<name>_trace.json,
+    tools/trace_summary.py: the probe's warm-up launches dropped), for
+    comparison with this run's HIP-event average."""
+    for d in PROFILES:
+        f = os.path.join(d, f"{name}_trace.json")
+        if os.path.exists(f):
+            with open(f) as fh:
+                tj = json.load(fh)
+            return {"rocprof_steady_mean_ms": round(tj["steady_mean_ns"] * 1e-6, 4),
+                    "rocprof_steady_median_ms": round(tj["steady_median_ns"] * 1e-6, 4),
+                    "source": os.path.relpath(f, ROOT)}
+    return None
 
 
 def roofline_sweep(Sector, make_config):
@@ -591,7 +608,8 @@ def main():
                     "ms_per_launch": round(ms28, 4), "bytes_per_launch": Bown,
                     "csr_equivalent_bytes": Bcsr,
                     "csr_equivalent_gbs": round(Bcsr / (ms28 * 1e-3) / 1e9, 1),
-                    "physical_gbs": round(traffic / (ms28 * 1e-3) / 1e9, 1) if traffic else None}
+                    "physical_gbs": round(traffic / (ms28 * 1e-3) / 1e9, 1) if traffic else None,
+                    "profile": _profile_ms("spmv_n28")}
             dimk, _, msk = measure_hxv(Sector, cfg28, (7, 7), 50, path=2)
             Bk = 16 * dimk
             tk, tksrc = _traffic("kron_n28_traffic.json")
@@ -600,6 +618,7 @@ def main():
                     "frac": round(Bk / (msk * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                     "traffic": tk, "traffic_source": tksrc,
                     "physical_gbs": round(tk / (msk * 1e-3) / 1e9, 1) if tk else None,
+                    "profile": _profile_ms("kron_n28"),
                     "two_pass_bytes": 40 * dimk,
                     "two_pass_gbs": round(40 * dimk / (msk * 1e-3) / 1e9, 1),
                     "basis": "SURVEY §8(d) direct: 16*dim real (read v, write Hv); two_pass_bytes = 40*dim, "
@@ -614,7 +633,7 @@ def main():
                                       "frac_16dim": round(Bk / (msd * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                                       "own_bytes": 24 * dimk,  # v read, Hv written, diagonal vector read
                                       "frac_own": round(24 * dimk / (msd * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                                      "traffic": td, "traffic_source": tdsrc}
+                                      "traffic": td, "traffic_source": tdsrc, "profile": _profile_ms("direct_n28")}
             infc = {}
             _, _, msc = measure_hxv(Sector, cfg28, (7, 7), 20, path=0, info=infc, cplx=True)
             Bc = spmv_bytes_packed_complex(infc["padded"], dim28)
@@ -624,7 +643,7 @@ def main():
                                "frac": round(Bc / (msc * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                                "csr_equivalent_gbs": round((20 * nnz28 + 8 * (dim28 + 1) + 32 * dim28)
                                                            / (msc * 1e-3) / 1e9, 1),
-                               "traffic": tc, "traffic_source": tcsrc,
+                               "traffic": tc, "traffic_source": tcsrc, "profile": _profile_ms("spmv_cplx_n28"),
                                "kernel": f"k_spmv_pk<complex> ({infc['npdict']}-value dictionary of (re, im) "
                                          "pairs; the reference's complex(8) arithmetic)",
                                "achieved_basis": "4*padded + 8*(nslice+1) + 16*dim (diagonal) + 32*dim (v, Hv)"}
