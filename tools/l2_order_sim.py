@@ -10,8 +10,11 @@ order, reverse Cuthill-McKee, a greedy cache-aware order, a partition by three
 bath bits, and the lower bound (distinct rows each XCD must touch at least
 once).  One fetch per row per XCD is the best any one-pass order can do.
 
-    python tools/l2_order_sim.py > profiles/r3/stored_l2_order_sim.txt
+    python tools/l2_order_sim.py [--vbytes 8|16] > profiles/r4/stored_l2_order_sim_{real,complex}.txt
+
+--vbytes 16: complex(8) vectors — a V row is 54 KB, the 4 MiB L2 holds ~75.
 """
+import argparse
 import collections
 
 import numpy as np
@@ -64,7 +67,11 @@ def distinct(parts):
     return sum(len({r for b in p for r in [b] + nbr[b]}) for p in parts)
 
 
-W = 150
+ap = argparse.ArgumentParser()
+ap.add_argument("--vbytes", type=int, default=8)
+args = ap.parse_args()
+ROWB = NB * args.vbytes               # bytes of one V row
+W = (4 << 20) // ROWB                 # rows one XCD's L2 holds
 ident = np.arange(NB)
 A = csr_matrix((np.ones(7 * NB), ([i for i in range(NB) for _ in nbr[i]], [j for l in nbr for j in l])),
                shape=(NB, NB))
@@ -74,8 +81,10 @@ cls = collections.defaultdict(list)
 for i, p in enumerate(pats):
     cls[(p >> 11) & 7].append(i)
 cls_parts = [cls[k] for k in range(8)]
-print(f"V rows: {NB} (one row = 27 KB); L2 model: {W} rows per XCD; 8 XCDs")
-print(f"rank order (k_spmv_pk):        {fetches(rank_parts, W):6d} row fetches")
+print(f"V rows: {NB} (one row = {ROWB / 1024:.0f} KB, {args.vbytes}-B elements); L2 model: {W} rows per XCD; 8 XCDs")
+fr = fetches(rank_parts, W)
+print(f"rank order (k_spmv_pk):        {fr:6d} row fetches = {fr / NB:.2f} reads of v, "
+      f"excess {(fr - NB) * ROWB / 1e9:.3f} GB")
 print(f"reverse Cuthill-McKee:         {fetches(np.array_split(rcm, 8), W):6d}")
 print(f"rank parts, greedy order:      {fetches([greedy(list(p), W) for p in rank_parts], W):6d}")
 print(f"3-bath-bit parts, greedy:      {fetches([greedy(p, W) for p in cls_parts], W):6d}")
