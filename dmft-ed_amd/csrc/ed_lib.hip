@@ -2046,7 +2046,6 @@ struct Trlan {
   bool solo = true;       // false (ED_OPT_TRLAN_NOSOLO): multi-kernel CGS on small sectors too (A/B)
   bool locupd = true;     // false (ED_OPT_TRLAN_FULLUPD): full CGS update every step (A/B)
   int* lof = nullptr;     // device: the current step's update was local-only
-  unsigned int* fold_cnt = nullptr;  // device: k_cgs last-block fold counter (zero between passes), or null
   double *Y = nullptr, *npart = nullptr, *alpha = nullptr, *beta = nullptr;
   double *npA = nullptr, *npB = nullptr;  // |w|^2 partials before / after the first CGS pass (DGKS)
   // persistent sweep (k_trl_sweep): grid, ping-pong residuals, barrier words
@@ -2074,11 +2073,11 @@ struct Trlan {
   // one fused sweep (k_cgs) with the column group rounded up to 8/16/24/32
   bool cgs(int ncol, const double2* hin, V* x, double2* pt, double* np, const double2* pin = nullptr,
            int add = 0, const double* dgA = nullptr, const double* dgB = nullptr, int* lf = nullptr,
-           const double* locA = nullptr, const CgsFold& fold = CgsFold{}) {
+           const double* locA = nullptr) {
     const int nc = (ncol + 7) / 8 * 8;
 #define ED_CGS(NCV) \
   hipLaunchKernelGGL((k_cgs<VC, NCV>), dim3(G), dim3(kBlock), 0, st, Vb, ncol, hin, x, dim, pt, np, pin, G, \
-                     coef, add, dgA, dgB, lf, locA, fold)
+                     coef, add, dgA, dgB, lf, locA)
     if (nc <= 8) ED_CGS(8);
     else if (nc <= 16) ED_CGS(16);
     else if (nc <= 24) ED_CGS(24);
@@ -2110,9 +2109,7 @@ struct Trlan {
     }
     // fused CGS: dots + |x|^2 | x -= V h1, dots, |x'|^2 | (DGKS: only if
     // |x'| <= 0.717 |x|) x -= V h2, |x''|^2 — V streamed 2x or 3x
-    unsigned int* const fcnt = (G > kFinFoldG) ? fold_cnt : nullptr;
-    if (fused && ncol > 0 && cgs(ncol, nullptr, x, part, npA, nullptr, 0, nullptr, nullptr, nullptr, nullptr,
-                                 CgsFold{fcnt, h, coef, 0, nullptr})) {
+    if (fused && ncol > 0 && cgs(ncol, nullptr, x, part, npA)) {
       // shifted steps: the update may be local-only (cgs_loc_only, decided
       // by the first update pass from the dots and recorded in *lof)
       int* const lf = (shifted && locupd) ? lof : nullptr;
@@ -2122,13 +2119,6 @@ struct Trlan {
         // its partials (k_vdot_fin folded in: 5 launches per step, not 7)
         cgs(ncol, nullptr, x, part2, npB, part, 0, nullptr, nullptr, lf, la);
         cgs(ncol, nullptr, x, nullptr, npart, part2, 1, npA, npB, lf);
-      } else if (fcnt) {
-        // large grids: the last block of each pass folds its coefficients
-        // (cgs_fold_last; ED_OPT_TRLAN_VDOTFIN: the separate k_vdot_fin, A/B).
-        // Pass A's fold ran in the launch above (fold armed there).
-        CgsFold f2{fcnt, h, coef, 1, npA};
-        cgs(ncol, h, x, part2, npB, nullptr, 0, nullptr, nullptr, lf, la, f2);
-        cgs(ncol, h, x, nullptr, npart, nullptr, 0, npA, npB, lf);
       } else {
         hipLaunchKernelGGL(k_vdot_fin<VC>, dim3(ncol), dim3(kBlock), 0, st, part, G, h, coef, 0,
                            (const double*)nullptr, (const double*)nullptr);
@@ -2560,10 +2550,6 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
   CK(T.alloc((void**)&T.npA, (size_t)T.G * sizeof(double)));
   CK(T.alloc((void**)&T.npB, (size_t)T.G * sizeof(double)));
   CK(T.alloc((void**)&T.lof, sizeof(int)));
-  if (!(s->opts & ED_OPT_TRLAN_VDOTFIN)) {
-    CK(T.alloc((void**)&T.fold_cnt, sizeof(unsigned int)));
-    HIPCK(hipMemsetAsync(T.fold_cnt, 0, sizeof(unsigned int), T.st));
-  }
   CK(T.alloc((void**)&T.alpha, (kTrlanMaxCols + 8) * sizeof(double)));
   CK(T.alloc((void**)&T.beta, (kTrlanMaxCols + 8) * sizeof(double)));
   CK(T.alloc((void**)&T.Y, (size_t)mcap * mcap * sizeof(double)));
@@ -2839,7 +2825,7 @@ int ed_sector_destroy(ed_sector* s) {
 static constexpr int32_t kOptKnown =
     ED_OPT_NO_PERSIST | ED_OPT_PERSIST_STORED | ED_OPT_NO_PREG | ED_OPT_NO_PKRON | ED_OPT_FUSED_STEP |
     ED_OPT_SPLIT_SIMPLE | ED_OPT_NO_BATCH | ED_OPT_EIGH_NO_VERIFY | ED_OPT_TRLAN_UNFUSED | ED_OPT_TRLAN_NOFOLD |
-    ED_OPT_TRLAN_PSWEEP | ED_OPT_NO_GRAPH | ED_OPT_TRLAN_NOLOCAL | ED_OPT_TRLAN_NOSOLO | ED_OPT_TRLAN_FULLUPD | ED_OPT_TRLAN_VDOTFIN |
+    ED_OPT_TRLAN_PSWEEP | ED_OPT_NO_GRAPH | ED_OPT_TRLAN_NOLOCAL | ED_OPT_TRLAN_NOSOLO | ED_OPT_TRLAN_FULLUPD |
     ED_OPT_PKRON_C1024 | ED_OPT_TRLAN_G128 | ED_OPT_EIGH_FULLPROBE;
 
 int ed_sector_set_options(ed_sector* s, int32_t opts) {

@@ -285,59 +285,6 @@ __global__ void __launch_bounds__(kBlock) k_coef_scale(const double* __restrict_
     out[i] = scl(inv, x[i]);
 }
 
-// Coefficient fold by the last workgroup of a k_cgs pass (large grids, where
-// folding into the next pass would make every block re-read G x ncol
-// partials): each block publishes its partials (stores drained, agent
-// release, relaxed counter add — MI355X_MICROARCH.md "Valid forms", producer
-// row); the block whose add completes the count acquires and sums them in a
-// fixed order (wave c mod NW, lanes strided, DPP sum — the folded small-grid
-// order), writes h and coef as k_vdot_fin did (dgA: skipped when the DGKS
-// test says the pass's update was not needed) and re-arms the counter.  One
-// launch per pass instead of two.
-struct CgsFold {
-  unsigned int* cnt = nullptr;  // zero between passes
-  double2* h = nullptr;
-  double2* coef = nullptr;
-  int add = 0;
-  const double* dgA = nullptr;  // |w|^2 partials before this pass (DGKS), or null
-};
-
-template <bool VC>
-__device__ __forceinline__ void cgs_fold_last(const CgsFold& f, const double2* __restrict__ part,
-                                              const double* __restrict__ npart, int ncol) {
-  __shared__ int last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial stores drained
-  __syncthreads();                                   // ... and every other wave's
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned int prev = __hip_atomic_fetch_add(f.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = prev == gridDim.x - 1;
-    if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  if (!last) return;
-  const int G = gridDim.x;
-  if (threadIdx.x == 0) __hip_atomic_store(f.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (f.dgA && dgks_skip(f.dgA, npart, G)) return;
-  constexpr int NW = kBlock / 64;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int c = wv; c < ncol; c += NW) {  // wave-uniform
-    double re = 0.0, im = 0.0;
-    for (int b = lane; b < G; b += 64) {
-      re += part[(int64_t)c * G + b].x;
-      if constexpr (VC) im += part[(int64_t)c * G + b].y;
-    }
-    re = wave_sum_dpp(re);
-    if constexpr (VC) im = wave_sum_dpp(im);
-    if (lane == 63) {
-      f.h[c] = make_double2(re, im);
-      f.coef[c] = f.add ? make_double2(f.coef[c].x + re, f.coef[c].y + im) : make_double2(re, im);
-    }
-  }
-}
-
 // Fused CGS sweep over the rows of x (one column group of up to NC columns
 // held in registers per row):
 //   hin != nullptr : x_i -= sum_{c<ncol} V_c,i hin_c   (written back)
@@ -354,8 +301,7 @@ __global__ void __launch_bounds__(kBlock) k_cgs(const val_t<VC>* __restrict__ V,
                                                 const double2* __restrict__ pin = nullptr, int gin = 0,
                                                 double2* __restrict__ coef = nullptr, int add = 0,
                                                 const double* dgA = nullptr, const double* dgB = nullptr,
-                                                int* lof = nullptr, const double* locA = nullptr,
-                                                const CgsFold fold = CgsFold{}) {
+                                                int* lof = nullptr, const double* locA = nullptr) {
   constexpr int NW = kBlock / 64;
   constexpr int NR = (VC ? 2 * NC : NC) + 1;  // partial slots per wave
   __shared__ double2 hs[NC];
@@ -473,7 +419,6 @@ __global__ void __launch_bounds__(kBlock) k_cgs(const val_t<VC>* __restrict__ V,
     for (int w = 0; w < NW; w++) r = r + red[w][NR - 1];
     npart[blockIdx.x] = r;
   }
-  if (fold.cnt) cgs_fold_last<VC>(fold, part, npart, ncol);
 }
 
 // ------------------------------------------------------------------------
