@@ -1636,8 +1636,7 @@ static int persist_mode(ed_sector* s, int vc, int path) {
 static int64_t persist_lds(const ed_sector* s, int vc, int mode) {
   const int64_t vs = vc ? 16 : 8, vr = persist_vrows(s, mode, vc);
   int64_t lds = ((vr * vs + 15) & ~(int64_t)15);
-  // (complex: + 16, the 512-thread form's gap between its two vector planes)
-  if (mode == 4) return lds + (vc ? 16 + vr * 8 + (int64_t)s->pkr_E * (s->pkr_dd + s->pkr_du) * 8 : 0);
+  if (mode == 4) return lds + (vc ? vr * 8 + (int64_t)s->pkr_E * (s->pkr_dd + s->pkr_du) * 8 : 0);
   if (mode == 2) {
     const int64_t hs = s->hc ? 16 : 8;
     return lds + ((vr * 8 + 15) & ~(int64_t)15) + (((int64_t)s->ndict * hs + 15) & ~(int64_t)15);

@@ -277,20 +277,6 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
   // p = v_{k-1} in global memory)
   constexpr bool KRV = KR && VC && NT == kPBlock;
   constexpr bool KRC = KR && VC && NT != kPBlock;
-  // KRC keeps the vector as two planes (real parts, then imaginary parts,
-  // 8 B per row each): a gather is two ds_read_b64 at one address and an
-  // immediate plane offset, banked in 32-lane halves like the real kernel —
-  // the up-hop slot order (pkr_order_up) is then conflict-optimal for it
-  // too, where the interleaved 16-B rows' ds_read_b128 lane groups saw about
-  // twice the ideal cycles on the up-hop gathers
-  // (the imaginary plane starts 8 B past the real one's end: an offset that
-  // is neither a multiple of 512 nor below 2 KiB, so the two reads are not
-  // merged into one ds_read2st64_b64 — 8 LDS cycles where two ds_read_b64
-  // take 4)
-  constexpr bool SPL = KRC;
-  constexpr int VSZ = SPL ? 8 : (int)sizeof(V);  // LDS bytes per row and plane
-  constexpr int kImOff = VROWS * 8 + 8;          // SPL: imaginary plane offset
-  static_assert(!SPL || kImOff < 65536, "plane offset must fit a ds_read offset");
   int ucol[KR ? E : 1];
   double uval[(KR && !KRV) ? E : 1];
   int dcol[KR ? RPT * E : 1];
@@ -308,7 +294,7 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
     if constexpr (KR && VC) {
       // LDS: vector | diagonal | down-hop values | up-hop values (KRC reads
       // only the down-hop values)
-      double* tg = (double*)(smem + (((int64_t)VROWS * sizeof(V) + (SPL ? 8 : 0) + 15) & ~(int64_t)15));
+      double* tg = (double*)(smem + (((int64_t)VROWS * sizeof(V) + 15) & ~(int64_t)15));
       for (int x = tid; x < VROWS; x += NT) {
         double d = 0.0;
         if (x < dim) {
@@ -333,7 +319,7 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
 #pragma unroll
     for (int e = 0; e < E; e++) {
       const bool ok = act && e < a.kdegu;
-      ucol[e] = ok ? a.kupc[e * du + q.iu] * VSZ : 0;
+      ucol[e] = ok ? a.kupc[e * du + q.iu] * (int)sizeof(V) : 0;
       if constexpr (!KRV) uval[e] = ok ? a.kupv[e * du + q.iu] : 0.0;
     }
 #pragma unroll
@@ -346,7 +332,7 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
         if constexpr (KR && VC) {
           // padding slots gather the row's own (zero) padding entry, valid
           // rows beyond their degree a zero table value
-          dcol[r * E + e] = (ok ? a.kdwc[e * dd + iw] * du + q.iu : (okr ? 0 : PROW(r))) * VSZ;
+          dcol[r * E + e] = (ok ? a.kdwc[e * dd + iw] * du + q.iu : (okr ? 0 : PROW(r))) * (int)sizeof(V);
         } else {
           dcol[r * E + e] = (ok ? a.kdwc[e * dd + iw] * du + q.iu : 0) * (int)sizeof(V);
           dval[r * E + e] = ok ? a.kdwv[e * dd + iw] : 0.0;
@@ -366,28 +352,6 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
       }
     }
   }
-
-  // LDS vector access by row and by byte offset (VSZ bytes per row)
-  auto vget_b = [&](const unsigned char* pb) -> V {
-    if constexpr (SPL) {
-      V r;
-      r.x = *(const double*)pb;
-      r.y = *(const double*)(pb + kImOff);
-      return r;
-    } else {
-      return *(const V*)pb;
-    }
-  };
-  auto vget = [&](int i) -> V { return vget_b((const unsigned char*)vl + i * VSZ); };
-  auto vset = [&](int i, V x) {
-    if constexpr (SPL) {
-      double* pb = (double*)((unsigned char*)vl + i * 8);
-      pb[0] = re_of(x);
-      pb[kImOff / 8] = x.y;
-    } else {
-      vl[i] = x;
-    }
-  };
 
   // --- state in
   // complex vectors in register modes keep p = v_{k-1} in global memory (own
@@ -414,7 +378,7 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
       const bool ok = r < q.nvalid;
       const V x = ok ? Rg[i] : vzero<V>();
       if constexpr (UREG) u[r] = x;
-      vset(i, x);
+      vl[i] = x;
       if constexpr (!PG) p[r] = (ok && !a.first) ? Pg[i] : vzero<V>();
       if (a.first) {
         nrm += redot(x, x);
@@ -517,7 +481,7 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
 #pragma unroll
     for (int r = 0; r < RPT; r++) {
       const int i = PROW(r);
-      const V ur = UREG ? u[r] : vget(i);
+      const V ur = UREG ? u[r] : vl[i];
       V acc;
       if constexpr (MODE == 0) {
         acc = vzero<V>();
@@ -552,20 +516,20 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
         if constexpr (KRV) acc = mul(sdg[i], ur);
         else acc = mul(dgr[r], ur);
         {
-        const unsigned char* rb = (const unsigned char*)vl + (i - q.iu) * VSZ;  // row iw of V
+        const unsigned char* rb = (const unsigned char*)(vl + (i - q.iu));  // row iw of V
         if constexpr (KRV) {
           // idle lanes (tid >= G*DimUp) read table column 0 with ucol = 0: their row base is a zero padding row
 #pragma unroll
           for (int e = 0; e < E; e++) acc = fmac(acc, suv[e * a.kdu + q.iu], *(const V*)(rb + ucol[e]));
         } else {
 #pragma unroll
-          for (int e = 0; e < E; e++) acc = fmac(acc, uval[e], vget_b(rb + ucol[e]));
+          for (int e = 0; e < E; e++) acc = fmac(acc, uval[e], *(const V*)(rb + ucol[e]));
         }
         if constexpr (KR && VC) {
           const int iwc = min(giw + (NT / a.kdu) * r, a.kdd - 1);
 #pragma unroll
           for (int e = 0; e < E; e++)
-            acc = fmac(acc, sdv[e * a.kdd + iwc], vget_b((const unsigned char*)vl + dcol[r * E + e]));
+            acc = fmac(acc, sdv[e * a.kdd + iwc], *(const V*)((const unsigned char*)vl + dcol[r * E + e]));
         } else {
 #pragma unroll
           for (int e = 0; e < E; e++)
@@ -611,12 +575,12 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
     if (basis) {  // uniform: no per-row EXEC masking when no basis is kept
 #pragma unroll
       for (int r = 0; r < RPT; r++)
-        if (r < q.nvalid) basis[(int64_t)it * dim + PROW(r)] = scl(s, UREG ? u[r] : vget(PROW(r)));  // column k = v_k
+        if (r < q.nvalid) basis[(int64_t)it * dim + PROW(r)] = scl(s, UREG ? u[r] : vl[PROW(r)]);  // column k = v_k
     }
 #pragma unroll
     for (int r = 0; r < RPT; r++) {
       const int i = PROW(r);
-      const V x = scl(s, UREG ? u[r] : vget(i));
+      const V x = scl(s, UREG ? u[r] : vl[i]);
       if constexpr (PIPE) {
         w[r] = fma(-alpha, x, w[r]);
         bp = fma(w[r], w[r], bp);
@@ -630,7 +594,7 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
         p[r] = x;
       }
       if constexpr (UREG) u[r] = w[r];
-      vset(i, w[r]);
+      vl[i] = w[r];
     }
     // beta barrier: also publishes r_{k+1}
 #ifdef ED_P4_NOBETA  // timing probe: the step without the beta reduction (a bare barrier)
@@ -658,7 +622,7 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
 #pragma unroll
   for (int r = 0; r < RPT; r++) {
     if (r < q.nvalid) {
-      Rg[PROW(r)] = UREG ? u[r] : vget(PROW(r));
+      Rg[PROW(r)] = UREG ? u[r] : vl[PROW(r)];
       if constexpr (!PG) Pg[PROW(r)] = p[r];
     }
   }
