@@ -420,6 +420,79 @@ def roofline_sweep(Sector, make_config):
     return out
 
 
+def bench_roofline(Sector, make_config):
+    """The roofline entries (rank 0, run before the farm sections so the
+    timed kernels see the same clean device a lone probe run sees): stored
+    real(8) H·v on the Nlevels=28 (7,7) sector (`roofline`), complex(8)
+    stored, two-pass matrix-free, generic matrix-free and SURVEY §8(d)'s
+    sweep (`kron_n28`, `roofline.sweep`)."""
+    from golden.golden_configs import SEED
+
+    cfg28 = make_config(Norb=1, Nbath=13, bath="random", seed=SEED)
+    inf28 = {}
+    dim28, nnz28, ms28 = measure_hxv(Sector, cfg28, (7, 7), 50, path=0, info=inf28)
+    # frac on the bytes the timed kernel moves (its own format: 4-B
+    # {col|value index} words when packed); SURVEY §8(d)'s CSR-equivalent
+    # rate is reported beside it and can exceed the physical rate
+    Bcsr = spmv_bytes_real(nnz28, dim28)
+    Bown = spmv_bytes_packed(inf28["padded"], dim28) if inf28["packed"] else Bcsr
+    ach = Bown / (ms28 * 1e-3) / 1e9
+    traffic, tsrc = _traffic("spmv_n28_traffic.json")
+    roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
+            "achieved_basis": ("bytes the timed kernel moves: 4*padded slots + 8*(nslice+1) + 8*dim "
+                               "(diagonal) + 16*dim (read v, write Hv)") if inf28["packed"]
+                              else "12*nnz + 8*(dim+1) + 16*dim",
+            "kernel": ("k_spmv_pk<real> (stored SELL-64, 32-bit {col|value index} words, "
+                       f"{inf28['npdict']}-value dictionary)") if inf28["packed"]
+                      else "k_spmv<real,real> (stored SELL-64 H·v)",
+            "workload": f"Nlevels=28 Norb=1 Nbath=13 (7,7) sector, dim {dim28}, nnz {nnz28}, real(8)",
+            "ms_per_launch": round(ms28, 4), "bytes_per_launch": Bown,
+            "csr_equivalent_bytes": Bcsr,
+            "csr_equivalent_gbs": round(Bcsr / (ms28 * 1e-3) / 1e9, 1),
+            "physical_gbs": round(traffic / (ms28 * 1e-3) / 1e9, 1) if traffic else None,
+            "profile": _profile_ms("spmv_n28")}
+    dimk, _, msk = measure_hxv(Sector, cfg28, (7, 7), 50, path=2)
+    Bk = 16 * dimk
+    tk, tksrc = _traffic("kron_n28_traffic.json")
+    kron = {"ms_per_hxv": round(msk, 4), "algorithmic_bytes": Bk,
+            "achieved_gbs": round(Bk / (msk * 1e-3) / 1e9, 1),
+            "frac": round(Bk / (msk * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "traffic": tk, "traffic_source": tksrc,
+            "physical_gbs": round(tk / (msk * 1e-3) / 1e9, 1) if tk else None,
+            "profile": _profile_ms("kron_n28"),
+            "two_pass_bytes": 40 * dimk,
+            "two_pass_gbs": round(40 * dimk / (msk * 1e-3) / 1e9, 1),
+            "basis": "SURVEY §8(d) direct: 16*dim real (read v, write Hv); two_pass_bytes = 40*dim, "
+                     "the least a two-pass form moves (pass U reads V, writes y; pass D reads V and "
+                     "y, writes Hv)",
+            "kernel": "k_kron_up + k_kron_dw (two-pass matrix-free Kronecker H·v)"}
+    # generic matrix-free (any ed_mode) and complex(8) stored H·v on the same sector
+    _, _, msd = measure_hxv(Sector, cfg28, (7, 7), 20, path=1)
+    td, tdsrc = _traffic("direct_n28_traffic.json")
+    kron["direct_generic"] = {"ms_per_hxv": round(msd, 4),
+                              "kernel": "k_direct (wave per 64-row chunk, op lists, LDS rank tables, diagonal vector from k_gen_diag)",
+                              "frac_16dim": round(Bk / (msd * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                              "own_bytes": 24 * dimk,  # v read, Hv written, diagonal vector read
+                              "frac_own": round(24 * dimk / (msd * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                              "traffic": td, "traffic_source": tdsrc, "profile": _profile_ms("direct_n28")}
+    infc = {}
+    _, _, msc = measure_hxv(Sector, cfg28, (7, 7), 20, path=0, info=infc, cplx=True)
+    Bc = spmv_bytes_packed_complex(infc["padded"], dim28)
+    tc, tcsrc = _traffic("spmv_cplx_n28_traffic.json")
+    roof["complex"] = {"ms_per_launch": round(msc, 4), "bytes_per_launch": Bc,
+                       "achieved": round(Bc / (msc * 1e-3) / 1e9, 1),
+                       "frac": round(Bc / (msc * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                       "csr_equivalent_gbs": round((20 * nnz28 + 8 * (dim28 + 1) + 32 * dim28)
+                                                   / (msc * 1e-3) / 1e9, 1),
+                       "traffic": tc, "traffic_source": tcsrc, "profile": _profile_ms("spmv_cplx_n28"),
+                       "kernel": f"k_spmv_pk<complex> ({infc['npdict']}-value dictionary of (re, im) "
+                                 "pairs; the reference's complex(8) arithmetic)",
+                       "achieved_basis": "4*padded + 8*(nslice+1) + 16*dim (diagonal) + 32*dim (v, Hv)"}
+    roof["sweep"] = roofline_sweep(Sector, make_config)
+    return roof, kron
+
+
 def spawn_ranks(n, argv):
     """`--gpus N` without an external launcher: start N ranks (one process per
     GPU) with torch.distributed.run as a CHILD process and return its exit
@@ -584,6 +657,7 @@ def main():
         direct_ips, _ = _lanc_rate(Sd, args.niter, v0)
         direct_mode = Sd.lanc_mode(real=True, path=2)
 
+    roof_kron = (None, None) if (args.no_roofline or rank != 0) else bench_roofline(Sector, make_config)
     split = None if args.no_farm else bench_split(dist, world, dev)
     farm = None if args.no_farm else bench_farm(dist, world, dev)
     nonsu2 = None if args.no_farm else bench_nonsu2(dist, world, dev)
@@ -595,70 +669,7 @@ def main():
         gbs2 = spmv_bytes_real(nnz2, dim2) / (ms2 * 1e-3) / 1e9
         batched = bench_batched(S, v0, args.niter, np.asarray(last[0]))
         batched_c = bench_batched(S, vc, args.niter, np.asarray(ac), cplx=True)
-        roof, kron = None, None
-        if not args.no_roofline:
-            cfg28 = make_config(Norb=1, Nbath=13, bath="random", seed=SEED)
-            inf28 = {}
-            dim28, nnz28, ms28 = measure_hxv(Sector, cfg28, (7, 7), 50, path=0, info=inf28)
-            # frac on the bytes the timed kernel moves (its own format: 4-B
-            # {col|value index} words when packed); SURVEY §8(d)'s CSR-equivalent
-            # rate is reported beside it and can exceed the physical rate
-            Bcsr = spmv_bytes_real(nnz28, dim28)
-            Bown = spmv_bytes_packed(inf28["padded"], dim28) if inf28["packed"] else Bcsr
-            ach = Bown / (ms28 * 1e-3) / 1e9
-            traffic, tsrc = _traffic("spmv_n28_traffic.json")
-            roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
-                    "achieved_basis": ("bytes the timed kernel moves: 4*padded slots + 8*(nslice+1) + 8*dim "
-                                       "(diagonal) + 16*dim (read v, write Hv)") if inf28["packed"]
-                                      else "12*nnz + 8*(dim+1) + 16*dim",
-                    "kernel": ("k_spmv_pk<real> (stored SELL-64, 32-bit {col|value index} words, "
-                               f"{inf28['npdict']}-value dictionary)") if inf28["packed"]
-                              else "k_spmv<real,real> (stored SELL-64 H·v)",
-                    "workload": f"Nlevels=28 Norb=1 Nbath=13 (7,7) sector, dim {dim28}, nnz {nnz28}, real(8)",
-                    "ms_per_launch": round(ms28, 4), "bytes_per_launch": Bown,
-                    "csr_equivalent_bytes": Bcsr,
-                    "csr_equivalent_gbs": round(Bcsr / (ms28 * 1e-3) / 1e9, 1),
-                    "physical_gbs": round(traffic / (ms28 * 1e-3) / 1e9, 1) if traffic else None,
-                    "profile": _profile_ms("spmv_n28")}
-            dimk, _, msk = measure_hxv(Sector, cfg28, (7, 7), 50, path=2)
-            Bk = 16 * dimk
-            tk, tksrc = _traffic("kron_n28_traffic.json")
-            kron = {"ms_per_hxv": round(msk, 4), "algorithmic_bytes": Bk,
-                    "achieved_gbs": round(Bk / (msk * 1e-3) / 1e9, 1),
-                    "frac": round(Bk / (msk * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                    "traffic": tk, "traffic_source": tksrc,
-                    "physical_gbs": round(tk / (msk * 1e-3) / 1e9, 1) if tk else None,
-                    "profile": _profile_ms("kron_n28"),
-                    "two_pass_bytes": 40 * dimk,
-                    "two_pass_gbs": round(40 * dimk / (msk * 1e-3) / 1e9, 1),
-                    "basis": "SURVEY §8(d) direct: 16*dim real (read v, write Hv); two_pass_bytes = 40*dim, "
-                             "the least a two-pass form moves (pass U reads V, writes y; pass D reads V and "
-                             "y, writes Hv)",
-                    "kernel": "k_kron_up + k_kron_dw (two-pass matrix-free Kronecker H·v)"}
-            # generic matrix-free (any ed_mode) and complex(8) stored H·v on the same sector
-            _, _, msd = measure_hxv(Sector, cfg28, (7, 7), 20, path=1)
-            td, tdsrc = _traffic("direct_n28_traffic.json")
-            kron["direct_generic"] = {"ms_per_hxv": round(msd, 4),
-                                      "kernel": "k_direct (wave per 64-row chunk, op lists, LDS rank tables, diagonal vector from k_gen_diag)",
-                                      "frac_16dim": round(Bk / (msd * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                                      "own_bytes": 24 * dimk,  # v read, Hv written, diagonal vector read
-                                      "frac_own": round(24 * dimk / (msd * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                                      "traffic": td, "traffic_source": tdsrc, "profile": _profile_ms("direct_n28")}
-            infc = {}
-            _, _, msc = measure_hxv(Sector, cfg28, (7, 7), 20, path=0, info=infc, cplx=True)
-            Bc = spmv_bytes_packed_complex(infc["padded"], dim28)
-            tc, tcsrc = _traffic("spmv_cplx_n28_traffic.json")
-            roof["complex"] = {"ms_per_launch": round(msc, 4), "bytes_per_launch": Bc,
-                               "achieved": round(Bc / (msc * 1e-3) / 1e9, 1),
-                               "frac": round(Bc / (msc * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                               "csr_equivalent_gbs": round((20 * nnz28 + 8 * (dim28 + 1) + 32 * dim28)
-                                                           / (msc * 1e-3) / 1e9, 1),
-                               "traffic": tc, "traffic_source": tcsrc, "profile": _profile_ms("spmv_cplx_n28"),
-                               "kernel": f"k_spmv_pk<complex> ({infc['npdict']}-value dictionary of (re, im) "
-                                         "pairs; the reference's complex(8) arithmetic)",
-                               "achieved_basis": "4*padded + 8*(nslice+1) + 16*dim (diagonal) + 32*dim (v, Hv)"}
-            roof["sweep"] = roofline_sweep(Sector, make_config)
+        roof, kron = roof_kron
         # the CPU baseline is a rank-0, N=1 measurement (task contract)
         cpu = None if (args.no_cpu or world > 1) else cpu_baseline()
         out = {

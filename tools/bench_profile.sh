@@ -5,23 +5,24 @@
 # (tools/trace_summary.py), so each sector's steady-state average sits beside
 # the line's HIP-event `ms_per_launch`.
 #   bash tools/bench_profile.sh TAG [bench.py arguments]
-# -> gpurun_out/bprof_TAG/ and profiles/TAG/bench_kernel_stats.csv,
-#    profiles/TAG/bench_trace_{spmv,spmv_cplx,kron,direct}.json
+# -> gpurun_out/bprof_TAG/profiles/ (merged back by gpurun; copy to
+#    profiles/TAG): bench_kernel_stats.csv, bench_trace_{spmv,spmv_cplx,kron,direct}.json
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-r4}; shift
 OUT=$R/gpurun_out/bprof_$TAG
-mkdir -p "$OUT" "$R/profiles/$TAG"
+P=$OUT/profiles
+mkdir -p "$OUT" "$P"
 ( cd /tmp && export TMPDIR=/tmp && \
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/st" -o st --output-format csv -- \
     python3 "$R/bench.py" "$@" ) > "$OUT/bench.log" 2>&1 || { echo "profiled bench failed"; tail -5 "$OUT/bench.log"; exit 1; }
 grep '^{' "$OUT/bench.log" > "$OUT/bench_line.json" || true
 t=$(find "$OUT/st" -name "*kernel_trace.csv" | head -1)
 s=$(find "$OUT/st" -name "*kernel_stats.csv" | head -1)
-[ -n "$s" ] && cp "$s" "$R/profiles/$TAG/bench_kernel_stats.csv"
+[ -n "$s" ] && cp "$s" "$P/bench_kernel_stats.csv"
 for e in "spmv|k_spmv_pk<false, false" "spmv_cplx|k_spmv_pk<true, true" "kron|k_kron_(up|dw)" "direct|k_direct<"; do
   IFS='|' read -r name pat <<< "$e"
-  python3 "$R/tools/trace_summary.py" "$t" "$pat" 5 "$R/profiles/$TAG/bench_trace_$name.json" \
+  python3 "$R/tools/trace_summary.py" "$t" "$pat" 5 "$P/bench_trace_$name.json" \
     --note "rocprofv3 of bench.py $*: per (kernel, grid) group, 5 warm-up launches dropped" \
     || { echo "trace summary $name failed"; exit 1; }
 done
