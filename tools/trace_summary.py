@@ -46,6 +46,23 @@ def main():
         groups.setdefault(f"{n[:60]} | grid {g}", []).append(d)
     by_grid = {k: {"launches": len(v), "steady_mean_ns": round(statistics.fmean(v[skip:]), 1) if v[skip:] else None}
                for k, v in groups.items()}
+    # runs: maximal stretches of consecutive dispatch ids of one (kernel,
+    # grid) — one measurement loop of one sector (sectors of equal dimension
+    # share a grid; the kernels that build the next sector break the run)
+    runs = []
+    for did, n, d, g in rows:
+        r = runs[-1] if runs else None
+        if r and r["kernel"] == n[:80] and r["grid_size_x"] == g and did == r["_last"] + 1:
+            r["_d"].append(d)
+            r["_last"] = did
+        else:
+            runs.append({"kernel": n[:80], "grid_size_x": g, "first_dispatch": did, "_last": did, "_d": [d]})
+    for r in runs:
+        dd = r.pop("_d")
+        r.pop("_last")
+        r["launches"] = len(dd)
+        r["steady_mean_ns"] = round(statistics.fmean(dd[skip:]), 1) if dd[skip:] else None
+    runs = [r for r in runs if r["launches"] > skip]
     steady = launches[skip:]
     if not steady:
         raise SystemExit("no steady-state launches")
@@ -62,6 +79,7 @@ def main():
         "steady_max_ns": max(steady),
         "all_mean_ns": round(statistics.fmean(launches), 1),
         "by_kernel_grid": by_grid,
+        "runs": runs,
         "note": note,
     }
     with open(out, "w") as fh:
