@@ -55,3 +55,41 @@ for _ in range(400):
             elif not (idw&1) and (u>>k)&1: t.append(row(idw|1, u&~(1<<k)))
         if t: tot['flip']+=len({x*8//128 for x in t}); cnt['flip']+=1
 for k in tot: print(k, "ops per chunk", round(cnt[k]/400,2), "lines per op", round(tot[k]/max(cnt[k],1),1), "lines per chunk", round(tot[k]/400,1))
+
+# ---- block order: an LRU model of each XCD's 4 MiB L2 at block granularity
+# (k_direct sweeps the blocks of its eighth of the chunks in idw order; a
+# block's gathers touch itself, its 12 spin-down and 13 spin-flip neighbours)
+import collections  # noqa: E402
+
+size = {idw: comb(NS, N - bin(idw).count('1')) * 8 if 0 <= N - bin(idw).count('1') <= NS else 0
+        for idw in range(1 << NS)}
+vbytes = sum(size.values())
+masks = [1 << k for k in range(NS)] + [1 | (1 << k) for k in range(1, NS)]
+
+
+def l2_fetch(order, cap=4 << 20, nx=8):
+    fetched = 0
+    for p in np.array_split(np.array(order), nx):
+        c, used = collections.OrderedDict(), 0
+        for b in p:
+            for r in [int(b)] + [int(b) ^ m for m in masks]:
+                if r in c:
+                    c.move_to_end(r)
+                else:
+                    fetched += size[r]
+                    c[r] = 1
+                    used += size[r]
+                    while used > cap:
+                        k, _ = c.popitem(last=False)
+                        used -= size[k]
+    return fetched
+
+
+ident = list(range(1 << NS))
+gray = [i ^ (i >> 1) for i in range(1 << NS)]
+shuf = ident[:]
+random.shuffle(shuf)
+print(f"block-order L2 model (v = {vbytes / 1e6:.1f} MB):")
+for name, o in (("idw order (k_direct)", ident), ("Gray-code sequence", gray), ("random", shuf)):
+    f = l2_fetch(o)
+    print(f"  {name:22s} {f / 1e9:.3f} GB fetched = {f / vbytes:.2f} reads of v")
