@@ -202,6 +202,8 @@ def bench_farm(dist, world, dev):
     return {"wall_s": round(dt, 4), "sectors": len(res.eigenvalues), "n_gpus": world,
             "E0": round(float(res.states.emin), 10), "gs_states": res.states.size,
             "rank0_sectors": len(res.local), "scaling": "strong",
+            "schedule": (f"{opt.farm_schedule} over {world} ranks" if world > 1 else "one rank") +
+                        f", {opt.workers} worker threads per GPU",
             "parity": {"fixture": "tests/golden/c4_diag_random.json", "E0_rel_dev": e0_dev,
                        "worst_eigenvalue_dev_rel_E0": worst, "bar": 1e-10},
             "workload": "configs[3]: Norb=2 Nbath=5 Uloc=(2,2,0) Ust=1 Jh=0.5 random bath, all 169 sectors, "

@@ -63,6 +63,11 @@ class DiagOptions:
     # Cache instead of evicting each other to HBM; a sector larger than the
     # budget runs when nothing else big is in flight.  0: no limit.
     cache_budget_mb: float = 0.0
+    # multi-rank farms: "dynamic" — every rank's workers take the next sector
+    # (largest cost first) from one global counter in the process group's
+    # key-value store, so the ranks finish together whatever the cost
+    # model's error; "lpt" — the static longest-processing-time partition
+    farm_schedule: str = "dynamic"
 
 
 @dataclass
@@ -208,17 +213,45 @@ def working_set_bytes(cfg: EDConfig, sec: SectorId, opt: DiagOptions) -> float:
 
 
 def solve_many(cfg: EDConfig, secs: List[SectorId], opt: DiagOptions, device: int = 0,
-               solver=None, cost=None) -> List[SectorResult]:
+               solver=None, cost=None, take_global=None) -> List[SectorResult]:
     """Solve a list of sectors on one GPU with `opt.workers` host threads,
     largest first; results in the order of `secs` (each sector's result does
     not depend on the schedule).  With `opt.cache_budget_mb` a worker takes
     the largest pending sector whose working set fits beside those in flight
     (a sector larger than the budget only when nothing else big runs), else
-    waits for one to finish."""
+    waits for one to finish.
+
+    take_global: the farm's multi-rank work queue — a callable returning the
+    next index into `secs` (already in schedule order) or None; the result
+    list then holds the sectors this process solved, None elsewhere."""
     solver = solver or solve_sector
+    import threading
+
+    if take_global is not None:
+        out_g: List[Optional[SectorResult]] = [None] * len(secs)
+        errs: List[BaseException] = []
+
+        def gworker():
+            while not errs:
+                i = take_global()
+                if i is None:
+                    return
+                try:
+                    out_g[i] = solver(cfg, secs[i], opt, device)
+                except BaseException as e:  # noqa: BLE001 - re-raised below
+                    errs.append(e)
+                    return
+
+        ths = [threading.Thread(target=gworker, daemon=True) for _ in range(max(1, min(opt.workers, len(secs))))]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        if errs:
+            raise errs[0]
+        return out_g
     if opt.workers <= 1 or len(secs) <= 1:
         return [solver(cfg, sec, opt, device) for sec in secs]
-    import threading
 
     order = sorted(range(len(secs)), key=lambda i: -(cost(secs[i]) if cost else secs[i].dim))
     budget = opt.cache_budget_mb * 1e6

@@ -5,7 +5,12 @@ across MPI ranks, with an MPI_Allgatherv of the whole vector on every H·v
 (ED_HAMILTONIAN_STORED_HxV.f90:147-197).  Sectors are independent
 (ED_DIAG.f90:71-249), so here whole sectors go to ranks instead:
 
-  * longest-processing-time partition by an H·v cost model (dim x elements/row);
+  * a dynamic schedule (default at N > 1): every rank's worker threads take
+    the next sector, largest modelled cost first, from one global counter in
+    the process group's key-value store (an atomic add per sector — no
+    collective, no data), so the ranks finish together even where the cost
+    model is off; or the static longest-processing-time partition by that
+    model (`DiagOptions.farm_schedule = "lpt"`);
   * each rank diagonalises its sectors on its own GPU — no collective in the
     data path;
   * one all_gather of the per-sector eigenvalues (KB), after which every rank
@@ -95,12 +100,22 @@ def farm_diag(cfg: EDConfig, opt: Optional[DiagOptions] = None, *, device: int =
     rank = dist.get_rank() if dist else 0
     world = dist.get_world_size() if dist else 1
     secs = [s for s in diag_sectors(cfg) if sectors is None or s.isector in set(sectors)]
-    parts = lpt_partition([sector_cost(cfg, s, opt) for s in secs], world)
-    assignment = [[secs[i].isector for i in p] for p in parts]
+    costs = [sector_cost(cfg, s, opt) for s in secs]
     local: Dict[int, SectorResult] = {}
-    mine = [secs[i] for i in parts[rank]]
-    for r in solve_many(cfg, mine, opt, device, solver=solver, cost=lambda s: sector_cost(cfg, s, opt)):
-        local[r.isector] = r
+    if dist and world > 1 and opt.farm_schedule == "dynamic":
+        order = sorted(range(len(secs)), key=lambda i: (-costs[i], i))   # the same on every rank
+        qsecs = [secs[i] for i in order]
+        take = _global_queue(dist, len(qsecs))
+        for r in solve_many(cfg, qsecs, opt, device, solver=solver, take_global=take):
+            if r is not None:
+                local[r.isector] = r
+        assignment = None   # from the gathered tables below
+    else:
+        parts = lpt_partition(costs, world)
+        assignment = [[secs[i].isector for i in p] for p in parts]
+        mine = [secs[i] for i in parts[rank]]
+        for r in solve_many(cfg, mine, opt, device, solver=solver, cost=lambda s: sector_cost(cfg, s, opt)):
+            local[r.isector] = r
     # gather eigenvalues (tiny) from every rank
     mine = {k: (v.q, v.dim, v.neigen, np.asarray(v.eigenvalues[: max(v.neigen, 1)])) for k, v in local.items()}
     if dist:
@@ -114,6 +129,8 @@ def farm_diag(cfg: EDConfig, opt: Optional[DiagOptions] = None, *, device: int =
         for k, v in t.items():
             merged[k] = v
             owner_of[k] = rk
+    if assignment is None:
+        assignment = [sorted(k for k, o in owner_of.items() if o == r) for r in range(world)]
     shadows = []
     for k, (q, dim, neigen, ev) in merged.items():
         loc = local.get(k)
@@ -122,6 +139,39 @@ def farm_diag(cfg: EDConfig, opt: Optional[DiagOptions] = None, *, device: int =
     owners = [owner_of[s] for s in states.sectors]
     tables = {k: v[3] for k, v in merged.items()}
     return FarmResult(states, owners, tables, local, assignment)
+
+
+_QUEUE_CALLS = [0]
+
+
+def _global_queue(dist, n: int):
+    """Work queue over the ranks of the default group: `take()` returns the
+    next of n indices (0, 1, ...) or None.  One counter key per farm call
+    (every rank makes the same sequence of farm_diag calls, so the keys
+    agree); the store's add is atomic, each index goes to exactly one taker.
+    A barrier first, so no rank takes from the counter of a call the others
+    have not reached."""
+    import threading
+
+    from torch.distributed import distributed_c10d as c10d
+
+    _QUEUE_CALLS[0] += 1
+    key = f"edgpu_farm_queue_{_QUEUE_CALLS[0]}"
+    store = c10d._get_default_store()
+    dist.barrier()
+    lock = threading.Lock()   # one store client per process: serialise its use
+    done = [False]
+
+    def take():
+        if done[0]:
+            return None
+        with lock:
+            i = int(store.add(key, 1)) - 1
+        if i >= n:
+            done[0] = True
+            return None
+        return i
+    return take
 
 
 def broadcast_vector(vec, owner: int, dim: int, cplx: bool, device: Optional[int] = None):

@@ -71,7 +71,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, q, cfg_kw, method):
+def _worker(rank, world, port, q, cfg_kw, method, schedule="dynamic"):
     import torch.distributed as dist
     from oracle_solver import solve_sector_oracle
     from edgpu.farm import broadcast_vector
@@ -80,7 +80,7 @@ def _worker(rank, world, port, q, cfg_kw, method):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     cfg = make_config(**cfg_kw)
-    res = farm_diag(cfg, DiagOptions(lanc_method=method), solver=solve_sector_oracle)
+    res = farm_diag(cfg, DiagOptions(lanc_method=method, farm_schedule=schedule), solver=solve_sector_oracle)
     gs_owner = res.owners[0]
     v = res.states.vectors[0] if rank == gs_owner else None
     dim = [s for s in setup_pointers(cfg) if s.isector == res.states.sectors[0]][0].dim
@@ -91,12 +91,13 @@ def _worker(rank, world, port, q, cfg_kw, method):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("schedule", ["dynamic", "lpt"])
 @pytest.mark.parametrize("cfg_kw,method", [
     (dict(Norb=1, Nbath=4), "arpack"),                 # configs[0]: all sectors dense
     (dict(Norb=1, Nbath=5), "lanczos"),                # sectors > 256 through the Lanczos branch
     (dict(Norb=1, Nbath=3, Nspin=2, ed_mode="nonsu2"), "arpack"),
 ])
-def test_gloo_farm_matches_serial(cfg_kw, method):
+def test_gloo_farm_matches_serial(cfg_kw, method, schedule):
     from oracle_solver import solve_sector_oracle
 
     cfg = make_config(**cfg_kw)
@@ -104,7 +105,7 @@ def test_gloo_farm_matches_serial(cfg_kw, method):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, cfg_kw, method)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, cfg_kw, method, schedule)) for r in range(2)]
     for p in procs:
         p.start()
     out = [q.get(timeout=300) for _ in range(2)]
@@ -116,10 +117,13 @@ def test_gloo_farm_matches_serial(cfg_kw, method):
         assert secs == serial.states.sectors
         np.testing.assert_allclose(en, serial.states.energies, rtol=0, atol=1e-12)
         assert abs(vnorm - 1.0) < 1e-10           # broadcast delivered the owner's unit vector
-    # both ranks got work and the assignment covers every sector once
+    # the assignment covers every sector once, the same on both ranks (LPT:
+    # both ranks got work; the dynamic queue gives work to whoever takes it)
     assign = out[0][4]
-    assert all(len(a) > 0 for a in assign)
-    assert sorted(i for a in assign for i in a) == [s.isector for s in setup_pointers(cfg)]
+    assert out[1][4] == assign
+    if schedule == "lpt":
+        assert all(len(a) > 0 for a in assign)
+    assert sorted(i for a in assign for i in a) == sorted(s.isector for s in setup_pointers(cfg))
 
 
 def _gf_worker(rank, world, port, q, cfg_kw):
