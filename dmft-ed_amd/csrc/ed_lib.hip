@@ -1636,7 +1636,16 @@ static int persist_mode(ed_sector* s, int vc, int path) {
 static int64_t persist_lds(const ed_sector* s, int vc, int mode) {
   const int64_t vs = vc ? 16 : 8, vr = persist_vrows(s, mode, vc);
   int64_t lds = ((vr * vs + 15) & ~(int64_t)15);
-  if (mode == 4) return lds + (vc ? vr * 8 + (int64_t)s->pkr_E * (s->pkr_dd + s->pkr_du) * 8 : 0);
+  if (mode == 4) {
+    // slot-major vector: RPT slots of NT + 1 elements (k_lanc_persist VSLOT;
+    // the 512-thread complex form keeps the natural order)
+    const bool c1024 = vc && (s->opts & ED_OPT_PKRON_C1024);
+    if (!vc || c1024) {
+      const int64_t nt = c1024 ? kPBlock : kPRegBlock;
+      lds = (((vr + vr / nt) * vs + 15) & ~(int64_t)15);
+    }
+    return lds + (vc ? vr * 8 + (int64_t)s->pkr_E * (s->pkr_dd + s->pkr_du) * 8 : 0);
+  }
   if (mode == 2) {
     const int64_t hs = s->hc ? 16 : 8;
     return lds + ((vr * 8 + 15) & ~(int64_t)15) + (((int64_t)s->ndict * hs + 15) & ~(int64_t)15);

@@ -106,6 +106,26 @@ __device__ __forceinline__ double pblock_sum(double v, double* ws) {
 constexpr uint32_t kPkColBits = 17, kPkColMask = (1u << kPkColBits) - 1;
 constexpr uint32_t kPkOffMask = (1u << 14) - 1;  // dictionary byte offset (<= 16 KiB)
 
+// Absolute LDS addressing for MODE 4's gathers: the byte address of an LDS
+// object, and loads through such an address — a constant added to it folds
+// into the ds_read immediate offset (no per-gather address add) when the
+// compiler can see the address is non-negative (masked at setup).
+__device__ __forceinline__ uint32_t lds_addr_of(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+template <typename T>
+__device__ __forceinline__ T lds_ldv(uint32_t a) {
+  if constexpr (sizeof(T) == 16) {
+    // through the native 2-vector type: one ds_read_b128 (a HIP_vector_type
+    // load is split into two 8-B loads, a ds_read2_b64 at twice the cycles)
+    typedef double d2v __attribute__((ext_vector_type(2)));
+    const d2v v = *(const __attribute__((address_space(3))) d2v*)(uintptr_t)a;
+    return T{v.x, v.y};
+  } else {
+    return *(const __attribute__((address_space(3))) T*)(uintptr_t)a;
+  }
+}
+
 // Rows of one thread: slot r holds row row0 + r*stride; slots r < nvalid are
 // basis rows (< dim), the others are padding rows in [dim, NT*RPT) whose LDS
 // entries, diagonal and matrix entries are zero, so every loop over r runs
@@ -155,6 +175,16 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
   __shared__ double ws[NT / 64];
   __shared__ double ws2[NT / 64];
   constexpr int VROWS = NT * RPT;  // LDS vector rows incl. padding
+  // MODE 4: slot-major LDS vector — row slot r of thread t at element
+  // r * VSLOT + t, VSLOT = NT + 1 (consecutive slots are 8 B off a 512-B
+  // multiple, so two slots' reads never merge into one ds_read2st64, which
+  // costs what two ds_read_b64 do twice over); a gather of slot r then
+  // addresses through a per-lane base plus the immediate r * VSLOT * size.
+  // (Not the 512-thread complex form: measured ~3 % slower per step and 18 %
+  // slower batched with it; that form keeps the natural row order.)
+  constexpr bool SLOT = MODE == 4 && !(VC && NT != kPBlock);
+  constexpr int VSLOT = NT + 1;
+  constexpr int VLDS = SLOT ? RPT * VSLOT : VROWS;  // LDS vector elements
   V* vl = (V*)smem;                // MODE 2/3 move it behind the dictionary
   const int64_t dim = a.dim;
   const int tid = threadIdx.x;
@@ -164,6 +194,7 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
   LancState* st = a.st + run;
   PRows q = persist_rows<MODE, RPT, NT>(tid, dim, a.kdu, a.kdd);
 #define PROW(r) (q.row0 + (r) * q.stride)
+#define LPOS(r) (SLOT ? (r) * VSLOT + tid : PROW(r))
 
   // --- Kronecker tables into LDS (after v)
   const H* aup = nullptr;
@@ -277,9 +308,9 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
   // p = v_{k-1} in global memory)
   constexpr bool KRV = KR && VC && NT == kPBlock;
   constexpr bool KRC = KR && VC && NT != kPBlock;
-  int ucol[KR ? E : 1];
+  uint32_t ucol[KR ? E : 1];  // KR: absolute LDS byte address of the up-hop target in slot 0
   double uval[(KR && !KRV) ? E : 1];
-  int dcol[KR ? RPT * E : 1];
+  uint32_t dcol[KR ? RPT * E : 1];  // KR: absolute LDS byte address of the down-hop target
   double dval[(KR && !VC) ? RPT * E : 1];
   double dgr[(KR && !KRV) ? RPT : 1];
   const double* sdv = nullptr;   // KRV: down-hop values [e * dd + iw]
@@ -294,7 +325,7 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
     if constexpr (KR && VC) {
       // LDS: vector | diagonal | down-hop values | up-hop values (KRC reads
       // only the down-hop values)
-      double* tg = (double*)(smem + (((int64_t)VROWS * sizeof(V) + 15) & ~(int64_t)15));
+      double* tg = (double*)(smem + (((int64_t)VLDS * sizeof(V) + 15) & ~(int64_t)15));
       for (int x = tid; x < VROWS; x += NT) {
         double d = 0.0;
         if (x < dim) {
@@ -316,10 +347,20 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
       sdv = t;
       suv = tu;
     }
+    const uint32_t lb = lds_addr_of(vl);
+    constexpr uint32_t kLdsMask = (1u << 18) - 1;  // LDS byte addresses < 256 KiB: known non-negative
 #pragma unroll
     for (int e = 0; e < E; e++) {
       const bool ok = act && e < a.kdegu;
-      ucol[e] = ok ? a.kupc[e * du + q.iu] * (int)sizeof(V) : 0;
+      // idle lanes read their own (zero) padding slot; padded hops a real
+      // entry of the row times a zero value
+      if constexpr (SLOT) {
+        const int pos = act ? g * du + (ok ? a.kupc[e * du + q.iu] : 0) : tid;
+        // (the mask also states the element alignment: b128 loads stay whole)
+        ucol[e] = (lb + (uint32_t)pos * (uint32_t)sizeof(V)) & kLdsMask & ~(uint32_t)(sizeof(V) - 1);
+      } else {  // byte offset inside the row iw (the row base added per row slot)
+        ucol[e] = ok ? (uint32_t)a.kupc[e * du + q.iu] * (uint32_t)sizeof(V) : 0u;
+      }
       if constexpr (!KRV) uval[e] = ok ? a.kupv[e * du + q.iu] : 0.0;
     }
 #pragma unroll
@@ -329,14 +370,19 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
 #pragma unroll
       for (int e = 0; e < E; e++) {
         const bool ok = okr && e < a.kdegd;
-        if constexpr (KR && VC) {
-          // padding slots gather the row's own (zero) padding entry, valid
-          // rows beyond their degree a zero table value
-          dcol[r * E + e] = (ok ? a.kdwc[e * dd + iw] * du + q.iu : (okr ? 0 : PROW(r))) * (int)sizeof(V);
+        // target row (iw', iu) sits in slot iw' / G of thread (iw' % G, iu)
+        int pos;
+        if (ok) {
+          const int iw2 = a.kdwc[e * dd + iw], r2 = iw2 / G;
+          pos = SLOT ? r2 * VSLOT + (iw2 - r2 * G) * du + q.iu : iw2 * du + q.iu;
         } else {
-          dcol[r * E + e] = (ok ? a.kdwc[e * dd + iw] * du + q.iu : 0) * (int)sizeof(V);
-          dval[r * E + e] = ok ? a.kdwv[e * dd + iw] : 0.0;
+          // padding slots gather their own (zero) slot, valid rows beyond
+          // their degree element 0 times a zero value
+          pos = okr ? 0 : LPOS(r);
         }
+        // (natural layout: a byte offset from vl, as before the slot layout)
+        dcol[r * E + e] = (SLOT ? lb : 0u) + (uint32_t)pos * (uint32_t)sizeof(V);
+        if constexpr (!(KR && VC)) dval[r * E + e] = ok ? a.kdwv[e * dd + iw] : 0.0;
       }
       if constexpr (!KRV) {
         double d = 0.0;
@@ -378,7 +424,7 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
       const bool ok = r < q.nvalid;
       const V x = ok ? Rg[i] : vzero<V>();
       if constexpr (UREG) u[r] = x;
-      vl[i] = x;
+      vl[LPOS(r)] = x;
       if constexpr (!PG) p[r] = (ok && !a.first) ? Pg[i] : vzero<V>();
       if (a.first) {
         nrm += redot(x, x);
@@ -441,13 +487,12 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
       // exposed ~20 times per step at 2 waves per SIMD)
       double gu[E], gd[E], go;
       auto gather = [&](int r, double* hu, double* hd, double& ho) {
-        const unsigned char* rb = (const unsigned char*)(vl + (PROW(r) - q.iu));  // row iw of V
 #pragma unroll
-        for (int e = 0; e < E; e++) hu[e] = *(const double*)(rb + ucol[e]);
+        for (int e = 0; e < E; e++) hu[e] = lds_ldv<double>(ucol[e] + r * VSLOT * 8);  // slot r of row iw
 #pragma unroll
-        for (int e = 0; e < E; e++) hd[e] = *(const double*)((const unsigned char*)vl + dcol[r * E + e]);
+        for (int e = 0; e < E; e++) hd[e] = lds_ldv<double>(dcol[r * E + e]);
         if constexpr (UREG) ho = u[r];
-        else ho = vl[PROW(r)];
+        else ho = vl[LPOS(r)];
       };
       gather(0, gu, gd, go);
 #pragma unroll
@@ -481,7 +526,7 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
 #pragma unroll
     for (int r = 0; r < RPT; r++) {
       const int i = PROW(r);
-      const V ur = UREG ? u[r] : vl[i];
+      const V ur = UREG ? u[r] : vl[LPOS(r)];
       V acc;
       if constexpr (MODE == 0) {
         acc = vzero<V>();
@@ -516,12 +561,16 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
         if constexpr (KRV) acc = mul(sdg[i], ur);
         else acc = mul(dgr[r], ur);
         {
-        const unsigned char* rb = (const unsigned char*)(vl + (i - q.iu));  // row iw of V
         if constexpr (KRV) {
-          // idle lanes (tid >= G*DimUp) read table column 0 with ucol = 0: their row base is a zero padding row
+          // idle lanes (tid >= G*DimUp) read table column 0 and their own zero padding slot
 #pragma unroll
-          for (int e = 0; e < E; e++) acc = fmac(acc, suv[e * a.kdu + q.iu], *(const V*)(rb + ucol[e]));
+          for (int e = 0; e < E; e++)
+            acc = fmac(acc, suv[e * a.kdu + q.iu], lds_ldv<V>(ucol[e] + r * VSLOT * (int)sizeof(V)));
+        } else if constexpr (SLOT) {
+#pragma unroll
+          for (int e = 0; e < E; e++) acc = fmac(acc, uval[e], lds_ldv<V>(ucol[e] + r * VSLOT * (int)sizeof(V)));
         } else {
+          const unsigned char* rb = (const unsigned char*)(vl + (i - q.iu));  // row iw of V
 #pragma unroll
           for (int e = 0; e < E; e++) acc = fmac(acc, uval[e], *(const V*)(rb + ucol[e]));
         }
@@ -529,11 +578,12 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
           const int iwc = min(giw + (NT / a.kdu) * r, a.kdd - 1);
 #pragma unroll
           for (int e = 0; e < E; e++)
-            acc = fmac(acc, sdv[e * a.kdd + iwc], *(const V*)((const unsigned char*)vl + dcol[r * E + e]));
+            acc = fmac(acc, sdv[e * a.kdd + iwc],
+                       SLOT ? lds_ldv<V>(dcol[r * E + e]) : *(const V*)((const unsigned char*)vl + dcol[r * E + e]));
         } else {
 #pragma unroll
           for (int e = 0; e < E; e++)
-            acc = fmac(acc, dval[r * E + e], *(const V*)((const unsigned char*)vl + dcol[r * E + e]));
+            acc = fmac(acc, dval[r * E + e], lds_ldv<V>(dcol[r * E + e]));
         }
         }
       } else {
@@ -575,12 +625,12 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
     if (basis) {  // uniform: no per-row EXEC masking when no basis is kept
 #pragma unroll
       for (int r = 0; r < RPT; r++)
-        if (r < q.nvalid) basis[(int64_t)it * dim + PROW(r)] = scl(s, UREG ? u[r] : vl[PROW(r)]);  // column k = v_k
+        if (r < q.nvalid) basis[(int64_t)it * dim + PROW(r)] = scl(s, UREG ? u[r] : vl[LPOS(r)]);  // column k = v_k
     }
 #pragma unroll
     for (int r = 0; r < RPT; r++) {
       const int i = PROW(r);
-      const V x = scl(s, UREG ? u[r] : vl[i]);
+      const V x = scl(s, UREG ? u[r] : vl[LPOS(r)]);
       if constexpr (PIPE) {
         w[r] = fma(-alpha, x, w[r]);
         bp = fma(w[r], w[r], bp);
@@ -594,7 +644,7 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
         p[r] = x;
       }
       if constexpr (UREG) u[r] = w[r];
-      vl[i] = w[r];
+      vl[LPOS(r)] = w[r];
     }
     // beta barrier: also publishes r_{k+1}
 #ifdef ED_P4_NOBETA  // timing probe: the step without the beta reduction (a bare barrier)
@@ -622,7 +672,7 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
 #pragma unroll
   for (int r = 0; r < RPT; r++) {
     if (r < q.nvalid) {
-      Rg[PROW(r)] = UREG ? u[r] : vl[PROW(r)];
+      Rg[PROW(r)] = UREG ? u[r] : vl[LPOS(r)];
       if constexpr (!PG) Pg[PROW(r)] = p[r];
     }
   }
@@ -631,6 +681,7 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
     st->beta = b;
   }
 #undef PROW
+#undef LPOS
 }
 
 }  // namespace edg
