@@ -20,7 +20,8 @@
 //     down-hop gathers of a wavefront are contiguous;
 //   * alpha and beta are block reductions (DPP wave sums + one LDS stage),
 //     two barriers per iteration, no global synchronisation.
-// configs[1]: MODE 4 2.4 µs per step (MODE 2 4.4 µs before this layout).
+// configs[1]: MODE 4 1.87 µs per step with the slot-major LDS vector below
+// (2.24 before it; MODE 2 4.4 µs before the Kronecker layout).
 #pragma once
 #include "ed_kernels.hpp"
 
