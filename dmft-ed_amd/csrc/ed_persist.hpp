@@ -294,6 +294,19 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
       }
     }
   }
+  if constexpr (REG) {
+    // words -> absolute LDS addresses {v entry: 17 bits | dictionary entry:
+    // 15 bits} (v ends below 128 KiB and the dictionary below 32 KiB in every
+    // layout the host admits): the loop then takes each address with one
+    // AND or one shift instead of a mask, a shift-add and a base add apiece
+    const uint32_t lbv = lds_addr_of(vl), lbd = lds_addr_of(dct);
+#pragma unroll
+    for (int k = 0; k < RPT * E; k++) {
+      const uint32_t x = pk[k];
+      pk[k] = (lbv + (x & kPkColMask) * (uint32_t)sizeof(V)) |
+              ((lbd + ((x >> kPkColBits) & kPkOffMask)) << kPkColBits);
+    }
+  }
   // --- MODE 4: Kronecker register layout (real H).  Up-hop list (target
   // rank as a byte offset inside the V row, value) once per thread; down-hop
   // entries (LDS byte address, value) and the diagonal per row; no
@@ -555,8 +568,8 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
 #pragma unroll
         for (int e = 0; e < E; e++) {
           const uint32_t x = pk[r * E + e];
-          const H h = *(const H*)(dct + ((x >> kPkColBits) & kPkOffMask));
-          acc = fmac(acc, h, vl[x & kPkColMask]);
+          const H h = lds_ldv<H>(x >> kPkColBits);
+          acc = fmac(acc, h, lds_ldv<V>(x & kPkColMask));
         }
       } else if constexpr (KR) {
         if constexpr (KRV) acc = mul(sdg[i], ur);

@@ -2,7 +2,7 @@
 # Round 4, call 13: MODE 4 slot-major LDS vector with absolute addressing
 # (no per-gather address adds): parity, then the configs[1] rates.
 set -o pipefail
-export RUN=${RUN:-r4n}
+export RUN=${RUN:-r4o}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$RUN
 bash tools/gpu_step.sh \
