@@ -20,7 +20,11 @@ grep '^{' "$OUT/bench.log" > "$OUT/bench_line.json" || true
 t=$(find "$OUT/st" -name "*kernel_trace.csv" | head -1)
 s=$(find "$OUT/st" -name "*kernel_stats.csv" | head -1)
 [ -n "$s" ] && cp "$s" "$P/bench_kernel_stats.csv"
-for e in "spmv|k_spmv_pk<false, false" "spmv_cplx|k_spmv_pk<true, true" "kron|k_kron_(up|dw)" "direct|k_direct<"; do
+# (persist: the headline configs[1] launches — one 512-thread workgroup,
+# grid 512 — apart from the batched ones of the same instantiation, whose
+# grids are K x 512: the runs split them)
+for e in "spmv|k_spmv_pk<false, false" "spmv_cplx|k_spmv_pk<true, true" "kron|k_kron_(up|dw)" "direct|k_direct<" \
+         "persist|k_lanc_persist<"; do
   IFS='|' read -r name pat <<< "$e"
   python3 "$R/tools/trace_summary.py" "$t" "$pat" 5 "$P/bench_trace_$name.json" \
     --note "rocprofv3 of bench.py $*: per (kernel, grid) group, 5 warm-up launches dropped" \

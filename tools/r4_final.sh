@@ -3,7 +3,7 @@
 # line, and bench.py under rocprofv3 (kernel statistics + per-sector
 # steady-state traces into profiles/r4).
 set -o pipefail
-export RUN=${RUN:-r4final}
+export RUN=${RUN:-r4final4}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$RUN
 bash tools/gpu_step.sh \
