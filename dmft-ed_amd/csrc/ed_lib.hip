@@ -2529,6 +2529,8 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
   T.st = s->stream;
   T.dim = s->dim;
   T.G = (int)std::min<int64_t>(grid_for(s->dim), (s->opts & ED_OPT_TRLAN_G128) ? 128 : kTrlanGridCap);
+  if (const char* eg = getenv("ED_TRLAN_GRID"))  // A/B (tools/trlan_ab.py --grid): Krylov sweep block cap
+    T.G = (int)std::min<int64_t>(grid_for(s->dim), std::max(1, atoi(eg)));
   T.hp = trlan_pinned();
   if (!T.hp) return fail(ED_ERR_OOM, "pinned host staging buffer");
   T.fused = !(s->opts & ED_OPT_TRLAN_UNFUSED);

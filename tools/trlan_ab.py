@@ -24,11 +24,14 @@ ap.add_argument("--opts", default="trlan_fullupd,eigh_no_verify")
 ap.add_argument("--sectors", default="6,6;5,6;4,5;3,4;2,3")
 ap.add_argument("--ncv", default="", help="comma list of ncv values (restart length) instead of the options")
 ap.add_argument("--keep", default="", help="comma list of ED_TRLAN_KEEP values (Ritz vectors kept beyond nev)")
+ap.add_argument("--grid", default="", help="comma list of ED_TRLAN_GRID values (Krylov sweep block cap)")
 a = ap.parse_args()
 cfg = c4_config("random")
 opt = DiagOptions()
 variants = [("default", (), None, None)]
-if a.ncv or a.keep:
+if a.grid:
+    variants += [(f"grid={g}", (), None, ("GRID", g)) for g in a.grid.split(",")]
+elif a.ncv or a.keep:
     for n in (a.ncv.split(",") if a.ncv else [None]):
         for k in (a.keep.split(",") if a.keep else [None]):
             variants.append((f"ncv={n} keep={k}", (), int(n) if n else None, k))
@@ -42,9 +45,11 @@ for q in a.sectors.split(";"):
         ref = None
         for name, o, ncv, keep in variants:
             S.set_options(*o)
-            if keep is None:
-                os.environ.pop("ED_TRLAN_KEEP", None)
-            else:
+            os.environ.pop("ED_TRLAN_KEEP", None)
+            os.environ.pop("ED_TRLAN_GRID", None)
+            if isinstance(keep, tuple):
+                os.environ["ED_TRLAN_" + keep[0]] = keep[1]
+            elif keep is not None:
                 os.environ["ED_TRLAN_KEEP"] = keep
             best, nhv = 1e9, 0
             for _ in range(a.reps):
@@ -57,3 +62,4 @@ for q in a.sectors.split(";"):
                   f"dE {np.max(np.abs(np.asarray(w) - ref)):.1e}", flush=True)
         S.set_options()
         os.environ.pop("ED_TRLAN_KEEP", None)
+        os.environ.pop("ED_TRLAN_GRID", None)
