@@ -2320,7 +2320,7 @@ static double* trlan_pinned() {
 }
 
 // blocks of the O(dim) Krylov sweeps
-static constexpr int kTrlanGridCap = 1024;
+static constexpr int kTrlanGridCap = 512;  // (1024 until round 4: 512 measured 13 % faster per large-sector solve, tools/trlan_ab.py --grid)
 // persistent sweeps (k_trl_sweep): sector size limit and rows per workgroup
 static constexpr int64_t kPSweepMaxDim = 131072;
 static constexpr int64_t kPSweepRows = 256;

@@ -285,6 +285,54 @@ __global__ void __launch_bounds__(kBlock) k_coef_scale(const double* __restrict_
     out[i] = scl(inv, x[i]);
 }
 
+// N wave sums at once (N a multiple of 4): a transposing reduction — each
+// v_permlane32_swap / v_permlane16_swap step exchanges half of two values'
+// lanes so that one add halves the lanes of both, and the 16-lane rows that
+// remain are summed by DPP (4 steps).  ~3 VALU per value per halving for the
+// first two levels instead of 18 per value for a full DPP sum each (k_cgs:
+// 25 values per wave, ~450 -> ~130 instructions).  Value k lands in row
+// {0, 2, 1, 3}[k mod 4] of register k / 4; lane 0 of each row stores it to
+// out[k].  Fixed order: deterministic.
+__device__ __forceinline__ double swap_add32(double a, double b) {
+  // lanes 32-63 of a <-> lanes 0-31 of b; then the lower lanes hold a's two
+  // halves' a-values, the upper lanes b's: a' + b' reduces a over lane pairs
+  // (l, l+32) in the lower half and b in the upper half
+  const auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(a), __double2loint(b), false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(a), __double2hiint(b), false, false);
+  return __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
+}
+__device__ __forceinline__ double swap_add16(double a, double b) {
+  // odd rows of a <-> even rows of b
+  const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(a), __double2loint(b), false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(a), __double2hiint(b), false, false);
+  return __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
+}
+template <int N>
+__device__ __forceinline__ void wave_sum_multi(const double (&v)[N], double* out, int nout) {
+  static_assert(N % 4 == 0, "wave_sum_multi: N multiple of 4");
+  const int lane = threadIdx.x & 63;
+  double t[N / 2];
+#pragma unroll
+  for (int i = 0; i < N / 2; i++) t[i] = swap_add32(v[2 * i], v[2 * i + 1]);
+  double u[N / 4];
+#pragma unroll
+  for (int i = 0; i < N / 4; i++) {
+    double w = swap_add16(t[2 * i], t[2 * i + 1]);
+    w = dpp_add<0xB1, 0xF>(w);   // quad_perm [1,0,3,2]
+    w = dpp_add<0x4E, 0xF>(w);   // quad_perm [2,3,0,1]
+    w = dpp_add<0x141, 0xF>(w);  // row_half_mirror
+    w = dpp_add<0x140, 0xF>(w);  // row_mirror: every lane holds its row's sum
+    u[i] = w;
+  }
+  if ((lane & 15) == 0) {
+    const int row = lane >> 4;
+    const int sub = row == 0 ? 0 : row == 1 ? 2 : row == 2 ? 1 : 3;
+#pragma unroll
+    for (int i = 0; i < N / 4; i++)
+      if (4 * i + sub < nout) out[4 * i + sub] = u[i];
+  }
+}
+
 // Fused CGS sweep over the rows of x (one column group of up to NC columns
 // held in registers per row):
 //   hin != nullptr : x_i -= sum_{c<ncol} V_c,i hin_c   (written back)
@@ -304,6 +352,7 @@ __global__ void __launch_bounds__(kBlock) k_cgs(const val_t<VC>* __restrict__ V,
                                                 int* lof = nullptr, const double* locA = nullptr) {
   constexpr int NW = kBlock / 64;
   constexpr int NR = (VC ? 2 * NC : NC) + 1;  // partial slots per wave
+  constexpr int NRP = (NR + 3) / 4 * 4;       // padded for wave_sum_multi
   __shared__ double2 hs[NC];
   __shared__ double red[NW][NR];
   // conditional second pass (dgA != null): when the DGKS test says the first
@@ -387,18 +436,18 @@ __global__ void __launch_bounds__(kBlock) k_cgs(const val_t<VC>* __restrict__ V,
   }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   if (part) {
+    // every dot and the norm in one transposing reduction
+    double vals[NRP];
+#pragma unroll
+    for (int c = 0; c < NRP; c++) vals[c] = 0.0;
 #pragma unroll
     for (int c = 0; c < NC; c++) {
-      if (c < c0 || c >= ncol) continue;  // uniform
-      const double r = wave_sum_dpp(are[c]);
-      if (lane == 63) red[wv][c] = r;
-      if constexpr (VC) {
-        const double q = wave_sum_dpp(aim[c]);
-        if (lane == 63) red[wv][NC + c] = q;
-      }
+      vals[c] = are[c];
+      if constexpr (VC) vals[NC + c] = aim[c];
     }
-  }
-  if (npart) {
+    vals[NR - 1] = n2;
+    wave_sum_multi<NRP>(vals, red[wv], NR);
+  } else if (npart) {
     const double r = wave_sum_dpp(n2);
     if (lane == 63) red[wv][NR - 1] = r;
   }
@@ -454,18 +503,32 @@ __device__ __forceinline__ void orth_solo_body(const val_t<VC>* __restrict__ V, 
   double are[NC], aim[VC ? NC : 1];
   // block sums (fixed order): are/aim (first nc columns) and n2 -> tot
   auto reduce = [&](int nc, double n2) {
+    if (nc >= 4) {  // uniform: every value in one transposing reduction
+      constexpr int NRP = (NR + 3) / 4 * 4;
+      double vals[NRP];
 #pragma unroll
-    for (int c = 0; c < NC; c++) {
-      if (c >= nc) continue;  // uniform
-      const double r = wave_sum_dpp(are[c]);
-      if (lane == 63) red[wv][c] = r;
-      if constexpr (VC) {
-        const double q = wave_sum_dpp(aim[c]);
-        if (lane == 63) red[wv][NC + c] = q;
+      for (int c = 0; c < NRP; c++) vals[c] = 0.0;
+#pragma unroll
+      for (int c = 0; c < NC; c++) {
+        vals[c] = are[c];
+        if constexpr (VC) vals[NC + c] = aim[c];
       }
+      vals[NR - 1] = n2;
+      wave_sum_multi<NRP>(vals, red[wv], NR);
+    } else {
+#pragma unroll
+      for (int c = 0; c < NC; c++) {
+        if (c >= nc) continue;  // uniform
+        const double r = wave_sum_dpp(are[c]);
+        if (lane == 63) red[wv][c] = r;
+        if constexpr (VC) {
+          const double q = wave_sum_dpp(aim[c]);
+          if (lane == 63) red[wv][NC + c] = q;
+        }
+      }
+      const double r = wave_sum_dpp(n2);
+      if (lane == 63) red[wv][NR - 1] = r;
     }
-    const double r = wave_sum_dpp(n2);
-    if (lane == 63) red[wv][NR - 1] = r;
     __syncthreads();
     if (t < NR) {
       double a = 0.0;
