@@ -2402,9 +2402,9 @@ static int trlan_core(Trlan<VC>& T, int k0, int nev, int maxit, double tol, cons
       if (fabs(beta * Z[(ma - 1) + (size_t)ma * i]) <= tol * std::max(eps23, fabs(theta[i]))) conv++;
     if (conv == nev || it == maxit - 1 || m == dim) break;
     // thick restart: keep nkeep Ritz vectors + the residual direction
-    int nkeep = std::max(nev, std::min(ma - 2, nev + (ma - nev) / 2));
-    if (const char* ek = getenv("ED_TRLAN_KEEP"))  // A/B (tools/trlan_ab.py): nev + k kept
-      nkeep = std::max(nev, std::min(ma - 2, nev + atoi(ek)));
+    // (kept beyond nev: (ma - nev) / 2 — within 5 % of the best of 16
+    // restart-length variants on configs[3])
+    const int nkeep = std::max(nev, std::min(ma - 2, nev + (ma - nev) / 2));
     // (the previous restart's upload of hZ completed at this sweep's sync)
     std::copy(Z.begin(), Z.begin() + (size_t)ma * ma, hZ);
     HIPCK(hipMemcpyAsync(T.Y, hZ, (size_t)ma * ma * sizeof(double), hipMemcpyHostToDevice, st));
@@ -2529,8 +2529,6 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
   T.st = s->stream;
   T.dim = s->dim;
   T.G = (int)std::min<int64_t>(grid_for(s->dim), (s->opts & ED_OPT_TRLAN_G128) ? 128 : kTrlanGridCap);
-  if (const char* eg = getenv("ED_TRLAN_GRID"))  // A/B (tools/trlan_ab.py --grid): Krylov sweep block cap
-    T.G = (int)std::min<int64_t>(grid_for(s->dim), std::max(1, atoi(eg)));
   T.hp = trlan_pinned();
   if (!T.hp) return fail(ED_ERR_OOM, "pinned host staging buffer");
   T.fused = !(s->opts & ED_OPT_TRLAN_UNFUSED);

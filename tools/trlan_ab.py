@@ -2,7 +2,7 @@
 sectors (device time of ed_sector_eigh, best of N): default against the
 listed ED_OPT_* alternatives.
 
-    python tools/trlan_ab.py [--reps 5] [--opts trlan_fullupd,eigh_no_verify]
+    python tools/trlan_ab.py [--reps 5] [--opts trlan_fullupd,eigh_no_verify] [--ncv 16,23,32]
 """
 import argparse
 import os
@@ -23,18 +23,14 @@ ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--opts", default="trlan_fullupd,eigh_no_verify")
 ap.add_argument("--sectors", default="6,6;5,6;4,5;3,4;2,3")
 ap.add_argument("--ncv", default="", help="comma list of ncv values (restart length) instead of the options")
-ap.add_argument("--keep", default="", help="comma list of ED_TRLAN_KEEP values (Ritz vectors kept beyond nev)")
-ap.add_argument("--grid", default="", help="comma list of ED_TRLAN_GRID values (Krylov sweep block cap)")
+# (round 4 also swept the kept Ritz vectors and the Krylov block cap through
+# temporary library switches, since removed: DESIGN.md §2 has the results)
 a = ap.parse_args()
 cfg = c4_config("random")
 opt = DiagOptions()
 variants = [("default", (), None, None)]
-if a.grid:
-    variants += [(f"grid={g}", (), None, ("GRID", g)) for g in a.grid.split(",")]
-elif a.ncv or a.keep:
-    for n in (a.ncv.split(",") if a.ncv else [None]):
-        for k in (a.keep.split(",") if a.keep else [None]):
-            variants.append((f"ncv={n} keep={k}", (), int(n) if n else None, k))
+if a.ncv:
+    variants += [(f"ncv={n}", (), int(n), None) for n in a.ncv.split(",")]
 else:
     variants += [(o, (o,), None, None) for o in a.opts.split(",") if o]
 for q in a.sectors.split(";"):
@@ -43,14 +39,8 @@ for q in a.sectors.split(";"):
         neigen, nitermax, nblock = lanczos_params(S.dim, opt)
         v0 = _start_vector(S.dim, False)
         ref = None
-        for name, o, ncv, keep in variants:
+        for name, o, ncv, _ in variants:
             S.set_options(*o)
-            os.environ.pop("ED_TRLAN_KEEP", None)
-            os.environ.pop("ED_TRLAN_GRID", None)
-            if isinstance(keep, tuple):
-                os.environ["ED_TRLAN_" + keep[0]] = keep[1]
-            elif keep is not None:
-                os.environ["ED_TRLAN_KEEP"] = keep
             best, nhv = 1e9, 0
             for _ in range(a.reps):
                 torch.cuda.synchronize()
@@ -61,5 +51,3 @@ for q in a.sectors.split(";"):
             print(f"({q1},{q2}) dim {S.dim:7d} {name:15s} {best * 1e3:8.2f} ms  nhv {nhv:4d}  "
                   f"dE {np.max(np.abs(np.asarray(w) - ref)):.1e}", flush=True)
         S.set_options()
-        os.environ.pop("ED_TRLAN_KEEP", None)
-        os.environ.pop("ED_TRLAN_GRID", None)
