@@ -50,6 +50,7 @@ struct PersistGeom {
   int64_t dim = 0;
   int preg_E = 0, preg_rpt = 0, kreg_W = 0, kreg_rpt = 0, pkr_E = 0, pkr_rpt = 0, pkr_rpt_c = 0;
   int pkr_c1024 = 0;  // complex MODE 4 in the 1024-thread layout (ED_OPT_PKRON_C1024)
+  int pkr_cslot = 0;  // complex MODE 4, 512 threads, slot-major LDS vector (ED_OPT_PKRON_CSLOT, A/B)
 };
 
 // Launch k_lanc_persist for (hc, vc, mode) on the geometry's template values;

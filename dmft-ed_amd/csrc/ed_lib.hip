@@ -1640,7 +1640,7 @@ static int64_t persist_lds(const ed_sector* s, int vc, int mode) {
     // slot-major vector: RPT slots of NT + 1 elements (k_lanc_persist VSLOT;
     // the 512-thread complex form keeps the natural order)
     const bool c1024 = vc && (s->opts & ED_OPT_PKRON_C1024);
-    if (!vc || c1024) {
+    if (!vc || c1024 || (s->opts & ED_OPT_PKRON_CSLOT)) {
       const int64_t nt = c1024 ? kPBlock : kPRegBlock;
       lds = (((vr + vr / nt) * vs + 15) & ~(int64_t)15);
     }
@@ -1677,6 +1677,7 @@ static PersistGeom persist_geom(const ed_sector* s) {
   g.pkr_rpt = s->pkr_rpt;
   g.pkr_rpt_c = s->pkr_rpt_c;
   g.pkr_c1024 = (s->opts & ED_OPT_PKRON_C1024) ? 1 : 0;
+  g.pkr_cslot = (s->opts & ED_OPT_PKRON_CSLOT) ? 1 : 0;
   return g;
 }
 
@@ -2834,7 +2835,7 @@ static constexpr int32_t kOptKnown =
     ED_OPT_NO_PERSIST | ED_OPT_PERSIST_STORED | ED_OPT_NO_PREG | ED_OPT_NO_PKRON | ED_OPT_FUSED_STEP |
     ED_OPT_SPLIT_SIMPLE | ED_OPT_NO_BATCH | ED_OPT_EIGH_NO_VERIFY | ED_OPT_TRLAN_UNFUSED | ED_OPT_TRLAN_NOFOLD |
     ED_OPT_TRLAN_PSWEEP | ED_OPT_NO_GRAPH | ED_OPT_TRLAN_NOLOCAL | ED_OPT_TRLAN_NOSOLO | ED_OPT_TRLAN_FULLUPD |
-    ED_OPT_PKRON_C1024 | ED_OPT_TRLAN_G128 | ED_OPT_EIGH_FULLPROBE;
+    ED_OPT_PKRON_C1024 | ED_OPT_TRLAN_G128 | ED_OPT_EIGH_FULLPROBE | ED_OPT_PKRON_CSLOT;
 
 int ed_sector_set_options(ed_sector* s, int32_t opts) {
   if (!s) return fail(ED_ERR_ARG, "null");

@@ -168,7 +168,7 @@ __device__ __forceinline__ PRows persist_rows(int tid, int64_t dim, int du, int 
 // LDS holds r_k = b_k v_k UNNORMALISED: w is stored as soon as a_k is known
 // (all gathers of the step are behind the alpha barrier) and the next step
 // scales H r by 1/b — two barriers per step (alpha, beta), one LDS vector.
-template <bool HC, bool VC, int MODE, int RPT, int E = 1, int NT = kPBlock>
+template <bool HC, bool VC, int MODE, int RPT, int E = 1, int NT = kPBlock, bool CSLOT = false>
 __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
   using V = val_t<VC>;
   using H = val_t<HC>;
@@ -183,7 +183,9 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
   // addresses through a per-lane base plus the immediate r * VSLOT * size.
   // (Not the 512-thread complex form: measured ~3 % slower per step and 18 %
   // slower batched with it; that form keeps the natural row order.)
-  constexpr bool SLOT = MODE == 4 && !(VC && NT != kPBlock);
+  // (CSLOT: the slot layout for the 512-thread complex form too — A/B,
+  // ED_OPT_PKRON_CSLOT)
+  constexpr bool SLOT = MODE == 4 && (!(VC && NT != kPBlock) || CSLOT);
   constexpr int VSLOT = NT + 1;
   constexpr int VLDS = SLOT ? RPT * VSLOT : VROWS;  // LDS vector elements
   V* vl = (V*)smem;                // MODE 2/3 move it behind the dictionary

@@ -87,6 +87,7 @@ extern "C" {
 #define ED_OPT_PKRON_C1024    0x8000 /* Lanczos MODE 4, complex vectors: 1024-thread LDS layout  */
 #define ED_OPT_TRLAN_G128    0x10000 /* eigh: Krylov sweeps on <= 128 blocks (coefficients folded) */
 #define ED_OPT_EIGH_FULLPROBE 0x20000 /* eigh: degeneracy probe without the plain-Lanczos screen */
+#define ED_OPT_PKRON_CSLOT   0x40000 /* Lanczos MODE 4, complex vectors, 512 threads: slot-major LDS vector (A/B) */
 
 /* status codes */
 #define ED_OK              0

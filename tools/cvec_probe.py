@@ -23,10 +23,13 @@ with Sector(cfg, 4, 4, stored=True, real=True) as S:
     i = torch.arange(1, S.dim + 1, dtype=torch.float64, device="cuda")
     v0 = torch.complex(torch.sin(i), torch.cos(3 * i)).contiguous()
     out = {}
-    for name, opts in (("c512", ()), ("c1024", ("pkron_c1024",))):
+    for name, opts in (("c512", ()), ("c1024", ("pkron_c1024",)), ("c512slot", ("pkron_cslot",)),
+                       ("c512_2", ())):
         ips, run = _lanc_rate(S, 512, v0, options=opts)
         out[name] = run
         print(f"{name}: {1e6 / ips:.3f} us/step ({ips:.0f} it/s)", flush=True)
+    a2 = np.asarray(out["c512slot"][0])
+    print(f"slot layout alpha max rel dev vs c512 {np.max(np.abs(a2[:64] - np.asarray(out['c512'][0])[:64])) / np.max(np.abs(a2[:64])):.2e}")
     a0, b0 = np.asarray(out["c512"][0]), np.asarray(out["c512"][1])
     a1, b1 = np.asarray(out["c1024"][0]), np.asarray(out["c1024"][1])
     n = min(len(a0), len(a1), 64)
