@@ -1297,7 +1297,10 @@ __global__ void __launch_bounds__(kKronUpBlock) k_kron_up(KronArgs<HC> K, const 
 // DimDw x nu column strip of the within-sector split),
 // dwi[iw*DEG + k] = its value's dictionary index (DEG slots per row, padded):
 // one wave-uniform row is one s_load_dwordx8/x16 + one of the index bytes
-template <bool HC, bool VC, int DEG, class Epi>
+// CW = 2 (real vectors, even ld and ncols, 16-byte aligned x and ypart): two
+// adjacent columns per lane, 128 per wave — one 16-byte gather per hop
+// instead of two 8-byte ones; the same per-element term order
+template <bool HC, bool VC, int DEG, class Epi, int CW = 1>
 __global__ void __launch_bounds__(kBlock) k_kron_dw(KronArgs<HC> K, const uint32_t* __restrict__ dwo,
                                                     const uint8_t* __restrict__ dwi,
                                                     const val_t<HC>* __restrict__ dwdict, int ndict,
@@ -1318,12 +1321,15 @@ __global__ void __launch_bounds__(kBlock) k_kron_dw(KronArgs<HC> K, const uint32
   // rows of length ld, columns [0, ncols): the whole DimDw x DimUp view
   // (ld = ncols = DimUp) or a column strip; ypart == nullptr: no first-pass
   // part (the strip's down-hop sum alone)
+  static_assert(CW == 1 || (CW == 2 && !VC), "two columns per lane: real vectors only");
   const int du = ld, dd = (int)K.dimdw;
-  const int nchunk = (ncols + 63) >> 6;
+  constexpr int CWID = 64 * CW;  // columns per chunk
+  const int nchunk = (ncols + CWID - 1) / CWID;
   // rows per wave: 4 at <= 8 slots; 2 above (the R x DEG gathered values sit
   // in VGPRs: 4 x 16 doubles held 149 VGPRs, 3 waves/SIMD, scalar spills);
   // half that for complex vectors (4 x 8 complex: 157 VGPRs, 3 waves/SIMD)
-  constexpr int R = VC ? (DEG <= 8 ? 2 : 1) : (DEG <= 8 ? kKronRowsPerWave : 2);
+  // and for two columns per lane
+  constexpr int R = (VC || CW == 2) ? (DEG <= 8 ? 2 : 1) : (DEG <= 8 ? kKronRowsPerWave : 2);
   constexpr int kTileRows = (kBlock / 64) * R;
   const int nrb = (dd + kTileRows - 1) / kTileRows;
   // blocks are dealt round-robin to the 8 XCDs: XCD x = blockIdx % 8 takes
@@ -1338,7 +1344,7 @@ __global__ void __launch_bounds__(kBlock) k_kron_dw(KronArgs<HC> K, const uint32
   }
   double part = 0.0;
   for (; m < mine;) {
-    const int iu = (xcd + 8 * m) * 64 + lane;
+    const int iu = (xcd + 8 * m) * CWID + lane * CW;
     const bool ok = iu < ncols;
     const int r0 = rb * kTileRows + wv * R;  // wave-uniform
     // every load of the wave's R rows in flight before any use
@@ -1355,6 +1361,44 @@ __global__ void __launch_bounds__(kBlock) k_kron_dw(KronArgs<HC> K, const uint32
         wo[r][k] = (wd & 0xffffffu) * (uint32_t)du;
         wi[r][k] = dwi[rr * DEG + k];
       }
+    }
+    if constexpr (CW == 2) {
+      typedef double d2 __attribute__((ext_vector_type(2)));
+      const d2 z2 = {0.0, 0.0};
+      d2 g[R][DEG], yv[R], xv[R];
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        const int i = (r0 + r) * du + iu;
+        const bool on = ok && r0 + r < dd;
+#pragma unroll
+        for (int k = 0; k < DEG; k++) {
+          g[r][k] = z2;
+          if (k < nk[r]) g[r][k] = on ? *(const d2*)(x + (int)wo[r][k] + iu) : z2;
+        }
+        xv[r] = on ? *(const d2*)(x + i) : z2;
+        yv[r] = (on && ypart) ? *(const d2*)(ypart + i) : z2;
+      }
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        if (!ok || r0 + r >= dd) continue;
+        double a0 = yv[r].x, a1 = yv[r].y;
+#pragma unroll
+        for (int k = 0; k < DEG; k++)
+          if (k < nk[r]) {
+            const H h = sdict[wi[r][k]];
+            a0 = add(a0, mul(h, g[r][k].x));
+            a1 = add(a1, mul(h, g[r][k].y));
+          }
+        const int i = (r0 + r) * du + iu;
+        part += epi.row((int64_t)i, a0, xv[r].x);
+        part += epi.row((int64_t)i + 1, a1, xv[r].y);
+      }
+      rb += g8;
+      while (rb >= nrb) {
+        rb -= nrb;
+        m++;
+      }
+      continue;
     }
     V g[R][DEG], yv[R], xv[R];
 #pragma unroll

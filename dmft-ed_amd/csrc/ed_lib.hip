@@ -1050,6 +1050,27 @@ static int launch_kron_dw(ed_sector* s, const void* x, const void* ypart, Epi ep
   using H = val_t<HC>;
   KronHost& K = s->K;
   const int grid = kron_dw_grid(VC);
+  if constexpr (!HC && !VC) {
+    // two columns per lane (16-byte gathers) where the rows, the column
+    // range and both vectors are 16-byte aligned
+    const bool a16 = ((uintptr_t)x % 16) == 0 && ((uintptr_t)ypart % 16) == 0;
+    if (!(s->opts & ED_OPT_KRON_DW1) && ld % 2 == 0 && ncols % 2 == 0 && a16) {
+      if (K.degD == 8)
+        hipLaunchKernelGGL((k_kron_dw<HC, VC, 8, Epi, 2>), dim3(grid), dim3(kBlock), 0, st, kron_args<HC>(s),
+                           K.dwo, K.dwi, (const H*)K.dwdict, K.ndwdict, (const V*)x, (const V*)ypart, epi, ld,
+                           ncols);
+      else if (K.degD == 12)
+        hipLaunchKernelGGL((k_kron_dw<HC, VC, 12, Epi, 2>), dim3(grid), dim3(kBlock), 0, st, kron_args<HC>(s),
+                           K.dwo, K.dwi, (const H*)K.dwdict, K.ndwdict, (const V*)x, (const V*)ypart, epi, ld,
+                           ncols);
+      else
+        hipLaunchKernelGGL((k_kron_dw<HC, VC, 16, Epi, 2>), dim3(grid), dim3(kBlock), 0, st, kron_args<HC>(s),
+                           K.dwo, K.dwi, (const H*)K.dwdict, K.ndwdict, (const V*)x, (const V*)ypart, epi, ld,
+                           ncols);
+      HIPCK(hipGetLastError());
+      return ED_OK;
+    }
+  }
   if (K.degD == 8)
     hipLaunchKernelGGL((k_kron_dw<HC, VC, 8, Epi>), dim3(grid), dim3(kBlock), 0, st, kron_args<HC>(s),
                        K.dwo, K.dwi, (const H*)K.dwdict, K.ndwdict, (const V*)x, (const V*)ypart, epi, ld, ncols);
@@ -2835,7 +2856,7 @@ static constexpr int32_t kOptKnown =
     ED_OPT_NO_PERSIST | ED_OPT_PERSIST_STORED | ED_OPT_NO_PREG | ED_OPT_NO_PKRON | ED_OPT_FUSED_STEP |
     ED_OPT_SPLIT_SIMPLE | ED_OPT_NO_BATCH | ED_OPT_EIGH_NO_VERIFY | ED_OPT_TRLAN_UNFUSED | ED_OPT_TRLAN_NOFOLD |
     ED_OPT_TRLAN_PSWEEP | ED_OPT_NO_GRAPH | ED_OPT_TRLAN_NOLOCAL | ED_OPT_TRLAN_NOSOLO | ED_OPT_TRLAN_FULLUPD |
-    ED_OPT_PKRON_C1024 | ED_OPT_TRLAN_G128 | ED_OPT_EIGH_FULLPROBE | ED_OPT_PKRON_CSLOT;
+    ED_OPT_PKRON_C1024 | ED_OPT_TRLAN_G128 | ED_OPT_EIGH_FULLPROBE | ED_OPT_PKRON_CSLOT | ED_OPT_KRON_DW1;
 
 int ed_sector_set_options(ed_sector* s, int32_t opts) {
   if (!s) return fail(ED_ERR_ARG, "null");

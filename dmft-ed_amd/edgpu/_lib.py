@@ -21,6 +21,7 @@ OPTIONS = {
     "trlan_unfused": 0x100, "trlan_nofold": 0x200, "trlan_psweep": 0x400, "no_graph": 0x800,
     "trlan_nolocal": 0x1000, "trlan_nosolo": 0x2000, "trlan_fullupd": 0x4000, "pkron_c1024": 0x8000,
     "trlan_g128": 0x10000, "eigh_fullprobe": 0x20000, "pkron_cslot": 0x40000,
+    "kron_dw1": 0x80000,
 }
 ED_OK = 0
 ERRORS = {1: "ED_ERR_ARG", 2: "ED_ERR_STATE", 3: "ED_ERR_HIP", 4: "ED_ERR_OOM",

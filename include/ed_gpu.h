@@ -88,6 +88,7 @@ extern "C" {
 #define ED_OPT_TRLAN_G128    0x10000 /* eigh: Krylov sweeps on <= 128 blocks (coefficients folded) */
 #define ED_OPT_EIGH_FULLPROBE 0x20000 /* eigh: degeneracy probe without the plain-Lanczos screen */
 #define ED_OPT_PKRON_CSLOT   0x40000 /* Lanczos MODE 4, complex vectors, 512 threads: slot-major LDS vector (A/B) */
+#define ED_OPT_KRON_DW1      0x80000 /* two-pass Kronecker H·v, real vectors: pass D one column per lane (A/B) */
 
 /* status codes */
 #define ED_OK              0

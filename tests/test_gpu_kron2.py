@@ -19,10 +19,10 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 
-def _both(cfg, q, real):
+def _both(cfg, q, real, options=()):
     from edgpu.hamiltonian import Sector
 
-    A = Sector(cfg, q[0], q[1], stored=False, direct=True, real=real, kron2=True)
+    A = Sector(cfg, q[0], q[1], stored=False, direct=True, real=real, kron2=True, options=options)
     B = Sector(cfg, q[0], q[1], stored=False, direct=True, real=real, kron2=False)
     return A, B
 
@@ -54,11 +54,14 @@ def test_two_pass_bit_identical(name, factory, sectors):
     (dict(Norb=2, Nbath=4, bath="random", seed=4), (3, 6)),              # du != dd
     (dict(Norb=1, Nbath=6, bath="random", seed=6), (3, 4)),              # odd DimUp (35)
 ])
-def test_two_pass_real_vectors_and_lanczos(cfg_kw, q):
+@pytest.mark.parametrize("opts", [(), ("kron_dw1",)], ids=["dw2", "dw1"])
+def test_two_pass_real_vectors_and_lanczos(cfg_kw, q, opts):
+    """Pass D takes two columns per lane at even DimUp (odd DimUp, or the
+    kron_dw1 option: one) — the same H·v bit for bit."""
     from edgpu.params import make_config
 
     cfg = make_config(**cfg_kw)
-    A, B = _both(cfg, q, real=True)
+    A, B = _both(cfg, q, real=True, options=opts)
     with A, B:
         i = torch.arange(1, A.dim + 1, dtype=torch.float64, device="cuda:0")
         x = torch.sin(i)
