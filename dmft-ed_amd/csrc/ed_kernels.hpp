@@ -1329,6 +1329,7 @@ __global__ void __launch_bounds__(kBlock) k_kron_dw(KronArgs<HC> K, const uint32
   // in VGPRs: 4 x 16 doubles held 149 VGPRs, 3 waves/SIMD, scalar spills);
   // half that for complex vectors (4 x 8 complex: 157 VGPRs, 3 waves/SIMD)
   // and for two columns per lane
+  // (4 rows per wave with two columns: 157 VGPRs, 3 waves/SIMD, slower)
   constexpr int R = (VC || CW == 2) ? (DEG <= 8 ? 2 : 1) : (DEG <= 8 ? kKronRowsPerWave : 2);
   constexpr int kTileRows = (kBlock / 64) * R;
   const int nrb = (dd + kTileRows - 1) / kTileRows;

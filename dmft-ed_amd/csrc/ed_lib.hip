@@ -957,6 +957,7 @@ static bool xcd_on(const ed_sector* s, int path) {
 // pass D of the two-pass Kronecker H·v: a multiple of 8 blocks (XCD column
 // chunks), 8 resident per CU
 static constexpr int kKronDwGrid = 2048;
+static constexpr int kKronDwGrid2 = 1280;  // two columns per lane
 // pass U LDS: dictionary + two sets of `rows` staged rows
 static constexpr int kKronUpSets = 2;
 static size_t kron_up_lds(bool hc, bool vc, int64_t du, int rows) {
@@ -973,9 +974,17 @@ static bool kron2_on(const ed_sector* s, int path, int vc) {
 // Complex vectors take half the grid: their column chunk V[:, c0:c0+64] is
 // twice the bytes, and fewer chunks in flight keep it in L2 (N28 complex
 // pass D: 512 blocks 187-193 us, 1024 160 us, 2048 167 us; real: 109, 81, 80).
-static int kron_dw_grid(bool vc) { return vc ? kKronDwGrid / 2 : kKronDwGrid; }
+// The two-column real form (even DimUp) has twice the chunk bytes too and
+// takes 1280 blocks, 5 per CU (N28: 2048 0.111 ms, 1536 0.115, 1280 0.104-
+// 0.106, 1024 0.104, 768 0.106-0.107; N28b 0.134 / 0.129 / 0.126-0.131 /
+// 0.129-0.130 / 0.135; configs[3] (6,6) 0.0150 / 0.0152 / 0.0152-0.0153 /
+// 0.0155 / 0.0161 ms).
+static int kron_dw_grid(const ed_sector* s, bool vc) {
+  if (vc) return kKronDwGrid / 2;
+  return (s->K.dimup % 2 == 0 && !(s->opts & ED_OPT_KRON_DW1)) ? kKronDwGrid2 : kKronDwGrid;
+}
 static int hxv_blocks(const ed_sector* s, int path, int vc = 0) {
-  if (kron2_on(s, path, vc)) return kron_dw_grid(vc);
+  if (kron2_on(s, path, vc)) return kron_dw_grid(s, vc);
   if (path == 1) return s->dir_grid;
   const int g = grid_for(s->nslice * 64);
   return xcd_on(s, path) ? (g & ~7) : g;
@@ -1049,7 +1058,7 @@ static int launch_kron_dw(ed_sector* s, const void* x, const void* ypart, Epi ep
   using V = val_t<VC>;
   using H = val_t<HC>;
   KronHost& K = s->K;
-  const int grid = kron_dw_grid(VC);
+  const int grid = kron_dw_grid(s, VC);
   if constexpr (!HC && !VC) {
     // two columns per lane (16-byte gathers) where the rows, the column
     // range and both vectors are 16-byte aligned
