@@ -3,7 +3,7 @@
 # smoke, the default bench line, bench.py under rocprofv3, and the kron
 # entries' kernel statistics and traffic.
 set -o pipefail
-export RUN=${RUN:-r4final7}
+export RUN=${RUN:-r4final9}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$RUN
 bash tools/gpu_step.sh \
