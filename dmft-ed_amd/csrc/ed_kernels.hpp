@@ -317,8 +317,16 @@ struct EpiStore {
   V* scratch() const { return hv; }  // where a two-pass H·v puts its first pass
   __device__ __forceinline__ bool skip() const { return false; }
   __device__ __forceinline__ void prepare() {}
+  // non-temporal: the Hv stream evicts fewer of the gathered vector's lines
+  // from L2 (same-process A/B at N28: stored complex 0.364 -> 0.350 ms,
+  // k_direct 0.170 -> 0.164 ms, stored real neutral)
   __device__ __forceinline__ double row(int64_t i, V acc, V) {
-    hv[i] = acc;
+    if constexpr (VC) {
+      typedef double d2 __attribute__((ext_vector_type(2)));
+      __builtin_nontemporal_store(d2{acc.x, acc.y}, (d2*)(hv + i));
+    } else {
+      __builtin_nontemporal_store(acc, hv + i);
+    }
     return 0.0;
   }
   template <int NT = kBlock>
@@ -1391,9 +1399,9 @@ __global__ void __launch_bounds__(kBlock) k_kron_dw(KronArgs<HC> K, const uint32
             a1 = add(a1, mul(h, g[r][k].y));
           }
         const int i = (r0 + r) * du + iu;
-        // the plain store epilogue writes Hv non-temporally: fewer of the
-        // chunk's V lines evicted by the Hv stream (N28 pass D FETCH 275 ->
-        // 257 MB, H·v -1.5 %)
+        // the plain store epilogue writes Hv non-temporally (as EpiStore::row):
+        // fewer of the chunk's V lines evicted by the Hv stream (N28 pass D
+        // FETCH 275 -> 257 MB, H·v -1.5 %); one 16-byte store here
         if constexpr (std::is_same_v<Epi, EpiStore<VC>>) {
           __builtin_nontemporal_store(d2{a0, a1}, (d2*)(epi.hv + i));
         } else {
