@@ -832,7 +832,7 @@ __global__ void __launch_bounds__(kBlock) k_spmv_pk(const val_t<HC>* __restrict_
 // evaluated once per sector by k_gen_diag into a vector (8 or 16 B per row).
 // The two directions of a hop on up levels are one op (kDirXor, build_direct):
 // ~half the per-lane evaluations of a normal-mode row.
-// Round-4 counters (nonSU2 N26, tools/r4_call1.sh): the kernel issued ~20
+// Round-4 counters (nonSU2 N26, an SQ_* pass of tools/spmv_probe.py): the kernel issued ~20
 // VALU and ~22 SALU instructions per op (per-op kind branches, per-lane
 // selects and sign assembly) and was issue-bound, not L1-bound.
 constexpr int kDirBlock = 1024;

@@ -131,7 +131,7 @@ ED_HD double jw_sign(uint32_t in, int b) {
   return (__builtin_popcount(below) & 1) ? -1.0 : 1.0;
 }
 
-// Local interaction on the diagonal, stored/Hint.f90:117-155 (= direct/HxVint.f90:1-47).
+// Local interaction on the diagonal, stored/Hint.f90:11-49 (= direct/HxVint.f90:1-47).
 // upbits/dwbits: impurity occupations n_{o,up} = bit o of upbits, n_{o,dw} = bit o of dwbits.
 ED_HD double hint_value(const EdModel& M, uint32_t upbits, uint32_t dwbits) {
   const int norb = M.norb;
@@ -173,7 +173,7 @@ ED_HD void gen_diag(const EdModel& M, uint32_t m, double* dre, double* dim_) {
   // dynamically indexed arrays would spill to scratch on the GPU)
 #define nup(o) ((double)bit(m, (o)))
 #define ndw(o) ((double)bit(m, (o) + ns))
-  // ---- diagonal: stored/Himp.f90:11-16, merged with Hint.f90:119-155 and
+  // ---- diagonal: stored/Himp.f90:11-16, merged with Hint.f90:11-49 and
   //      Hbath.f90:13-27 / :33-40 (sp_insert_element adds into the first slot).
   double dr = 0.0, di = 0.0;
   for (int o = 0; o < norb; o++) {
@@ -267,7 +267,7 @@ ED_HD void gen_row(const EdModel& M, uint32_t m, Acc& acc) {
         }
     }
   }
-  // ---- stored/Hint.f90:169-229 spin exchange and pair hopping
+  // ---- stored/Hint.f90:60-123 spin exchange and pair hopping
   if (norb > 1 && M.jhflag) {
     for (int io = 0; io < norb; io++)
       for (int jo = 0; jo < norb; jo++)
@@ -350,7 +350,7 @@ ED_HD void gen_row(const EdModel& M, uint32_t m, Acc& acc) {
         }
       }
   }
-  // ---- stored/Himp_bath.f90:192-249 spin-conserving hybridisation
+  // ---- stored/Himp_bath.f90:10-67 spin-conserving hybridisation
   for (int o = 0; o < norb; o++)
     for (int k = 0; k < nbath; k++) {
       int ms = M.stride[o][k];
@@ -373,7 +373,7 @@ ED_HD void gen_row(const EdModel& M, uint32_t m, Acc& acc) {
         }
       }
     }
-  // ---- stored/Himp_bath.f90:253-310 nonSU2 spin-flip hybridisation (no u/=0 test)
+  // ---- stored/Himp_bath.f90:70-128 nonSU2 spin-flip hybridisation (no u/=0 test)
   if (M.mode == ED_MODE_NONSU2 && M.bath != ED_BATH_REPLICA) {
     for (int o = 0; o < norb; o++)
       for (int k = 0; k < nbath; k++) {
@@ -494,7 +494,7 @@ inline void direct_candidates(const EdModel& M, Vec& out) {
           if (hr != 0.0 || hi != 0.0) hop(io + is * ns, jo + js * ns, hr, -hi);
         }
     }
-  // stored/Hint.f90:169-229
+  // stored/Hint.f90:60-123
   if (norb > 1 && M.jhflag) {
     for (int io = 0; io < norb; io++)
       for (int jo = 0; jo < norb; jo++) {
@@ -554,7 +554,7 @@ inline void direct_candidates(const EdModel& M, Vec& out) {
           if (cb.finish(dd, 0.0)) out.push_back(cb.c);
         }
       }
-  // stored/Himp_bath.f90:192-249
+  // stored/Himp_bath.f90:10-67
   for (int o = 0; o < norb; o++)
     for (int k = 0; k < nbath; k++) {
       const int ms = M.stride[o][k];
@@ -567,7 +567,7 @@ inline void direct_candidates(const EdModel& M, Vec& out) {
         hop(a, b, hr, -hi);  // bit a = 0, bit b = 1: c+_a c_b
       }
     }
-  // stored/Himp_bath.f90:253-310 (no u /= 0 test)
+  // stored/Himp_bath.f90:70-128 (no u /= 0 test)
   if (M.mode == ED_MODE_NONSU2 && M.bath != ED_BATH_REPLICA)
     for (int o = 0; o < norb; o++)
       for (int k = 0; k < nbath; k++) {

@@ -103,10 +103,10 @@ def farm_diag(cfg: EDConfig, opt: Optional[DiagOptions] = None, *, device: int =
     secs = [s for s in diag_sectors(cfg) if sectors is None or s.isector in set(sectors)]
     costs = [sector_cost(cfg, s, opt) for s in secs]
     local: Dict[int, SectorResult] = {}
-    if dist and world > 1 and opt.farm_schedule == "dynamic":
+    take = _global_queue(dist, len(secs)) if dist and world > 1 and opt.farm_schedule == "dynamic" else None
+    if take is not None:
         order = sorted(range(len(secs)), key=lambda i: (-costs[i], i))   # the same on every rank
         qsecs = [secs[i] for i in order]
-        take = _global_queue(dist, len(qsecs))
         for r in solve_many(cfg, qsecs, opt, device, solver=solver, take_global=take):
             if r is not None:
                 local[r.isector] = r
@@ -143,6 +143,40 @@ def farm_diag(cfg: EDConfig, opt: Optional[DiagOptions] = None, *, device: int =
 
 
 _QUEUE_CALLS = [0]
+_QUEUE_STORE: list = []      # [store] once connected, [None] once found unusable
+QUEUE_FALLBACK: list = []    # reasons the dynamic schedule fell back to LPT (for logs / tests)
+
+
+def _queue_store(dist):
+    """A client of the job's rendezvous key-value server, through the public
+    torch.distributed.TCPStore API: MASTER_ADDR:MASTER_PORT is the server that
+    torchrun's agent (or rank 0's env:// init) keeps alive for the whole job.
+    Every rank connects as a client (is_master=False); keys live under the
+    prefix "edgpu_farm/".  None (and the reason recorded) when the variables are
+    absent or the connection fails: the farm then runs the static LPT
+    partition, which needs no store."""
+    if _QUEUE_STORE:
+        return _QUEUE_STORE[0]
+    import datetime
+    import os
+    import sys
+
+    addr, port = os.environ.get("MASTER_ADDR"), os.environ.get("MASTER_PORT")
+    store, why = None, None
+    if not addr or not port:
+        why = "MASTER_ADDR/MASTER_PORT not set (process group not from env://)"
+    else:
+        try:
+            tcp = dist.TCPStore(addr, int(port), is_master=False, timeout=datetime.timedelta(seconds=60))
+            store = dist.PrefixStore("edgpu_farm/", tcp)
+        except Exception as e:   # noqa: BLE001 - any connection failure means: no dynamic queue
+            why = f"TCPStore({addr}:{port}) client failed: {type(e).__name__}: {e}"
+    if store is None:
+        QUEUE_FALLBACK.append(why)
+        print(f"edgpu.farm: dynamic sector queue unavailable ({why}); using the LPT partition",
+              file=sys.stderr, flush=True)
+    _QUEUE_STORE.append(store)
+    return store
 
 
 def _global_queue(dist, n: int):
@@ -151,14 +185,22 @@ def _global_queue(dist, n: int):
     (every rank makes the same sequence of farm_diag calls, so the keys
     agree); the store's add is atomic, each index goes to exactly one taker.
     A barrier first, so no rank takes from the counter of a call the others
-    have not reached."""
+    have not reached.  Returns None when no store is reachable (every rank
+    decides the same way: a collective agreement on the store's availability
+    precedes the first use, so ranks never mix the two schedules)."""
     import threading
 
-    from torch.distributed import distributed_c10d as c10d
+    import torch
 
+    store = _queue_store(dist)
+    ok = torch.tensor([1 if store is not None else 0], dtype=torch.int64)
+    if dist.get_backend() == "nccl":
+        ok = ok.cuda()
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if int(ok.item()) == 0:
+        return None
     _QUEUE_CALLS[0] += 1
-    key = f"edgpu_farm_queue_{_QUEUE_CALLS[0]}"
-    store = c10d._get_default_store()
+    key = f"queue_{_QUEUE_CALLS[0]}"
     dist.barrier()
     lock = threading.Lock()   # one store client per process: serialise its use
     done = [False]

@@ -197,7 +197,7 @@ static inline cplx diag_hybr(const model_t* M, int ispin, int o, int k) {
   return mkc(p->bath_vr_re[k], p->bath_vr_im[k]);
 }
 
-/* Hint diagonal (shared by stored Hint.f90:117-155 and direct HxVint.f90:1-47) */
+/* Hint diagonal (shared by stored Hint.f90:11-49 and direct HxVint.f90:1-47) */
 static double hint_diag(const model_t* M, const double* nup, const double* ndw) {
   const ed_params* p = M->p;
   const int norb = M->norb;
@@ -297,13 +297,13 @@ static int stored_row(const model_t* M, const uint32_t* map, int64_t dim, int64_
         }
     }
   }
-  /* ---- stored/Hint.f90:117-162  density-density (+ Hartree) merged on (i,i) */
+  /* ---- stored/Hint.f90:11-56  density-density (+ Hartree) merged on (i,i) */
   {
     double h = hint_diag(M, nup, ndw);
     j = i + 1;
     INSERT(mkc(h, 0.0));
   }
-  /* ---- stored/Hint.f90:169-196  spin exchange */
+  /* ---- stored/Hint.f90:60-90  spin exchange */
   if (norb > 1 && M->jhflag) {
     for (int io = 0; io < norb; io++)
       for (int jo = 0; jo < norb; jo++) {
@@ -319,7 +319,7 @@ static int stored_row(const model_t* M, const uint32_t* map, int64_t dim, int64_
         }
       }
   }
-  /* ---- stored/Hint.f90:202-229  pair hopping */
+  /* ---- stored/Hint.f90:93-123  pair hopping */
   if (norb > 1 && M->jhflag) {
     for (int io = 0; io < norb; io++)
       for (int jo = 0; jo < norb; jo++) {
@@ -422,7 +422,7 @@ static int stored_row(const model_t* M, const uint32_t* map, int64_t dim, int64_
         }
       }
   }
-  /* ---- stored/Himp_bath.f90:192-249  spin-conserving hybridisation */
+  /* ---- stored/Himp_bath.f90:10-67  spin-conserving hybridisation */
   for (int o = 0; o < norb; o++)
     for (int k = 0; k < nbath; k++) {
       int ms = M->stride[o][k];
@@ -453,7 +453,7 @@ static int stored_row(const model_t* M, const uint32_t* map, int64_t dim, int64_
         INSERT(cscale2(mkc(hd.re, -hd.im), sg1, sg2));
       }
     }
-  /* ---- stored/Himp_bath.f90:253-310  nonSU2 spin-flip hybridisation (inserted even if u=0) */
+  /* ---- stored/Himp_bath.f90:70-128  nonSU2 spin-flip hybridisation (inserted even if u=0) */
   if (M->mode == ED_MODE_NONSU2 && M->bath != ED_BATH_REPLICA) {
     for (int o = 0; o < norb; o++)
       for (int k = 0; k < nbath; k++) {

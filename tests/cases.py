@@ -80,7 +80,7 @@ def replica_cplx():
 
 def replica_cplx_vr():
     """Complex replica hybridisation vr: the reference conjugates it in BOTH
-    hopping directions (stored/Himp_bath.f90:202 and :214), so its stored H is
+    hopping directions (stored/Himp_bath.f90:20 and :32), so its stored H is
     complex-symmetric in that block, not Hermitian (and directMatVec_cc uses the
     unconjugated value).  Parity target = the stored semantics."""
     cfg = replica_cplx()

@@ -71,14 +71,19 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, q, cfg_kw, method, schedule="dynamic"):
+def _worker(rank, world, port, q, cfg_kw, method, schedule="dynamic", init="env"):
     import torch.distributed as dist
     from oracle_solver import solve_sector_oracle
-    from edgpu.farm import broadcast_vector
+    from edgpu.farm import QUEUE_FALLBACK, broadcast_vector
 
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if init == "env":
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    else:   # a file rendezvous: no MASTER_ADDR/PORT, so no key-value server to reach
+        os.environ.pop("MASTER_ADDR", None)
+        os.environ.pop("MASTER_PORT", None)
+        dist.init_process_group("gloo", rank=rank, world_size=world, init_method=init)
     cfg = make_config(**cfg_kw)
     res = farm_diag(cfg, DiagOptions(lanc_method=method, farm_schedule=schedule), solver=solve_sector_oracle)
     gs_owner = res.owners[0]
@@ -86,9 +91,52 @@ def _worker(rank, world, port, q, cfg_kw, method, schedule="dynamic"):
     dim = [s for s in setup_pointers(cfg) if s.isector == res.states.sectors[0]][0].dim
     vb = broadcast_vector(v, gs_owner, dim, cplx=True)
     q.put((rank, res.states.energies, res.states.sectors, res.owners, res.assignment,
-           float(np.linalg.norm(vb))))
+           float(np.linalg.norm(vb)), list(QUEUE_FALLBACK)))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _run_ranks(world, cfg_kw, method, schedule, init="env"):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, cfg_kw, method, schedule, init))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return sorted(out, key=lambda o: o[0])
+
+
+@pytest.mark.parametrize("world,init", [(4, "env"), (2, "file")])
+def test_gloo_dynamic_queue(world, init, tmp_path):
+    """The dynamic sector queue through the public TCPStore client: 4 ranks
+    (processes) take sectors from one counter and reproduce the serial state
+    list; with a file rendezvous (no MASTER_ADDR/PORT) every rank falls back
+    to the LPT partition, says why, and still reproduces it."""
+    from oracle_solver import solve_sector_oracle
+
+    cfg_kw, method = dict(Norb=1, Nbath=5), "lanczos"
+    cfg = make_config(**cfg_kw)
+    serial = farm_diag(cfg, DiagOptions(lanc_method=method), solver=solve_sector_oracle)
+    init_arg = "env" if init == "env" else f"file://{tmp_path}/rdzv"
+    out = _run_ranks(world, cfg_kw, method, "dynamic", init_arg)
+    for rank, en, secs, owners, assignment, vnorm, fallback in out:
+        assert secs == serial.states.sectors
+        np.testing.assert_allclose(en, serial.states.energies, rtol=0, atol=1e-12)
+        assert abs(vnorm - 1.0) < 1e-10
+        if init == "env":
+            assert fallback == []
+        else:
+            assert len(fallback) == 1 and "MASTER_ADDR" in fallback[0]
+    assign = out[0][4]
+    assert all(o[4] == assign for o in out)
+    assert sorted(i for a in assign for i in a) == sorted(s.isector for s in setup_pointers(cfg))
+    if init != "env":    # LPT: every rank got work
+        assert all(len(a) > 0 for a in assign)
 
 
 @pytest.mark.parametrize("schedule", ["dynamic", "lpt"])
@@ -102,18 +150,9 @@ def test_gloo_farm_matches_serial(cfg_kw, method, schedule):
 
     cfg = make_config(**cfg_kw)
     serial = farm_diag(cfg, DiagOptions(lanc_method=method), solver=solve_sector_oracle)
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, cfg_kw, method, schedule)) for r in range(2)]
-    for p in procs:
-        p.start()
-    out = [q.get(timeout=300) for _ in range(2)]
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    out.sort()
-    for rank, en, secs, owners, assignment, vnorm in out:
+    out = _run_ranks(2, cfg_kw, method, schedule)
+    for rank, en, secs, owners, assignment, vnorm, fallback in out:
+        assert fallback == []
         assert secs == serial.states.sectors
         np.testing.assert_allclose(en, serial.states.energies, rtol=0, atol=1e-12)
         assert abs(vnorm - 1.0) < 1e-10           # broadcast delivered the owner's unit vector

@@ -106,7 +106,7 @@ def test_plain_lanczos_restatement():
 
 def test_complex_vr_reference_quirk():
     """Complex replica vr: stored H has conj(vr) on both (i,j) and (j,i) of a
-    hybridisation pair (stored/Himp_bath.f90:202,214) -> symmetric, not
+    hybridisation pair (stored/Himp_bath.f90:20,32) -> symmetric, not
     Hermitian, in that block.  The oracle reproduces the stored semantics."""
     from cases import replica_cplx_vr
 
