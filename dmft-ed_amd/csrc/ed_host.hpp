@@ -32,9 +32,8 @@ static inline int fail(int code, const std::string& msg) {
 namespace edg {
 
 // Kronecker register layout (MODE 4): rows per thread that fit the register
-// budget with E hop slots (real vectors / complex vectors on 1024 threads)
+// budget with E hop slots (real vectors)
 constexpr bool pkr_fits(int E, int RPT) { return RPT * (3 * E + 8) + 3 * E <= 216; }
-constexpr bool pkr_fits_c(int E, int RPT) { return E == 4 ? RPT <= 5 : RPT <= 2; }
 // complex vectors, 512-thread layout (-Rpass-analysis: spill-free forms)
 constexpr bool pkr_fits_c512(int E, int RPT) { return E == 4 ? RPT <= 10 : RPT <= 6; }
 // register-resident ELL words per thread (MODE 2/3) without spills
@@ -48,9 +47,7 @@ static inline int persist_rpt01(int64_t dim) {
 // The sector fields that pick a k_lanc_persist instantiation
 struct PersistGeom {
   int64_t dim = 0;
-  int preg_E = 0, preg_rpt = 0, kreg_W = 0, kreg_rpt = 0, pkr_E = 0, pkr_rpt = 0, pkr_rpt_c = 0;
-  int pkr_c1024 = 0;  // complex MODE 4 in the 1024-thread layout (ED_OPT_PKRON_C1024)
-  int pkr_cslot = 0;  // complex MODE 4, 512 threads, slot-major LDS vector (ED_OPT_PKRON_CSLOT, A/B)
+  int preg_E = 0, preg_rpt = 0, kreg_W = 0, kreg_rpt = 0, pkr_E = 0, pkr_rpt = 0;
 };
 
 // Launch k_lanc_persist for (hc, vc, mode) on the geometry's template values;

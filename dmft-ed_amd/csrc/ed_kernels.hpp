@@ -439,65 +439,6 @@ __device__ __forceinline__ double2 ld_wt(const double2* p) {
                       __hip_atomic_load((const double*)p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
-__device__ __forceinline__ void lanc_set_beta(double tot, LancState* st, double* beta_out);
-
-// Whole Lanczos step in ONE kernel, for grids of at most kTicketMaxBlocks
-// blocks (small sectors, where launch and reduction latency dominate): part A
-// as EpiLancA but P and W stored write-through; the last block to take the
-// ticket holds alpha and runs part B (w -= alpha v, R <- w, beta = |w|) over
-// all rows itself, reading P/W with sc1 loads.  Saves one launch and one
-// grid reduction per step.
-template <bool VC>
-struct EpiLancFused {
-  using V = val_t<VC>;
-  LancState* st;
-  V* P;
-  V* W;
-  V* R;
-  V* basis;
-  int64_t dim;
-  double* alpha_out;
-  double* beta_out;
-  RedSlot slot;
-  double invb, b;
-  V* bcol;
-  V* scratch() const { return W; }  // W is rewritten row by row by row() itself
-  __device__ __forceinline__ bool skip() const { return st->done != 0; }
-  __device__ __forceinline__ void prepare() {
-    invb = st->invb;
-    b = st->beta;
-    bcol = basis ? basis + (int64_t)st->iter * dim : nullptr;
-  }
-  __device__ __forceinline__ double row(int64_t i, V acc, V xi) {
-    V v = scl(invb, xi);
-    V h = scl(invb, acc);
-    V w = sub(h, scl(b, P[i]));
-    st_wt(P + i, v);
-    st_wt(W + i, w);
-    if (bcol) bcol[i] = v;
-    return redot(v, w);
-  }
-  template <int NT = kBlock>
-  __device__ __forceinline__ void finish(double part) {
-    double alpha;
-    if (!grid_reduce_last<NT>(part, slot, &alpha)) return;
-    // last block: R is no longer read by anyone (every block took its ticket
-    // after its gathers completed)
-    double np = 0.0;
-    for (int64_t i = threadIdx.x; i < dim; i += NT) {
-      V w = sub(ld_wt(W + i), scl(alpha, ld_wt(P + i)));
-      R[i] = w;
-      np += redot(w, w);
-    }
-    const double tot = block_sum<NT>(np);
-    if (threadIdx.x == 0) {
-      st->alpha = alpha;
-      alpha_out[st->iter] = alpha;
-      lanc_set_beta(tot, st, beta_out);
-    }
-  }
-};
-
 // Two-pass finishing kernels of one Lanczos step (one block of kBlock threads).
 static __global__ void __launch_bounds__(kBlock) k_lanc_fin_a(const double* __restrict__ partials, int n,
                                                        LancState* st, double* alpha_out) {
@@ -509,7 +450,6 @@ static __global__ void __launch_bounds__(kBlock) k_lanc_fin_a(const double* __re
   }
 }
 __device__ __forceinline__ void lanc_set_beta(double tot, LancState* st, double* beta_out) {
-  // (defined here, declared above EpiLancFused)
   const double b = sqrt(tot);
   const int it = st->iter;
   beta_out[it + 1] = b;

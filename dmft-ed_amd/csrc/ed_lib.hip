@@ -12,7 +12,6 @@
 #include <string.h>
 
 #include <algorithm>
-#include <condition_variable>
 #include <mutex>
 #include <string>
 #include <map>
@@ -134,7 +133,6 @@ struct ed_sector {
   int pkr_state = 0;        // 0 not tried, -1 ineligible, 1 tables ready
   int pkr_src = -1;         // path the tables came from (0 stored SELL, 2 hop tables)
   int pkr_E = 0, pkr_rpt = 0, pkr_du = 0, pkr_dd = 0, pkr_degu = 0, pkr_degd = 0;
-  int pkr_rpt_c = 0;        // rows per thread of the complex-vector layout (1024 threads), 0: none
   const int32_t *d_kupc = nullptr, *d_kdwc = nullptr;
   const double *d_kupv = nullptr, *d_kdwv = nullptr, *d_kdiag = nullptr;
   // graph cache for Lanczos iterations
@@ -981,7 +979,9 @@ static bool kron2_on(const ed_sector* s, int path, int vc) {
 // 0.0155 / 0.0161 ms).
 static int kron_dw_grid(const ed_sector* s, bool vc) {
   if (vc) return kKronDwGrid / 2;
-  return (s->K.dimup % 2 == 0 && !(s->opts & ED_OPT_KRON_DW1)) ? kKronDwGrid2 : kKronDwGrid;
+  // (a launch whose pointers are not 16-byte aligned falls back to the
+  // one-column form on this same grid: hxv_blocks() must match the launch)
+  return s->K.dimup % 2 == 0 ? kKronDwGrid2 : kKronDwGrid;
 }
 static int hxv_blocks(const ed_sector* s, int path, int vc = 0) {
   if (kron2_on(s, path, vc)) return kron_dw_grid(s, vc);
@@ -1061,9 +1061,11 @@ static int launch_kron_dw(ed_sector* s, const void* x, const void* ypart, Epi ep
   const int grid = kron_dw_grid(s, VC);
   if constexpr (!HC && !VC) {
     // two columns per lane (16-byte gathers) where the rows, the column
-    // range and both vectors are 16-byte aligned
-    const bool a16 = ((uintptr_t)x % 16) == 0 && ((uintptr_t)ypart % 16) == 0;
-    if (!(s->opts & ED_OPT_KRON_DW1) && ld % 2 == 0 && ncols % 2 == 0 && a16) {
+    // range, both vectors and (plain store: one 16-byte store per lane) the
+    // output are 16-byte aligned
+    bool a16 = ((uintptr_t)x % 16) == 0 && ((uintptr_t)ypart % 16) == 0;
+    if constexpr (std::is_same_v<Epi, EpiStore<VC>>) a16 = a16 && ((uintptr_t)epi.hv % 16) == 0;
+    if (ld % 2 == 0 && ncols % 2 == 0 && a16) {
       if (K.degD == 8)
         hipLaunchKernelGGL((k_kron_dw<HC, VC, 8, Epi, 2>), dim3(grid), dim3(kBlock), 0, st, kron_args<HC>(s),
                            K.dwo, K.dwi, (const H*)K.dwdict, K.ndwdict, (const V*)x, (const V*)ypart, epi, ld,
@@ -1247,21 +1249,6 @@ static int lanc_iter(ed_sector* s, int path, bool basis, hipStream_t st) {
   LancWS& w = s->ws;
   const int g1 = hxv_blocks(s, path, VC), g2 = grid_for(s->dim);
   const bool two1 = g1 > kTicketMaxBlocks, two2 = g2 > kTicketMaxBlocks;
-  // single-kernel step: opt-in (measured slower on c2: 13.0 vs 8.9 us/step —
-  // the last block's serial sc1 pass over all rows is latency-bound)
-  if (!two1 && (s->opts & ED_OPT_FUSED_STEP)) {
-    EpiLancFused<VC> f;
-    f.st = w.st;
-    f.P = (val_t<VC>*)w.P;
-    f.W = (val_t<VC>*)w.W;
-    f.R = (val_t<VC>*)w.R;
-    f.basis = basis ? (val_t<VC>*)w.basis : nullptr;
-    f.dim = s->dim;
-    f.alpha_out = w.alpha;
-    f.beta_out = w.beta;
-    f.slot = RedSlot{w.partials, w.counter};
-    return launch_hxv<VC>(s, path, w.R, f, st);
-  }
   EpiLancA<VC> e;
   e.st = w.st;
   e.P = (val_t<VC>*)w.P;
@@ -1403,9 +1390,6 @@ static int pkr_geom(ed_sector* s, int64_t du, int64_t dd, int degu, int degd) {
   if (!RPT || !pkr_fits(E, RPT)) return -1;
   s->pkr_E = E;
   s->pkr_rpt = RPT;
-  const int64_t Gc = kPBlock / du, rc = (dd + Gc - 1) / Gc;
-  const int RC = rc <= 2 ? 2 : rc <= 5 ? (int)rc : 0;
-  s->pkr_rpt_c = (RC && pkr_fits_c(E, RC)) ? RC : 0;
   s->pkr_du = (int)du;
   s->pkr_dd = (int)dd;
   s->pkr_degu = degu;
@@ -1593,9 +1577,7 @@ static int64_t persist_vrows(const ed_sector* s, int mode, int vc = 0) {
   switch (mode) {
     case 2: return (int64_t)kPRegBlock * s->preg_rpt;
     case 3: return (int64_t)kPRegBlock * s->kreg_rpt;
-    case 4:
-      return (vc && (s->opts & ED_OPT_PKRON_C1024)) ? (int64_t)kPBlock * s->pkr_rpt_c
-                                                    : (int64_t)kPRegBlock * s->pkr_rpt;
+    case 4: return (int64_t)kPRegBlock * s->pkr_rpt;
     default: return (int64_t)kPBlock * persist_rpt01(s->dim);
   }
 }
@@ -1614,7 +1596,7 @@ static int persist_mode(ed_sector* s, int vc, int path) {
   if (!(o & (ED_OPT_NO_PKRON | ED_OPT_NO_PREG)) &&
       ((path == 0 && !(o & ED_OPT_PERSIST_STORED) && build_pkron_stored(s) > 0) ||
        (path == 2 && build_pkron_direct(s) > 0)) &&
-      (vc == 0 || ((s->opts & ED_OPT_PKRON_C1024) ? s->pkr_rpt_c > 0 : pkr_fits_c512(s->pkr_E, s->pkr_rpt))) &&
+      (vc == 0 || pkr_fits_c512(s->pkr_E, s->pkr_rpt)) &&
       persist_lds(s, vc, 4) <= kLdsBudget)
     return 4;
   // stored: MODE 2 (ELL entries in registers; c2 4.6 us/step) by default.
@@ -1667,14 +1649,10 @@ static int64_t persist_lds(const ed_sector* s, int vc, int mode) {
   const int64_t vs = vc ? 16 : 8, vr = persist_vrows(s, mode, vc);
   int64_t lds = ((vr * vs + 15) & ~(int64_t)15);
   if (mode == 4) {
-    // slot-major vector: RPT slots of NT + 1 elements (k_lanc_persist VSLOT;
-    // the 512-thread complex form keeps the natural order)
-    const bool c1024 = vc && (s->opts & ED_OPT_PKRON_C1024);
-    if (!vc || c1024 || (s->opts & ED_OPT_PKRON_CSLOT)) {
-      const int64_t nt = c1024 ? kPBlock : kPRegBlock;
-      lds = (((vr + vr / nt) * vs + 15) & ~(int64_t)15);
-    }
-    return lds + (vc ? vr * 8 + (int64_t)s->pkr_E * (s->pkr_dd + s->pkr_du) * 8 : 0);
+    // real vectors: slot-major, RPT slots of NT + 1 elements (k_lanc_persist
+    // VSLOT); complex vectors: natural order + the down-hop value table
+    if (!vc) return (((vr + vr / kPRegBlock) * vs + 15) & ~(int64_t)15);
+    return lds + (int64_t)s->pkr_E * s->pkr_dd * 8;
   }
   if (mode == 2) {
     const int64_t hs = s->hc ? 16 : 8;
@@ -1705,9 +1683,6 @@ static PersistGeom persist_geom(const ed_sector* s) {
   g.kreg_rpt = s->kreg_rpt;
   g.pkr_E = s->pkr_E;
   g.pkr_rpt = s->pkr_rpt;
-  g.pkr_rpt_c = s->pkr_rpt_c;
-  g.pkr_c1024 = (s->opts & ED_OPT_PKRON_C1024) ? 1 : 0;
-  g.pkr_cslot = (s->opts & ED_OPT_PKRON_CSLOT) ? 1 : 0;
   return g;
 }
 
@@ -2036,37 +2011,6 @@ __global__ void k_hash_vec(double* v, int64_t n, uint64_t seed) {
 // stay on the device; one expansion sweep (j0 .. m-1) is captured once per
 // start column into a hipGraph (j0 = 0 and j0 = nkeep), so a restart cycle is
 // one graph launch + one host sync for the m x m projected problem.
-// Workgroups of persistent sweeps in flight in this process.  A sweep's
-// workgroups wait for each other at grid barriers, so all of them must be
-// resident at once; concurrent sweeps (farm worker threads) whose workgroups
-// together exceed what the chip holds would each keep part of their grid
-// spinning while the rest cannot be placed.  k_trl_sweep admits 2 workgroups
-// per CU (launch bounds); the budget is half of that, so two processes
-// sharing a GPU fit as well.  Blocking acquire (no fallback to the graph
-// sweep: results do not depend on the schedule).
-static constexpr int kPSweepBudget = 256;
-struct PSweepBudget {
-  std::mutex mu;
-  std::condition_variable cv;
-  int used = 0;
-};
-static PSweepBudget g_psb;
-struct PSweepSlot {
-  int n;
-  explicit PSweepSlot(int n_) : n(n_) {
-    std::unique_lock<std::mutex> lk(g_psb.mu);
-    g_psb.cv.wait(lk, [&] { return g_psb.used + n <= kPSweepBudget; });
-    g_psb.used += n;
-  }
-  ~PSweepSlot() {
-    {
-      std::lock_guard<std::mutex> lk(g_psb.mu);
-      g_psb.used -= n;
-    }
-    g_psb.cv.notify_all();
-  }
-};
-
 template <bool VC>
 struct Trlan {
   using V = val_t<VC>;
@@ -2087,12 +2031,6 @@ struct Trlan {
   int* lof = nullptr;     // device: the current step's update was local-only
   double *Y = nullptr, *npart = nullptr, *alpha = nullptr, *beta = nullptr;
   double *npA = nullptr, *npB = nullptr;  // |w|^2 partials before / after the first CGS pass (DGKS)
-  // persistent sweep (k_trl_sweep): grid, ping-pong residuals, barrier words
-  int PG = 0;                    // 0: multi-kernel sweeps
-  V* wb = nullptr;
-  unsigned int* bar = nullptr;   // [0] arrival counter, [1] abort word
-  unsigned int bar_count = 0;    // counter value after the last launch
-  unsigned int abort_h = 0;      // abort word read back with alpha/beta
   double* hp = nullptr;          // pinned staging (trlan_pinned)
   std::vector<void*> mine;
   std::vector<std::pair<int, hipGraphExec_t>> graphs;
@@ -2256,59 +2194,8 @@ struct Trlan {
     CK(orth(j + 1, w, j, j + 1 < m ? col(Vb, j + 1) : nullptr, loc ? 1 : 0));
     return ED_OK;
   }
-  template <bool HC, bool PK, int NC>
-  void psweep_launch(const TrlSweepArgs<HC>& a) {
-    const size_t lds = PG == 1 ? (size_t)dim * sizeof(V) : 0;  // solo: the gathered vector
-    hipLaunchKernelGGL((k_trl_sweep<HC, VC, PK, NC>), dim3(PG), dim3(kBlock), lds, st, a);
-  }
-  template <bool HC>
-  int psweep_t(int j0) {
-    using H = val_t<HC>;
-    TrlSweepArgs<HC> a;
-    a.diag = (const H*)s->d_diag;
-    a.sptr = s->d_sptr;
-    a.words = s->d_words;
-    a.dict = (const H*)s->d_pdict;
-    a.cols = s->d_cols;
-    a.vals = (const H*)s->d_vals;
-    a.dim = dim;
-    a.nslice = s->nslice;
-    a.Vb = Vb;
-    a.wbuf = wb;
-    a.wout = w;
-    a.p1 = part;
-    a.p2 = part2;
-    a.pn = npart;
-    a.alpha = alpha;
-    a.beta = beta;
-    a.bar = bar;
-    a.bar0 = bar_count;
-    a.j0 = j0;
-    a.m = m;
-    const bool pk = s->d_words != nullptr;
-    if (m <= 24) {
-      if (pk) psweep_launch<HC, true, 24>(a);
-      else psweep_launch<HC, false, 24>(a);
-    } else {
-      if (pk) psweep_launch<HC, true, 32>(a);
-      else psweep_launch<HC, false, 32>(a);
-    }
-    HIPCK(hipGetLastError());
-    bar_count += (unsigned int)(3 * PG * (m - j0));
-    HIPCK(hipMemcpyAsync(&abort_h, bar + 1, sizeof(unsigned int), hipMemcpyDeviceToHost, st));
-    return ED_OK;
-  }
   int sweep(int j0) {
     const int n = m - j0;
-    if constexpr (!VC) {
-      if (PG > 0 && m <= 32) {  // one launch for the whole sweep
-        PSweepSlot slot(PG);      // held until the sweep has finished
-        CK(psweep_t<false>(j0));
-        HIPCK(hipStreamSynchronize(st));
-        nhv += n;
-        return ED_OK;
-      }
-    }
     hipGraphExec_t ge = nullptr;
     for (auto& g : graphs)
       if (g.first == j0) ge = g.second;
@@ -2352,11 +2239,6 @@ static double* trlan_pinned() {
 
 // blocks of the O(dim) Krylov sweeps
 static constexpr int kTrlanGridCap = 512;  // (1024 until round 4: 512 measured 13 % faster per large-sector solve, tools/trlan_ab.py --grid)
-// persistent sweeps (k_trl_sweep): sector size limit and rows per workgroup
-static constexpr int64_t kPSweepMaxDim = 131072;
-static constexpr int64_t kPSweepRows = 256;
-static constexpr int64_t kPSweepSolo = 2048;  // one workgroup, vector in LDS (<= 32 KB)
-
 // One thick-restart Lanczos solve on the columns [k0, m) of the basis; the
 // columns [0, k0) are locked (deflation: every new vector is orthogonalised
 // against them, their coefficients are not part of the projected matrix).
@@ -2401,7 +2283,6 @@ static int trlan_core(Trlan<VC>& T, int k0, int nev, int maxit, double tol, cons
       HIPCK(hipStreamSynchronize(st));
       std::copy(hal, hal + m, al.begin());
       std::copy(hbe, hbe + m, be.begin());
-      if (T.abort_h) return fail(ED_ERR_HIP, "persistent Krylov sweep: grid barrier timed out");
       int jb = -1;
       for (int j = j0; j < m; j++) {
         const int l = j - k0;
@@ -2559,7 +2440,7 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
   T.path = resolve_path(s, -1);
   T.st = s->stream;
   T.dim = s->dim;
-  T.G = (int)std::min<int64_t>(grid_for(s->dim), (s->opts & ED_OPT_TRLAN_G128) ? 128 : kTrlanGridCap);
+  T.G = (int)std::min<int64_t>(grid_for(s->dim), kTrlanGridCap);
   T.hp = trlan_pinned();
   if (!T.hp) return fail(ED_ERR_OOM, "pinned host staging buffer");
   T.fused = !(s->opts & ED_OPT_TRLAN_UNFUSED);
@@ -2592,17 +2473,6 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
   CK(T.alloc((void**)&T.alpha, (kTrlanMaxCols + 8) * sizeof(double)));
   CK(T.alloc((void**)&T.beta, (kTrlanMaxCols + 8) * sizeof(double)));
   CK(T.alloc((void**)&T.Y, (size_t)mcap * mcap * sizeof(double)));
-  // persistent sweeps: whole stored sectors up to kPSweepMaxDim rows, about
-  // kPSweepRows rows per workgroup (opt-in: ED_OPT_TRLAN_PSWEEP; measured
-  // slower than the multi-kernel sweeps)
-  // (real vectors: the complex instantiations spill at the 2-per-CU bound)
-  if (!VC && T.path == 0 && T.fused && s->row0 == 0 && s->nrows == dim && dim <= kPSweepMaxDim &&
-      (s->opts & ED_OPT_TRLAN_PSWEEP) && (s->d_words || s->d_cols)) {
-    T.PG = dim <= kPSweepSolo ? 1 : (int)std::min<int64_t>((dim + kPSweepRows - 1) / kPSweepRows, 128);
-    CK(T.alloc((void**)&T.wb, 2 * dim * vs));
-    CK(T.alloc((void**)&T.bar, 2 * sizeof(unsigned int)));
-    HIPCK(hipMemsetAsync(T.bar, 0, 2 * sizeof(unsigned int), T.st));
-  }
   hipStream_t st = T.st;
   const int g = grid_for(dim);
   T.m = m;
@@ -2629,7 +2499,7 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
       constexpr double kProbeTol = 1e-5;  // 1e-3 misses copies; 1e-4 and 1e-5 find them
       const double tprobe = std::max(tol, kProbeTol);
       const double cut = ev[nev - 1] - 1e-9 * std::max(1.0, fabs(ev[nev - 1]));
-      if (!(s->opts & ED_OPT_EIGH_FULLPROBE)) {
+      {
         // cheap screen first: a plain Lanczos run on the complement decides
         // most sectors (no missed eigenvalue); the thick-restart probe below
         // runs only when it finds one or cannot decide
@@ -2862,10 +2732,9 @@ int ed_sector_destroy(ed_sector* s) {
 
 // every defined ED_OPT_* bit (include/ed_gpu.h); any other bit is refused
 static constexpr int32_t kOptKnown =
-    ED_OPT_NO_PERSIST | ED_OPT_PERSIST_STORED | ED_OPT_NO_PREG | ED_OPT_NO_PKRON | ED_OPT_FUSED_STEP |
-    ED_OPT_SPLIT_SIMPLE | ED_OPT_NO_BATCH | ED_OPT_EIGH_NO_VERIFY | ED_OPT_TRLAN_UNFUSED | ED_OPT_TRLAN_NOFOLD |
-    ED_OPT_TRLAN_PSWEEP | ED_OPT_NO_GRAPH | ED_OPT_TRLAN_NOLOCAL | ED_OPT_TRLAN_NOSOLO | ED_OPT_TRLAN_FULLUPD |
-    ED_OPT_PKRON_C1024 | ED_OPT_TRLAN_G128 | ED_OPT_EIGH_FULLPROBE | ED_OPT_PKRON_CSLOT | ED_OPT_KRON_DW1;
+    ED_OPT_NO_PERSIST | ED_OPT_PERSIST_STORED | ED_OPT_NO_PREG | ED_OPT_NO_PKRON | ED_OPT_SPLIT_SIMPLE |
+    ED_OPT_NO_BATCH | ED_OPT_EIGH_NO_VERIFY | ED_OPT_TRLAN_UNFUSED | ED_OPT_TRLAN_NOFOLD | ED_OPT_NO_GRAPH |
+    ED_OPT_TRLAN_NOLOCAL | ED_OPT_TRLAN_NOSOLO | ED_OPT_TRLAN_FULLUPD;
 
 int ed_sector_set_options(ed_sector* s, int32_t opts) {
   if (!s) return fail(ED_ERR_ARG, "null");

@@ -168,7 +168,7 @@ __device__ __forceinline__ PRows persist_rows(int tid, int64_t dim, int du, int 
 // LDS holds r_k = b_k v_k UNNORMALISED: w is stored as soon as a_k is known
 // (all gathers of the step are behind the alpha barrier) and the next step
 // scales H r by 1/b — two barriers per step (alpha, beta), one LDS vector.
-template <bool HC, bool VC, int MODE, int RPT, int E = 1, int NT = kPBlock, bool CSLOT = false>
+template <bool HC, bool VC, int MODE, int RPT, int E = 1, int NT = kPBlock>
 __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
   using V = val_t<VC>;
   using H = val_t<HC>;
@@ -181,11 +181,10 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
   // multiple, so two slots' reads never merge into one ds_read2st64, which
   // costs what two ds_read_b64 do twice over); a gather of slot r then
   // addresses through a per-lane base plus the immediate r * VSLOT * size.
-  // (Not the 512-thread complex form: measured ~3 % slower per step and 18 %
-  // slower batched with it; that form keeps the natural row order.)
-  // (CSLOT: the slot layout for the 512-thread complex form too — A/B,
-  // ED_OPT_PKRON_CSLOT)
-  constexpr bool SLOT = MODE == 4 && (!(VC && NT != kPBlock) || CSLOT);
+  // (Not the complex-vector form: measured ~3 % slower per step (3.94-3.98
+  // against 3.82-3.86 us) and 18 % slower batched with it; that form keeps
+  // the natural row order.)
+  constexpr bool SLOT = MODE == 4 && !VC;
   constexpr int VSLOT = NT + 1;
   constexpr int VLDS = SLOT ? RPT * VSLOT : VROWS;  // LDS vector elements
   V* vl = (V*)smem;                // MODE 2/3 move it behind the dictionary
@@ -313,55 +312,31 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
   // rank as a byte offset inside the V row, value) once per thread; down-hop
   // entries (LDS byte address, value) and the diagonal per row; no
   // dictionary, no matrix byte in LDS.  Complex vectors (the reference's
-  // complex(8) arithmetic on a real H): 1024-thread workgroups, the down-hop
-  // values read from a [slot][iw] table behind the vector in LDS (lanes of
-  // one iw broadcast) instead of registers, whose budget the complex w and
-  // p take.
+  // complex(8) arithmetic on a real H; KRC): the up-hop values and the
+  // diagonal in registers as for real vectors, the down-hop values read from
+  // a [slot][iw] table behind the vector in LDS (lanes of one iw broadcast)
+  // instead of registers, whose budget the complex w take; p = v_{k-1} in
+  // global memory.  (Round 3's 1,024-thread complex layout, 4.10 us per
+  // configs[1] step against 3.83-3.86, was removed in round 5.)
   constexpr bool KR = MODE == 4;
-  // complex vectors: KRV = the 1024-thread layout (values and diagonal read
-  // from LDS); KRC = the 512-thread layout (up-hop values and diagonal in
-  // registers as for real vectors, down-hop values broadcast from LDS,
-  // p = v_{k-1} in global memory)
-  constexpr bool KRV = KR && VC && NT == kPBlock;
-  constexpr bool KRC = KR && VC && NT != kPBlock;
+  constexpr bool KRC = KR && VC;
   uint32_t ucol[KR ? E : 1];  // KR: absolute LDS byte address of the up-hop target in slot 0
-  double uval[(KR && !KRV) ? E : 1];
+  double uval[KR ? E : 1];
   uint32_t dcol[KR ? RPT * E : 1];  // KR: absolute LDS byte address of the down-hop target
   double dval[(KR && !VC) ? RPT * E : 1];
-  double dgr[(KR && !KRV) ? RPT : 1];
-  const double* sdv = nullptr;   // KRV: down-hop values [e * dd + iw]
-  const double* suv = nullptr;   // KRV: up-hop values [e * du + iu] (reordered lists)
-  const double* sdg = nullptr;   // KRV: diagonal [VROWS] (padding rows 0)
+  double dgr[KR ? RPT : 1];
+  const double* sdv = nullptr;   // KRC: down-hop values [e * dd + iw]
   int giw = 0;                   // KR: g of the thread (row slot r has iw = g + G*r)
   if constexpr (KR) {
     const int du = a.kdu, dd = a.kdd, G = NT / du;
     const bool act = tid < G * du;
     const int g = act ? tid / du : 0;
     giw = g;
-    if constexpr (KR && VC) {
-      // LDS: vector | diagonal | down-hop values | up-hop values (KRC reads
-      // only the down-hop values)
-      double* tg = (double*)(smem + (((int64_t)VLDS * sizeof(V) + 15) & ~(int64_t)15));
-      for (int x = tid; x < VROWS; x += NT) {
-        double d = 0.0;
-        if (x < dim) {
-          if (a.kdiag) {
-            d = a.kdiag[x];
-          } else {
-            const KronArgs<HC>& K = a.K;
-            const int xw = x / du, xu = x - xw * du;
-            d = re_of(add(add(K.aup[xu], K.adw[xw]), mk<HC>(K.uimp[K.impu[xu] * K.nimp + K.impd[xw]], 0.0)));
-          }
-        }
-        tg[x] = d;
-      }
-      double* t = tg + VROWS;
+    if constexpr (KRC) {
+      // LDS: vector | down-hop values [e * dd + iw]
+      double* t = (double*)(smem + (((int64_t)VLDS * sizeof(V) + 15) & ~(int64_t)15));
       for (int x = tid; x < E * dd; x += NT) t[x] = x < a.kdegd * dd ? a.kdwv[x] : 0.0;
-      double* tu = t + E * dd;
-      for (int x = tid; x < E * du; x += NT) tu[x] = x < a.kdegu * du ? a.kupv[x] : 0.0;
-      sdg = tg;
       sdv = t;
-      suv = tu;
     }
     const uint32_t lb = lds_addr_of(vl);
     constexpr uint32_t kLdsMask = (1u << 18) - 1;  // LDS byte addresses < 256 KiB: known non-negative
@@ -377,7 +352,7 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
       } else {  // byte offset inside the row iw (the row base added per row slot)
         ucol[e] = ok ? (uint32_t)a.kupc[e * du + q.iu] * (uint32_t)sizeof(V) : 0u;
       }
-      if constexpr (!KRV) uval[e] = ok ? a.kupv[e * du + q.iu] : 0.0;
+      uval[e] = ok ? a.kupv[e * du + q.iu] : 0.0;
     }
 #pragma unroll
     for (int r = 0; r < RPT; r++) {
@@ -400,7 +375,7 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
         dcol[r * E + e] = (SLOT ? lb : 0u) + (uint32_t)pos * (uint32_t)sizeof(V);
         if constexpr (!(KR && VC)) dval[r * E + e] = ok ? a.kdwv[e * dd + iw] : 0.0;
       }
-      if constexpr (!KRV) {
+      {
         double d = 0.0;
         if (okr) {
           if (a.kdiag) {
@@ -574,15 +549,9 @@ __global__ void __launch_bounds__(NT) k_lanc_persist(const PersistRun<HC> a) {
           acc = fmac(acc, h, lds_ldv<V>(x & kPkColMask));
         }
       } else if constexpr (KR) {
-        if constexpr (KRV) acc = mul(sdg[i], ur);
-        else acc = mul(dgr[r], ur);
+        acc = mul(dgr[r], ur);
         {
-        if constexpr (KRV) {
-          // idle lanes (tid >= G*DimUp) read table column 0 and their own zero padding slot
-#pragma unroll
-          for (int e = 0; e < E; e++)
-            acc = fmac(acc, suv[e * a.kdu + q.iu], lds_ldv<V>(ucol[e] + r * VSLOT * (int)sizeof(V)));
-        } else if constexpr (SLOT) {
+        if constexpr (SLOT) {
 #pragma unroll
           for (int e = 0; e < E; e++) acc = fmac(acc, uval[e], lds_ldv<V>(ucol[e] + r * VSLOT * (int)sizeof(V)));
         } else {

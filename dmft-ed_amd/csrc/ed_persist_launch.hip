@@ -8,17 +8,15 @@
 
 namespace edg {
 
-// C1024: complex vectors in MODE 4's 1024-thread layout (ED_OPT_PKRON_C1024)
-template <bool HC, bool VC, int MODE, int RPT, int E = 1, bool C1024 = false, bool CSLOT = false>
+template <bool HC, bool VC, int MODE, int RPT, int E = 1>
 static int persist_launch_t(const PersistGeom& s, const PersistRun<HC>& run, int64_t lds, hipStream_t st, int nb) {
   if constexpr ((MODE == 2 || MODE == 3) && RPT * E > preg_cap(HC, VC)) {
     return fail(ED_ERR_UNSUPPORTED, "register-resident ELL exceeds the spill-free budget");
-  } else if constexpr (MODE == 4 && (HC || (VC ? (C1024 ? !pkr_fits_c(E, RPT) : !pkr_fits_c512(E, RPT))
-                                                 : !pkr_fits(E, RPT)))) {
+  } else if constexpr (MODE == 4 && (HC || (VC ? !pkr_fits_c512(E, RPT) : !pkr_fits(E, RPT)))) {
     return fail(ED_ERR_UNSUPPORTED, "Kronecker register layout: real H within the register budget");
   } else {
-  constexpr int NT = (MODE >= 2 && !(MODE == 4 && VC && C1024)) ? kPRegBlock : kPBlock;
-  auto fn = k_lanc_persist<HC, VC, MODE, RPT, E, NT, CSLOT>;
+  constexpr int NT = MODE >= 2 ? kPRegBlock : kPBlock;
+  auto fn = k_lanc_persist<HC, VC, MODE, RPT, E, NT>;
   HIPCK(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(fn, dim3(nb), dim3(NT), (size_t)lds, st, run);
   HIPCK(hipGetLastError());
@@ -28,27 +26,6 @@ static int persist_launch_t(const PersistGeom& s, const PersistRun<HC>& run, int
 
 template <bool HC, bool VC, int MODE, int W>
 static int persist_launch_e(const PersistGeom& s, const PersistRun<HC>& run, int64_t lds, hipStream_t st, int nb) {
-  if constexpr (MODE == 4 && VC) {
-    if (s.pkr_c1024) {
-      switch (s.pkr_rpt_c) {
-        case 2: return persist_launch_t<HC, VC, MODE, 2, W, true>(s, run, lds, st, nb);
-        case 3: return persist_launch_t<HC, VC, MODE, 3, W, true>(s, run, lds, st, nb);
-        case 4: return persist_launch_t<HC, VC, MODE, 4, W, true>(s, run, lds, st, nb);
-        default: return persist_launch_t<HC, VC, MODE, 5, W, true>(s, run, lds, st, nb);
-      }
-    }
-  }
-  if constexpr (MODE == 4 && VC) {
-    if (s.pkr_cslot) {  // 512-thread complex form with the slot layout (A/B)
-      switch (s.pkr_rpt) {
-        case 2: return persist_launch_t<HC, VC, MODE, 2, W, false, true>(s, run, lds, st, nb);
-        case 4: return persist_launch_t<HC, VC, MODE, 4, W, false, true>(s, run, lds, st, nb);
-        case 6: return persist_launch_t<HC, VC, MODE, 6, W, false, true>(s, run, lds, st, nb);
-        case 8: return persist_launch_t<HC, VC, MODE, 8, W, false, true>(s, run, lds, st, nb);
-        default: return persist_launch_t<HC, VC, MODE, 10, W, false, true>(s, run, lds, st, nb);
-      }
-    }
-  }
   switch (MODE == 2 ? s.preg_rpt : MODE == 3 ? s.kreg_rpt : s.pkr_rpt) {
     case 2: return persist_launch_t<HC, VC, MODE, 2, W>(s, run, lds, st, nb);
     case 4: return persist_launch_t<HC, VC, MODE, 4, W>(s, run, lds, st, nb);

@@ -682,331 +682,5 @@ __global__ void __launch_bounds__(kOrthSoloBlock) k_step_solo(const StepSoloArgs
                             a.shifted && a.locupd);
 }
 
-// ------------------------------------------------------------------------
-// Persistent expansion sweep (small and mid-size stored sectors).
-//
-// The multi-kernel sweep costs five dependent launches per Lanczos step
-// (H·v, three CGS passes, coefficient/scale), ≈40 µs per step on sectors
-// up to ~10^5 rows whatever their size — launch and boundary latency, and
-// host dispatch shared by every concurrent farm worker.  Here ONE launch of
-// G <= 128 workgroups runs the whole sweep j0 .. m-1:
-//   * row i belongs to thread (i / kBlock) mod G of the grid-strided layout of
-//     k_spmv_pk for the whole sweep, so the CGS2 work on V and on the new
-//     vector is thread-local (own rows, plain loads and stores);
-//   * only three things cross workgroups: the residual that the next H·v
-//     gathers, and the block partials of the two coefficient passes and of
-//     the norm.  They are stored write-through (sc1), drained, and handed over
-//     by a grid barrier (one agent-scope counter; one lane per workgroup adds
-//     after a workgroup barrier and polls with sc1 loads; consumers read with
-//     sc1 loads) — MI355X_MICROARCH.md "Valid forms", table row 1;
-//   * every workgroup folds the same G partials in the same order, so all of
-//     them hold bit-identical coefficients and beta;
-//   * H·v of step j gathers the unnormalised residual of step j-1 and scales
-//     the row sums by 1/beta_{j-1}; the owner writes V_j = w / beta_{j-1} for
-//     its rows in the same pass (no extra barrier for V_j).
-// Three grid barriers per step.  Every spin is bounded (~2 s of wall clock):
-// a workgroup that times out raises the abort word, every other one leaves at
-// its next poll, and the host reports the sweep as failed — the grid always
-// drains.  Residency: G <= 128 workgroups of 256 threads (launch bounds: 2
-// per CU); the host caps the workgroups of all sweeps in flight (ed_lib.hip,
-// PSweepSlot) so that every grid fits the chip at once.
-// Sectors of a few thousand rows run as ONE workgroup (solo): no barrier and
-// no partials in memory, and the H·v gathers read the vector from LDS.
-template <bool HC>
-struct TrlSweepArgs {
-  const val_t<HC>* diag;
-  const int64_t* sptr;
-  const uint32_t* words;    // packed {col | dictionary index} words, or null
-  const val_t<HC>* dict;    // 256-entry dictionary (packed)
-  const int32_t* cols;      // plain SELL columns / values (words == null)
-  const val_t<HC>* vals;
-  int64_t dim, nslice;
-  void* Vb;                 // basis, column c at Vb + c*dim
-  void* wbuf;               // 2 x dim ping-pong residuals (handed over)
-  void* wout;               // residual after the last step (unnormalised)
-  double2* p1;              // [c*G + b] pass-1 partials
-  double2* p2;              // pass-2 partials
-  double* pn;               // [b] norm partials
-  double* alpha;
-  double* beta;
-  unsigned int* bar;        // [0] arrival counter (monotonic), [1] abort word
-  unsigned int bar0;        // counter value at launch
-  int j0, m;
-};
-
-constexpr unsigned long long kSweepSpinTicks = 200000000ull;  // 2 s at the 100 MHz wall clock
-
-// Grid barrier: returns false if the sweep was aborted (time-out anywhere).
-__device__ __forceinline__ bool sweep_barrier(unsigned int* bar, unsigned int target, int* sok) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 stores drained
-  __syncthreads();                                   // ... and every other wave's
-  if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int ok = 1;
-    const unsigned long long t0 = wall_clock64();
-    for (;;) {
-      const unsigned int v = __hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if ((int)(v - target) >= 0) break;
-      if (__hip_atomic_load(bar + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) { ok = 0; break; }
-      if (wall_clock64() - t0 > kSweepSpinTicks) {
-        __hip_atomic_store(bar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = 0;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-    *sok = ok;
-  }
-  __syncthreads();
-  return *sok != 0;
-}
-
-template <bool HC, bool VC, bool PK, int NC>
-__global__ void __launch_bounds__(kBlock, 2) k_trl_sweep(const TrlSweepArgs<HC> a) {
-  using V = val_t<VC>;
-  using H = val_t<HC>;
-  constexpr int NW = kBlock / 64;
-  constexpr int NR = (VC ? 2 * NC : NC) + 1;
-  constexpr int CPW = (NC + NW - 1) / NW;  // coefficient columns folded per wave
-  extern __shared__ __align__(16) unsigned char xsm[];  // solo: the gathered vector
-  __shared__ H sdict[PK ? kBlock : 1];
-  __shared__ double2 hs[NC];
-  __shared__ double red[NW][NR];
-  __shared__ double sab[2];  // h1_j.x, then alpha_j = (h1_j + h2_j).x
-  __shared__ double sbeta;
-  __shared__ int sok;
-  if constexpr (PK) sdict[threadIdx.x] = a.dict[threadIdx.x];
-  const int G = gridDim.x, blk = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  // one workgroup: no grid barrier, no partials in memory, gathers from LDS
-  const bool solo = G == 1;
-  const int64_t dim = a.dim, nrow = a.nslice * 64;
-  V* const Vb = (V*)a.Vb;
-  V* const wb = (V*)a.wbuf;
-  V* const xl = (V*)xsm;
-  unsigned int target = a.bar0;
-  double inv = 1.0;
-  __syncthreads();
-
-  // block sums of the coefficient partials; solo: straight into hs, else
-  // -> p[c*G + blk] (sc1)
-  auto publish_coef = [&](const double* are, const double* aim, int ncol, double2* p, int j, int pass) {
-#pragma unroll
-    for (int c = 0; c < NC; c++) {
-      if (c >= ncol) continue;  // uniform
-      const double r = wave_sum_dpp(are[c]);
-      if (lane == 63) red[wv][c] = r;
-      if constexpr (VC) {
-        const double q = wave_sum_dpp(aim[c]);
-        if (lane == 63) red[wv][NC + c] = q;
-      }
-    }
-    __syncthreads();
-    if (t < ncol) {
-      double re = 0.0, im = 0.0;
-#pragma unroll
-      for (int w = 0; w < NW; w++) {
-        re = re + red[w][t];
-        if constexpr (VC) im = im + red[w][NC + t];
-      }
-      if (solo) {
-        hs[t] = make_double2(re, im);
-        if (t == j) sab[pass] = pass == 0 ? re : sab[0] + re;
-      } else {
-        st_wt(p + (int64_t)t * G + blk, make_double2(re, im));
-      }
-    }
-  };
-  // every workgroup: hs[c] = sum_b p[c*G + b] (G <= 128) in the same fixed
-  // order; all loads of a wave issued before the first sum
-  auto fold_coef = [&](int ncol, const double2* p, int j, int pass) {
-    V v[CPW][2];  // real vectors: the partials' real parts only
-#pragma unroll
-    for (int k = 0; k < CPW; k++) {
-      const int c = wv + k * NW;
-#pragma unroll
-      for (int h = 0; h < 2; h++) {
-        const int bb = lane + 64 * h;
-        if constexpr (VC)
-          v[k][h] = (c < ncol && bb < G) ? ld_wt(p + (int64_t)c * G + bb) : make_double2(0.0, 0.0);
-        else
-          v[k][h] = (c < ncol && bb < G) ? ld_wt((const double*)(p + (int64_t)c * G + bb)) : 0.0;
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < CPW; k++) {
-      const int c = wv + k * NW;
-      if (c >= ncol) break;  // wave-uniform
-      double re, im = 0.0;
-      if constexpr (VC) {
-        re = wave_sum_dpp(v[k][0].x + v[k][1].x);
-        im = wave_sum_dpp(v[k][0].y + v[k][1].y);
-      } else {
-        re = wave_sum_dpp(v[k][0] + v[k][1]);
-      }
-      if (lane == 63) {
-        hs[c] = make_double2(re, im);
-        if (c == j) sab[pass] = pass == 0 ? re : sab[0] + re;
-      }
-    }
-  };
-  // phase A row loop: gathers from LDS (solo) or sc1 loads of the handed-over residual
-  auto phase_a = [&](auto solo_tag, const V* xs, V* yd, V* Vj, bool first, int j, int ncol, double* are,
-                     double* aim) {
-    constexpr bool S = decltype(solo_tag)::value;
-    for (int64_t i = (int64_t)blk * kBlock + t; i < nrow; i += (int64_t)G * kBlock) {
-      if (i >= dim) continue;
-      const int64_t sl = (int64_t)__builtin_amdgcn_readfirstlane((int)(i >> 6));
-      const int64_t s0 = a.sptr[sl];
-      const int wd = (int)((a.sptr[sl + 1] - s0) >> 6);
-      const V xi = S ? xl[i] : ld_wt(xs + i);
-      V acc = mul(a.diag[i], xi);
-      for (int k0 = 0; k0 < wd; k0 += kPChunk) {
-        int32_t c[kPChunk];
-        H h[kPChunk];
-        if constexpr (PK) {
-          const uint32_t* wp = a.words + s0 + (i & 63);
-#pragma unroll
-          for (int k = 0; k < kPChunk; k++) {
-            const uint32_t wdw = (k0 + k < wd) ? wp[64 * (k0 + k)] : (uint32_t)i;
-            c[k] = (int32_t)(wdw & kPackColMask);
-            h[k] = sdict[wdw >> kPackShift];
-          }
-        } else {
-          const int32_t* cp = a.cols + s0 + (i & 63);
-          const H* vp = a.vals + s0 + (i & 63);
-#pragma unroll
-          for (int k = 0; k < kPChunk; k++) {
-            c[k] = (k0 + k < wd) ? cp[64 * (k0 + k)] : (int32_t)i;
-            h[k] = (k0 + k < wd) ? vp[64 * (k0 + k)] : mk<HC>(0.0, 0.0);
-          }
-        }
-        V g[kPChunk];
-#pragma unroll
-        for (int k = 0; k < kPChunk; k++) g[k] = S ? xl[c[k]] : ld_wt(xs + c[k]);
-#pragma unroll
-        for (int k = 0; k < kPChunk; k++)
-          if (k0 + k < wd) acc = add(acc, mul(h[k], g[k]));
-      }
-      const V y = scl(inv, acc);
-      const V vj = scl(inv, xi);
-      if (!first) Vj[i] = vj;
-      yd[i] = y;
-#pragma unroll
-      for (int c = 0; c < NC; c++) {
-        if (c >= ncol) continue;  // uniform
-        const double2 d = cdotc(c == j ? vj : Vb[(int64_t)c * dim + i], y);
-        are[c] += d.x;
-        if constexpr (VC) aim[c] += d.y;
-      }
-    }
-  };
-  // y -= V h (h = hs); with DOTS the partials of <V_c, y> after the update
-  // (V re-read from L1: one column in registers at a time), else |y|^2
-  auto update = [&](auto dots_tag, V* yd, int ncol, bool last, double* are, double* aim, double& n2) {
-    constexpr bool DOTS = decltype(dots_tag)::value;
-    for (int64_t i = (int64_t)blk * kBlock + t; i < dim; i += (int64_t)G * kBlock) {
-      V y = yd[i];
-#pragma unroll
-      for (int c = 0; c < NC; c++) {
-        if (c >= ncol) continue;
-        const V v = Vb[(int64_t)c * dim + i];
-        if constexpr (VC) {
-          y.x -= v.x * hs[c].x - v.y * hs[c].y;
-          y.y -= v.x * hs[c].y + v.y * hs[c].x;
-        } else {
-          y -= v * hs[c].x;
-        }
-      }
-      if constexpr (DOTS) {
-        yd[i] = y;
-#pragma unroll
-        for (int c = 0; c < NC; c++) {
-          if (c >= ncol) continue;
-          const double2 d = cdotc(Vb[(int64_t)c * dim + i], y);
-          are[c] += d.x;
-          if constexpr (VC) aim[c] += d.y;
-        }
-      } else {
-        if (last || solo) yd[i] = y;
-        else st_wt(yd + i, y);
-        n2 += redot(y, y);
-      }
-    }
-  };
-
-  for (int j = a.j0; j < a.m; j++) {
-    const int ncol = j + 1;
-    const bool first = j == a.j0;
-    const bool last = j == a.m - 1;
-    const V* xs = first ? Vb + (int64_t)j * dim : wb + (int64_t)(j & 1) * dim;
-    V* const yd = last ? (V*)a.wout : wb + (int64_t)((j + 1) & 1) * dim;
-    V* const Vj = Vb + (int64_t)j * dim;
-    double are[NC], aim[VC ? NC : 1], n2 = 0.0;
-#pragma unroll
-    for (int c = 0; c < NC; c++) {
-      are[c] = 0.0;
-      if constexpr (VC) aim[c] = 0.0;
-    }
-    // ---- phase A: y = (H x) / beta_{j-1}; V_j = x / beta_{j-1} (own rows); pass-1 partials
-    if (solo) {
-      for (int64_t i = t; i < dim; i += kBlock) xl[i] = xs[i];  // same CU: plain loads
-      __syncthreads();
-      phase_a(std::true_type{}, xs, yd, Vj, first, j, ncol, are, aim);
-    } else {
-      phase_a(std::false_type{}, xs, yd, Vj, first, j, ncol, are, aim);
-    }
-    publish_coef(are, aim, ncol, a.p1, j, 0);
-    if (!solo) {
-      target += G;
-      if (!sweep_barrier(a.bar, target, &sok)) return;
-      fold_coef(ncol, a.p1, j, 0);
-    }
-    __syncthreads();
-    // ---- phase B: y -= V h1; pass-2 partials
-#pragma unroll
-    for (int c = 0; c < NC; c++) {
-      are[c] = 0.0;
-      if constexpr (VC) aim[c] = 0.0;
-    }
-    update(std::true_type{}, yd, ncol, last, are, aim, n2);
-    publish_coef(are, aim, ncol, a.p2, j, 1);
-    if (!solo) {
-      target += G;
-      if (!sweep_barrier(a.bar, target, &sok)) return;
-      fold_coef(ncol, a.p2, j, 1);
-    }
-    __syncthreads();
-    // ---- phase C: y -= V h2; |y|^2 partials; hand the residual over
-    update(std::false_type{}, yd, ncol, last, are, aim, n2);
-    {
-      const double r = wave_sum_dpp(n2);
-      if (lane == 63) red[wv][0] = r;
-      __syncthreads();
-      if (t == 0) {
-        double s = 0.0;
-#pragma unroll
-        for (int w = 0; w < NW; w++) s = s + red[w][0];
-        if (solo) sbeta = sqrt(s);
-        else st_wt(a.pn + blk, s);
-      }
-    }
-    if (!solo) {
-      target += G;
-      if (!sweep_barrier(a.bar, target, &sok)) return;
-      if (wv == 0) {
-        const double s = wave_sum_dpp((lane < G ? ld_wt(a.pn + lane) : 0.0) +
-                                      (lane + 64 < G ? ld_wt(a.pn + lane + 64) : 0.0));
-        if (lane == 63) sbeta = sqrt(s);
-      }
-    }
-    __syncthreads();
-    const double bn = sbeta;
-    if (blk == 0 && t == 0) {
-      a.alpha[j] = sab[1];
-      a.beta[j] = bn;
-    }
-    inv = bn > 0.0 ? 1.0 / bn : 0.0;
-  }
-}
 
 }  // namespace edg

@@ -17,11 +17,9 @@ ED_NO_PACK, ED_KRON2_OFF, ED_KRON2_ON = 0x10, 0x20, 0x40
 # kernel alternatives of a built sector (ed_sector_set_options, include/ed_gpu.h)
 OPTIONS = {
     "no_persist": 0x001, "persist_stored": 0x002, "no_preg": 0x004, "no_pkron": 0x008,
-    "fused_step": 0x010, "split_simple": 0x020, "no_batch": 0x040, "eigh_no_verify": 0x080,
-    "trlan_unfused": 0x100, "trlan_nofold": 0x200, "trlan_psweep": 0x400, "no_graph": 0x800,
-    "trlan_nolocal": 0x1000, "trlan_nosolo": 0x2000, "trlan_fullupd": 0x4000, "pkron_c1024": 0x8000,
-    "trlan_g128": 0x10000, "eigh_fullprobe": 0x20000, "pkron_cslot": 0x40000,
-    "kron_dw1": 0x80000,
+    "split_simple": 0x020, "no_batch": 0x040, "eigh_no_verify": 0x080,
+    "trlan_unfused": 0x100, "trlan_nofold": 0x200, "no_graph": 0x800,
+    "trlan_nolocal": 0x1000, "trlan_nosolo": 0x2000, "trlan_fullupd": 0x4000,
 }
 ED_OK = 0
 ERRORS = {1: "ED_ERR_ARG", 2: "ED_ERR_STATE", 3: "ED_ERR_HIP", 4: "ED_ERR_OOM",

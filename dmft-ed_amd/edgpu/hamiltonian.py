@@ -85,9 +85,9 @@ class Sector:
 
     def set_options(self, *names: str) -> None:
         """Select kernel alternatives by name (ED_OPT_*: no_persist,
-        persist_stored, no_preg, no_pkron, fused_step, split_simple, no_batch,
-        eigh_no_verify, trlan_unfused, trlan_nofold, trlan_psweep, no_graph,
-        trlan_nolocal, trlan_nosolo, pkron_c1024); no names
+        persist_stored, no_preg, no_pkron, split_simple, no_batch,
+        eigh_no_verify, trlan_unfused, trlan_nofold, no_graph, trlan_nolocal,
+        trlan_nosolo, trlan_fullupd; edgpu._lib.OPTIONS); no names
         restores the defaults."""
         bits = 0
         for n in names:

@@ -68,27 +68,23 @@ extern "C" {
 
 /* Kernel-selection options of a built sector (ed_sector_set_options): the
  * alternatives kept for parity tests and A/B measurements.  0 = the default
- * choice everywhere; nothing in the library reads the environment. */
+ * choice everywhere; nothing in the library reads the environment.  Bits
+ * 0x010, 0x400, 0x8000 and 0x10000-0x80000 belonged to alternatives measured
+ * slower and removed in round 5 (DESIGN.md keeps their numbers); they are
+ * rejected as unknown. */
 #define ED_OPT_NO_PERSIST     0x001 /* Lanczos: graph-captured multi-kernel recurrence only   */
 #define ED_OPT_PERSIST_STORED 0x002 /* Lanczos: persistent MODE 0 (stored matrix from L2)      */
 #define ED_OPT_NO_PREG        0x004 /* Lanczos: no register-resident modes (2, 3, 4)           */
 #define ED_OPT_NO_PKRON       0x008 /* Lanczos: no Kronecker register layout (MODE 4)          */
-#define ED_OPT_FUSED_STEP     0x010 /* multi-kernel Lanczos: one-kernel step on small grids    */
 #define ED_OPT_SPLIT_SIMPLE   0x020 /* kron_rows/cols: one-thread-per-row kernels              */
 #define ED_OPT_NO_BATCH       0x040 /* lanc_tridiag_batch: seeds one after the other           */
 #define ED_OPT_EIGH_NO_VERIFY 0x080 /* eigh: no deflated search for missed degenerate copies   */
 #define ED_OPT_TRLAN_UNFUSED  0x100 /* eigh: four-sweep CGS2 instead of the fused sweeps       */
 #define ED_OPT_TRLAN_NOFOLD   0x200 /* eigh: separate coefficient kernels on small grids       */
-#define ED_OPT_TRLAN_PSWEEP   0x400 /* eigh: one persistent launch per expansion sweep (opt-in) */
 #define ED_OPT_NO_GRAPH       0x800 /* eigh: Krylov sweeps launched directly, not as hipGraphs  */
 #define ED_OPT_TRLAN_NOLOCAL  0x1000 /* eigh: plain w = H v_j (no shifted three-term step)     */
 #define ED_OPT_TRLAN_NOSOLO   0x2000 /* eigh: multi-kernel CGS also on sectors <= 2048 rows     */
 #define ED_OPT_TRLAN_FULLUPD  0x4000 /* eigh: full CGS update every step (no local-only update) */
-#define ED_OPT_PKRON_C1024    0x8000 /* Lanczos MODE 4, complex vectors: 1024-thread LDS layout  */
-#define ED_OPT_TRLAN_G128    0x10000 /* eigh: Krylov sweeps on <= 128 blocks (coefficients folded) */
-#define ED_OPT_EIGH_FULLPROBE 0x20000 /* eigh: degeneracy probe without the plain-Lanczos screen */
-#define ED_OPT_PKRON_CSLOT   0x40000 /* Lanczos MODE 4, complex vectors, 512 threads: slot-major LDS vector (A/B) */
-#define ED_OPT_KRON_DW1      0x80000 /* two-pass Kronecker H·v, real vectors: pass D one column per lane (A/B) */
 
 /* status codes */
 #define ED_OK              0

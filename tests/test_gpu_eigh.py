@@ -86,29 +86,6 @@ def test_eigh_large_sector_vs_plain_lanczos():
             assert r < 1e-8 * max(1.0, abs(w[k]))
 
 
-@pytest.mark.parametrize("q", [(4, 4), (3, 3)], ids=["dim4900", "dim3136"])
-def test_eigh_persistent_sweep_option(q):
-    """ED_OPT_TRLAN_PSWEEP (one persistent launch per expansion sweep), grid
-    form (20 and 13 workgroups with grid barriers): the configs[1] sectors
-    (4,4) and (3,3) against dense diagonalisation, like the default path."""
-    cfg = CASES[0][1]()
-    H = _oracle_H(cfg, q)
-    with Sector(cfg, q[0], q[1], stored=True, real=True, options=("trlan_psweep",)) as S:
-        _check(S, H, True)
-
-
-def test_eigh_persistent_sweep_solo_small():
-    """The one-workgroup form (dim <= 2,048, vector in LDS): a configs[0]-size
-    sector."""
-    from edgpu.params import make_config
-
-    cfg = make_config(Norb=1, Nbath=5, bath="random", seed=3)
-    H = _oracle_H(cfg, (3, 3))
-    assert 2 * NCV < H.shape[0] <= 2048
-    with Sector(cfg, 3, 3, stored=True, real=True, options=("trlan_psweep",)) as S:
-        _check(S, H, True)
-
-
 @pytest.mark.parametrize("opts", [("trlan_nolocal",), ("trlan_nosolo",), ("trlan_nolocal", "trlan_nosolo")],
                          ids=["nolocal", "nosolo", "plain"])
 @pytest.mark.parametrize("real", [True, False], ids=["real", "complex"])

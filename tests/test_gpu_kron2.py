@@ -54,20 +54,28 @@ def test_two_pass_bit_identical(name, factory, sectors):
     (dict(Norb=2, Nbath=4, bath="random", seed=4), (3, 6)),              # du != dd
     (dict(Norb=1, Nbath=6, bath="random", seed=6), (3, 4)),              # odd DimUp (35)
 ])
-@pytest.mark.parametrize("opts", [(), ("kron_dw1",)], ids=["dw2", "dw1"])
-def test_two_pass_real_vectors_and_lanczos(cfg_kw, q, opts):
-    """Pass D takes two columns per lane at even DimUp (odd DimUp, or the
-    kron_dw1 option: one) — the same H·v bit for bit."""
+@pytest.mark.parametrize("offset", [False, True], ids=["aligned", "offset8"])
+def test_two_pass_real_vectors_and_lanczos(cfg_kw, q, offset):
+    """Pass D takes two columns per lane at even DimUp and 16-byte aligned
+    vectors (odd DimUp, or input / output 8 bytes off a 16-byte boundary: one
+    column per lane on the same grid) — the same H·v bit for bit."""
     from edgpu.params import make_config
 
     cfg = make_config(**cfg_kw)
-    A, B = _both(cfg, q, real=True, options=opts)
+    A, B = _both(cfg, q, real=True)
     with A, B:
         i = torch.arange(1, A.dim + 1, dtype=torch.float64, device="cuda:0")
         x = torch.sin(i)
         ya, yb = torch.empty_like(x), torch.empty_like(x)
-        A.hxv_dev(x, ya, path=2)
-        B.hxv_dev(x, yb, path=2)
+        B.hxv_dev(x, yb, path=2)   # one-pass k_kron: the reference sums
+        if offset:   # views one element into larger buffers: 8-byte aligned only
+            xb = torch.zeros(A.dim + 1, dtype=torch.float64, device="cuda:0")
+            xb[1:] = x
+            yo = torch.empty(A.dim + 1, dtype=torch.float64, device="cuda:0")
+            A.hxv_dev(xb[1:], yo[1:], path=2)
+            ya = yo[1:]
+        else:
+            A.hxv_dev(x, ya, path=2)
         torch.cuda.synchronize()
         assert torch.equal(ya, yb)
         # the Lanczos epilogue (w = Hv/b - b p, alpha) in pass D: multi-kernel

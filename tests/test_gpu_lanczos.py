@@ -106,22 +106,6 @@ def test_persistent_matches_multikernel(path):
     np.testing.assert_allclose(b1[:40], b2[:40], rtol=1e-9, atol=1e-11)
 
 
-def test_fused_step_matches_two_kernel():
-    """Single-kernel step (small grids) vs the two-kernel step: same recurrence."""
-    from edgpu.hamiltonian import Sector
-    from cases import c5
-
-    cfg = c5()
-    with Sector(cfg, 7, 0, stored=True) as S:
-        v0 = np.sin(np.arange(1, S.dim + 1, dtype=np.float64)) + 0j
-        S.set_options("no_persist", "fused_step")
-        a1, b1, n1 = S.lanc_tridiag(v0, 50)
-        S.set_options("no_persist")
-        a2, b2, n2 = S.lanc_tridiag(v0, 50)
-    np.testing.assert_allclose(a1[:30], a2[:30], rtol=1e-10, atol=1e-12)
-    np.testing.assert_allclose(b1[:30], b2[:30], rtol=1e-10, atol=1e-12)
-
-
 def test_c4_half_filled_ground_state_pin():
     """configs[3] half-filled sector at full size: nnz and E0 of the reference
     run through the large-grid (two-pass reduction) recurrence."""
@@ -139,12 +123,10 @@ def test_c4_half_filled_ground_state_pin():
             assert abs(np.linalg.norm(vec) - 1.0) < 1e-10
 
 
-@pytest.mark.parametrize("layout", [(), ("pkron_c1024",)], ids=["c512", "c1024"])
 @pytest.mark.parametrize("direct", [False, True], ids=["stored", "direct"])
-def test_complex_vectors_kronecker_register_layout(direct, layout):
+def test_complex_vectors_kronecker_register_layout(direct):
     """The reference's arithmetic — complex(8) vectors — on a real H through
-    the Kronecker register layout (persistent MODE 4; the 512-thread register
-    form, default, and the 1024-thread LDS form, ED_OPT_PKRON_C1024):
+    the Kronecker register layout (persistent MODE 4, 512-thread form):
     alpha/beta (first 15 steps) and E0 against the oracle's complex
     recurrence at 1e-10, and 40 steps against the multi-kernel one at 1e-9."""
     from edgpu.hamiltonian import Sector
@@ -157,7 +139,7 @@ def test_complex_vectors_kronecker_register_layout(direct, layout):
     v0 = start_vector(len(hmap))
     ar, br, nr = lanc_tridiag(csr, v0, 60)
     kw = dict(stored=False, direct=True) if direct else dict(stored=True)
-    with Sector(cfg, 4, 4, real=True, options=layout, **kw) as S:
+    with Sector(cfg, 4, 4, real=True, **kw) as S:
         assert S.lanc_mode(real=False) == 4
         a, b, n = S.lanc_tridiag(v0, 60, real=False)
         assert n == nr == 60
@@ -173,15 +155,14 @@ def test_complex_vectors_kronecker_register_layout(direct, layout):
     np.testing.assert_allclose(b[:40], b2[:40], rtol=1e-9, atol=1e-11)
 
 
-@pytest.mark.parametrize("layout", [(), ("pkron_c1024",)], ids=["c512", "c1024"])
-def test_complex_vectors_batched_mode4(layout):
-    """Batched complex runs (one workgroup per start vector, both MODE 4
-    complex layouts) give each run's single-launch alpha/beta."""
+def test_complex_vectors_batched_mode4():
+    """Batched complex runs (one workgroup per start vector, MODE 4 complex
+    layout) give each run's single-launch alpha/beta."""
     from edgpu.gf import _tridiag_batch
     from edgpu.hamiltonian import Sector
     from cases import c2
 
-    with Sector(c2(), 4, 4, real=True, stored=True, options=layout) as S:
+    with Sector(c2(), 4, 4, real=True, stored=True) as S:
         assert S.lanc_mode(real=False) == 4
         i = torch.arange(1, S.dim + 1, dtype=torch.float64, device="cuda:0")
         seeds = torch.stack([torch.complex(torch.sin(k * i), torch.cos(3 * k * i)) for k in (1, 2, 3)])
