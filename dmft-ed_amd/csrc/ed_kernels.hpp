@@ -214,6 +214,15 @@ static __global__ void __launch_bounds__(kBlock) k_count(const EdModel* __restri
 }
 
 // Exclusive scan of 64*width -> sptr (int64), three-pass.
+// *out += sum of n 16-bit counts (grid-strided; wave sums, one atomic per wave)
+static __global__ void __launch_bounds__(kBlock) k_sum_u16(const uint16_t* __restrict__ c, int64_t n,
+                                                    unsigned long long* out) {
+  unsigned long long acc = 0;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) acc += c[i];
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, acc);
+}
+
 static __global__ void __launch_bounds__(1024) k_scan_blocks(const int32_t* __restrict__ width, int64_t n,
                                                       int64_t* __restrict__ out,
                                                       int64_t* __restrict__ bsum) {

@@ -20,6 +20,7 @@
 #include "ed_kernels.hpp"
 #include "ed_persist.hpp"
 #include "ed_trlan.hpp"
+#include "ed_split.hpp"
 #include "ed_tables.hpp"
 #include "ed_host.hpp"
 
@@ -102,6 +103,18 @@ struct ed_sector {
   uint32_t* d_words = nullptr;
   void* d_pdict = nullptr;   // real(8) or complex(8) values (hc)
   int npdict = 0;
+  // two-segment stored H (ed_split.hpp): A words (diagonal + in-block
+  // elements, row order), B slices (cross-block elements: U list + L words)
+  bool split = false;
+  int64_t* d_sptrA = nullptr;
+  uint32_t* d_wordsA = nullptr;
+  int64_t paddedA = 0;
+  SplitSlice* d_bsl = nullptr;
+  int nbsl = 0;
+  int* d_bxoff = nullptr;   // [9] per-XCD slice ranges
+  int2* d_ul = nullptr;
+  uint32_t* d_lw = nullptr;
+  int64_t nul = 0, nlw = 0, nfar = 0, nfar_u = 0;  // U entries, L words, cross-block elements (all / in U)
   // matrix-free, generic (k_direct): chunk list, per-block op lists, 16-bit tables
   DirChunk* d_dchunk = nullptr;   // 64-row chunks (real vectors)
   int ndchunk = 0;
@@ -329,6 +342,134 @@ static int64_t stored_mbytes(const ed_sector* s) {
   return s->padded * (4 + hv) + s->nrows * hv;
 }
 
+// ---------------------------------------------------- two-segment stored H
+// (ed_split.hpp).  Built for whole packed sectors whose stored matrix does
+// not fit the 256 MB Infinity Cache (the sectors whose one-pass kernel pays
+// the down-spin re-gathers from HBM).
+static constexpr int64_t kSplitMinBytes = (int64_t)192 << 20;
+
+static int build_split(ed_sector* s) {
+  const int64_t dim = s->dim, ns = s->nslice;
+  const int hw = s->hc ? 2 : 1;
+  const int nsp = s->Mh.ns;
+  // the dictionary's zero (padding slots); appended when absent
+  std::vector<double> dict(256 * hw);
+  CK(dcopy(s, dict.data(), s->d_pdict, dict.size() * 8, hipMemcpyDeviceToHost));
+  int z = -1;
+  for (int k = 0; k < s->npdict && z < 0; k++) {
+    bool zero = true;
+    for (int h = 0; h < hw; h++) zero = zero && dict[k * hw + h] == 0.0 && !std::signbit(dict[k * hw + h]);
+    if (zero) z = k;
+  }
+  if (z < 0) {
+    if (s->npdict >= 256) return ED_OK;  // no room for a zero: the one-pass kernel serves
+    z = s->npdict++;
+    HIPCK(hipMemsetAsync((double*)s->d_pdict + (size_t)z * hw, 0, 8 * hw, s->stream));
+  }
+  const uint32_t zpad = (uint32_t)z << kPackShift;
+  // ---- segment A: counts, slice widths, offsets, fill
+  uint16_t* na;
+  int32_t* width;
+  int64_t *bsum, *total;
+  int* farmax;
+  const int64_t nb = (ns + 1023) / 1024;
+  HIPCK(hipMallocAsync((void**)&na, dim * sizeof(uint16_t), s->stream));
+  HIPCK(hipMallocAsync((void**)&width, ns * sizeof(int32_t), s->stream));
+  HIPCK(hipMallocAsync((void**)&bsum, std::max<int64_t>(nb, 1) * sizeof(int64_t), s->stream));
+  HIPCK(hipMallocAsync((void**)&total, sizeof(int64_t), s->stream));
+  HIPCK(hipMallocAsync((void**)&farmax, sizeof(int), s->stream));
+  auto scratch_free = [&]() {
+    (void)hipFreeAsync(na, s->stream);
+    (void)hipFreeAsync(width, s->stream);
+    (void)hipFreeAsync(bsum, s->stream);
+    (void)hipFreeAsync(total, s->stream);
+    (void)hipFreeAsync(farmax, s->stream);
+  };
+  HIPCK(hipMemsetAsync(farmax, 0, sizeof(int), s->stream));
+  hipLaunchKernelGGL(k_split_count_a, dim3(grid_for(ns * 64)), dim3(kBlock), 0, s->stream, s->d_sptr, s->d_words,
+                     s->d_cnt, s->d_map, nsp, dim, ns, na, width, farmax);
+  HIPCK(hipGetLastError());
+  int hfar = 0;
+  HIPCK(hipMemcpyAsync(&hfar, farmax, sizeof(int), hipMemcpyDeviceToHost, s->stream));
+  HIPCK(hipStreamSynchronize(s->stream));
+  if (hfar > kSplitFarMax) {
+    scratch_free();
+    return ED_OK;  // rows with more cross-block elements than the build stages: one-pass
+  }
+  CK(dalloc_t(s, &s->d_sptrA, ns + 1));
+  hipLaunchKernelGGL(k_scan_blocks, dim3((unsigned)nb), dim3(1024), 0, s->stream, width, ns, s->d_sptrA, bsum);
+  hipLaunchKernelGGL(k_scan_spine, dim3(1), dim3(64), 0, s->stream, bsum, nb, total);
+  hipLaunchKernelGGL(k_scan_add, dim3((unsigned)nb), dim3(1024), 0, s->stream, s->d_sptrA, ns, bsum, total);
+  HIPCK(hipGetLastError());
+  int64_t slotsA = 0;
+  HIPCK(hipMemcpyAsync(&slotsA, total, sizeof(int64_t), hipMemcpyDeviceToHost, s->stream));
+  HIPCK(hipStreamSynchronize(s->stream));
+  s->paddedA = slotsA;
+  CK(dalloc_t(s, &s->d_wordsA, std::max<int64_t>(slotsA, 1)));
+  hipLaunchKernelGGL(k_split_fill_a, dim3(grid_for(ns * 64)), dim3(kBlock), 0, s->stream, s->d_sptr, s->d_words,
+                     s->d_cnt, s->d_map, nsp, dim, ns, s->d_sptrA, s->d_wordsA, zpad);
+  HIPCK(hipGetLastError());
+  // ---- segment B: slices of <= 64 rows of one block, chunk-major
+  const SectorTables& T = s->T;
+  const int64_t nblk = (int64_t)T.blk_off.size() - 1;
+  int64_t maxlen = 0;
+  for (int64_t b = 0; b < nblk; b++) maxlen = std::max(maxlen, T.blk_off[b + 1] - T.blk_off[b]);
+  std::vector<SplitSlice> sl;
+  for (int64_t c = 0; c * 64 < maxlen; c++)
+    for (int64_t b = 0; b < nblk; b++) {
+      const int64_t len = T.blk_off[b + 1] - T.blk_off[b];
+      if (c * 64 >= len) continue;
+      SplitSlice q{};
+      q.row0 = (int32_t)(T.blk_off[b] + c * 64);
+      q.n = (int32_t)std::min<int64_t>(64, len - c * 64);
+      sl.push_back(q);
+    }
+  const int64_t nsl = (int64_t)sl.size();
+  CK(dalloc_t(s, &s->d_bsl, std::max<int64_t>(nsl, 1)));
+  CK(dcopy(s, s->d_bsl, sl.data(), nsl * sizeof(SplitSlice), hipMemcpyHostToDevice));
+  const int gb = (int)std::min<int64_t>((nsl + 3) / 4, 65536);
+  hipLaunchKernelGGL(k_split_b<false>, dim3(gb), dim3(kBlock), 0, s->stream, s->d_sptr, s->d_words, s->d_cnt,
+                     s->d_map, nsp, s->d_bsl, nsl, (int2*)nullptr, (uint32_t*)nullptr, zpad);
+  HIPCK(hipGetLastError());
+  CK(dcopy(s, sl.data(), s->d_bsl, nsl * sizeof(SplitSlice), hipMemcpyDeviceToHost));
+  int64_t uo = 0, lo = 0, nfar_u = 0;
+  for (SplitSlice& q : sl) {
+    q.uoff = uo;
+    q.loff = lo;
+    uo += q.nu;
+    lo += 64 * (int64_t)q.wl;
+    nfar_u += (int64_t)q.nu * q.n;
+  }
+  CK(dcopy(s, s->d_bsl, sl.data(), nsl * sizeof(SplitSlice), hipMemcpyHostToDevice));
+  CK(dalloc_t(s, &s->d_ul, std::max<int64_t>(uo, 1)));
+  CK(dalloc_t(s, &s->d_lw, std::max<int64_t>(lo, 1)));
+  hipLaunchKernelGGL(k_split_b<true>, dim3(gb), dim3(kBlock), 0, s->stream, s->d_sptr, s->d_words, s->d_cnt,
+                     s->d_map, nsp, s->d_bsl, nsl, s->d_ul, s->d_lw, zpad);
+  HIPCK(hipGetLastError());
+  // per-XCD ranges: eight equal contiguous parts of the chunk-major list
+  std::vector<int> xo(9);
+  for (int x = 0; x <= 8; x++) xo[x] = (int)((nsl * x) / 8);
+  CK(upload(s, &s->d_bxoff, xo));
+  // cross-block elements = nnz - dim - sum(nA) (the U entries cover nfar_u of them)
+  unsigned long long* dn;
+  HIPCK(hipMallocAsync((void**)&dn, sizeof(unsigned long long), s->stream));
+  HIPCK(hipMemsetAsync(dn, 0, sizeof(unsigned long long), s->stream));
+  hipLaunchKernelGGL(k_sum_u16, dim3(grid_once(dim)), dim3(kBlock), 0, s->stream, na, dim, dn);
+  HIPCK(hipGetLastError());
+  unsigned long long sumA = 0;
+  HIPCK(hipMemcpyAsync(&sumA, dn, sizeof(sumA), hipMemcpyDeviceToHost, s->stream));
+  HIPCK(hipStreamSynchronize(s->stream));
+  (void)hipFreeAsync(dn, s->stream);
+  scratch_free();
+  s->nbsl = (int)nsl;
+  s->nul = uo;
+  s->nlw = lo;
+  s->nfar_u = nfar_u;
+  s->nfar = s->nnz - dim - (int64_t)sumA;
+  s->split = true;
+  return ED_OK;
+}
+
 static int build_stored(ed_sector* s) {
   const int64_t dim = s->nrows, ns = s->nslice;  // rows held by this sector object
   const uint32_t* map = s->d_map + s->row0;
@@ -374,14 +515,21 @@ static int build_stored(ed_sector* s) {
                        map, dim, idx, s->d_sptr, (double*)s->d_diag, s->d_cols,
                        (double*)s->d_vals);
   HIPCK(hipGetLastError());
-  // nnz = dim (diagonal) + sum(cnt)
-  std::vector<uint16_t> hc(dim);
-  HIPCK(hipMemcpyAsync(hc.data(), cnt, dim * sizeof(uint16_t), hipMemcpyDeviceToHost, s->stream));
+  // nnz = dim (diagonal) + sum(cnt), reduced on the device (no D2H of the counts)
+  unsigned long long* dn;
+  HIPCK(hipMallocAsync((void**)&dn, sizeof(unsigned long long), s->stream));
+  HIPCK(hipMemsetAsync(dn, 0, sizeof(unsigned long long), s->stream));
+  hipLaunchKernelGGL(k_sum_u16, dim3(grid_once(dim)), dim3(kBlock), 0, s->stream, cnt, dim, dn);
+  HIPCK(hipGetLastError());
+  unsigned long long hn = 0;
+  HIPCK(hipMemcpyAsync(&hn, dn, sizeof(hn), hipMemcpyDeviceToHost, s->stream));
   HIPCK(hipStreamSynchronize(s->stream));
-  int64_t nnz = dim;
-  for (int64_t i = 0; i < dim; i++) nnz += hc[i];
-  s->nnz = nnz;
+  (void)hipFreeAsync(dn, s->stream);
+  s->nnz = dim + (int64_t)hn;
   if (s->dim <= (int64_t)kPackColMask + 1 && !(s->flags & ED_NO_PACK)) CK(build_pack(s));
+  if (s->d_words && s->row0 == 0 && s->nrows == s->dim &&
+      (stored_mbytes(s) > kSplitMinBytes || (s->flags & ED_SPLIT_ON)) && !(s->flags & ED_NO_SPLIT))
+    CK(build_split(s));
   return ED_OK;
 }
 
@@ -983,8 +1131,13 @@ static int kron_dw_grid(const ed_sector* s, bool vc) {
   // one-column form on this same grid: hxv_blocks() must match the launch)
   return s->K.dimup % 2 == 0 ? kKronDwGrid2 : kKronDwGrid;
 }
+// the two-segment stored kernels serve path 0 unless ED_OPT_STORED_EXACT
+static bool split_on(const ed_sector* s, int path) {
+  return path == 0 && s->split && !(s->opts & ED_OPT_STORED_EXACT);
+}
 static int hxv_blocks(const ed_sector* s, int path, int vc = 0) {
   if (kron2_on(s, path, vc)) return kron_dw_grid(s, vc);
+  if (split_on(s, path)) return kSplitGrid;
   if (path == 1) return s->dir_grid;
   const int g = grid_for(s->nslice * 64);
   return xcd_on(s, path) ? (g & ~7) : g;
@@ -1102,6 +1255,35 @@ static int launch_kron2(ed_sector* s, const void* x, Epi epi, hipStream_t st) {
   return launch_kron_dw<HC, VC>(s, x, y, epi, st, (int)s->K.dimup, (int)s->K.dimup);
 }
 
+// Two-segment stored H·v (ed_split.hpp): segment A (diagonal + in-block
+// elements, k_spmv_pk on the A words) writes y into the epilogue's scratch
+// vector, segment B adds the cross-block elements and runs the epilogue.
+template <bool HC, bool VC, class Epi>
+static int launch_split(ed_sector* s, const void* x, Epi epi, hipStream_t st) {
+  using V = val_t<VC>;
+  using H = val_t<HC>;
+  V* y = (V*)epi.scratch();
+  EpiStore<VC> ea{y};
+  const int64_t dim = s->dim, ns = s->nslice;
+  const int ga = grid_for(ns * 64) & ~7;  // XCD row ranges (k_spmv_pk's remap)
+  const bool nta = (s->paddedA * 4 + dim * (int64_t)sizeof(H)) > kSplitMinBytes;
+  if (nta)
+    hipLaunchKernelGGL((k_spmv_pk<HC, VC, 1, EpiStore<VC>>), dim3(ga), dim3(kBlock), 0, st, (const H*)s->d_diag,
+                       s->d_sptrA, s->d_wordsA, (const H*)s->d_pdict, (const V*)x, (const V*)x, dim, ns, ea, 1);
+  else
+    hipLaunchKernelGGL((k_spmv_pk<HC, VC, 0, EpiStore<VC>>), dim3(ga), dim3(kBlock), 0, st, (const H*)s->d_diag,
+                       s->d_sptrA, s->d_wordsA, (const H*)s->d_pdict, (const V*)x, (const V*)x, dim, ns, ea, 1);
+  HIPCK(hipGetLastError());
+  if (s->nlw * 4 > kSplitMinBytes)
+    hipLaunchKernelGGL((k_spmv_sb<HC, VC, 1, Epi>), dim3(kSplitGrid), dim3(kBlock), 0, st, s->d_bsl, s->d_bxoff,
+                       s->d_ul, s->d_lw, (const H*)s->d_pdict, (const V*)x, (const V*)y, epi);
+  else
+    hipLaunchKernelGGL((k_spmv_sb<HC, VC, 0, Epi>), dim3(kSplitGrid), dim3(kBlock), 0, st, s->d_bsl, s->d_bxoff,
+                       s->d_ul, s->d_lw, (const H*)s->d_pdict, (const V*)x, (const V*)y, epi);
+  HIPCK(hipGetLastError());
+  return ED_OK;
+}
+
 template <bool HC, bool VC, class Epi>
 static int launch_hxv_t(ed_sector* s, int path, const void* x, Epi epi, hipStream_t st) {
   using V = val_t<VC>;
@@ -1112,6 +1294,7 @@ static int launch_hxv_t(ed_sector* s, int path, const void* x, Epi epi, hipStrea
   const V* xo = (const V*)x + s->row0;  // the rows' own entries
   // non-temporal matrix loads once the matrix cannot stay in the 256 MB MALL
   const bool nt = stored_mbytes(s) > ((int64_t)192 << 20);
+  if (split_on(s, path)) return launch_split<HC, VC>(s, x, epi, st);
   if (path == 0 && s->d_words) {
     using H = val_t<HC>;
     if (nt)
@@ -2734,7 +2917,7 @@ int ed_sector_destroy(ed_sector* s) {
 static constexpr int32_t kOptKnown =
     ED_OPT_NO_PERSIST | ED_OPT_PERSIST_STORED | ED_OPT_NO_PREG | ED_OPT_NO_PKRON | ED_OPT_SPLIT_SIMPLE |
     ED_OPT_NO_BATCH | ED_OPT_EIGH_NO_VERIFY | ED_OPT_TRLAN_UNFUSED | ED_OPT_TRLAN_NOFOLD | ED_OPT_NO_GRAPH |
-    ED_OPT_TRLAN_NOLOCAL | ED_OPT_TRLAN_NOSOLO | ED_OPT_TRLAN_FULLUPD;
+    ED_OPT_TRLAN_NOLOCAL | ED_OPT_TRLAN_NOSOLO | ED_OPT_TRLAN_FULLUPD | ED_OPT_STORED_EXACT;
 
 int ed_sector_set_options(ed_sector* s, int32_t opts) {
   if (!s) return fail(ED_ERR_ARG, "null");
@@ -2763,6 +2946,10 @@ int ed_sector_get_info(const ed_sector* s, ed_sector_info* info) {
   info->device_bytes = s->bytes;
   info->packed = s->d_words ? 1 : 0;
   info->npdict = s->npdict;
+  info->split = s->split ? 1 : 0;
+  info->split_far = s->nfar;
+  info->split_far_uniform = s->nfar_u;
+  info->split_bytes = s->split ? (s->paddedA + s->nlw) * 4 + s->nul * 8 + (int64_t)s->nbsl * sizeof(SplitSlice) : 0;
   return ED_OK;
 }
 

@@ -13,13 +13,14 @@ _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(_PKG_ROOT, "libedgpu.so")
 
 ED_STORED, ED_DIRECT, ED_REAL = 0x1, 0x2, 0x4
-ED_NO_PACK, ED_KRON2_OFF, ED_KRON2_ON = 0x10, 0x20, 0x40
+ED_NO_PACK, ED_KRON2_OFF, ED_KRON2_ON, ED_NO_SPLIT, ED_SPLIT_ON = 0x10, 0x20, 0x40, 0x80, 0x100
 # kernel alternatives of a built sector (ed_sector_set_options, include/ed_gpu.h)
 OPTIONS = {
     "no_persist": 0x001, "persist_stored": 0x002, "no_preg": 0x004, "no_pkron": 0x008,
     "split_simple": 0x020, "no_batch": 0x040, "eigh_no_verify": 0x080,
     "trlan_unfused": 0x100, "trlan_nofold": 0x200, "no_graph": 0x800,
     "trlan_nolocal": 0x1000, "trlan_nosolo": 0x2000, "trlan_fullupd": 0x4000,
+    "stored_exact": 0x100000,
 }
 ED_OK = 0
 ERRORS = {1: "ED_ERR_ARG", 2: "ED_ERR_STATE", 3: "ED_ERR_HIP", 4: "ED_ERR_OOM",
@@ -78,7 +79,9 @@ class SectorInfo(ctypes.Structure):
     _fields_ = [("dim", _i64), ("nnz", _i64), ("padded", _i64), ("ns", _i32), ("mode", _i32),
                 ("q1", _i32), ("q2", _i32), ("flags", _i32), ("kron", _i32),
                 ("dimup", _i64), ("dimdw", _i64), ("device_bytes", _i64),
-                ("packed", _i32), ("npdict", _i32), ("row0", _i64), ("nrows", _i64)]
+                ("packed", _i32), ("npdict", _i32), ("row0", _i64), ("nrows", _i64),
+                ("split", _i32), ("pad_", _i32), ("split_far", _i64), ("split_far_uniform", _i64),
+                ("split_bytes", _i64)]
 
 
 class EDGPUError(RuntimeError):

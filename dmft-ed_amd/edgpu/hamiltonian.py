@@ -49,11 +49,14 @@ class Sector:
 
     def __init__(self, cfg: EDConfig, q1: int, q2: int = 0, *, stored: bool = True,
                  direct: bool = False, real: bool = False, device: int = 0, rows=None,
-                 pack: bool = True, kron2: Optional[bool] = None, options=()):
+                 pack: bool = True, kron2: Optional[bool] = None, split: Optional[bool] = None,
+                 options=()):
         """rows=(row0, nrows): hold only those rows of H (ed_sector_create_rows,
         the reference's MPI row split); H·v then maps a whole-sector vector to
         the nrows local entries.  pack=False keeps the plain SELL arrays only;
         kron2 forces the two-pass Kronecker tables on (True) or off (False);
+        split forces the two-segment stored form on (True, any size) or off
+        (False; default: built for stored matrices beyond the Infinity Cache);
         options: names of ED_OPT_* kernel alternatives (see set_options)."""
         lib = _lib.load()
         self.cfg = cfg
@@ -62,6 +65,8 @@ class Sector:
         flags |= 0 if pack else ED_NO_PACK
         if kron2 is not None:
             flags |= ED_KRON2_ON if kron2 else ED_KRON2_OFF
+        if split is not None:
+            flags |= _lib.ED_SPLIT_ON if split else _lib.ED_NO_SPLIT
         h = ctypes.c_void_p()
         if rows is None:
             check(lib.ed_sector_create(ctypes.byref(self._params), q1, q2, flags, device, None,

@@ -65,6 +65,8 @@ extern "C" {
 #define ED_NO_PACK   0x10 /* stored: plain SELL arrays only (no {col|value index} words) */
 #define ED_KRON2_OFF 0x20 /* matrix-free Kronecker form: one-pass k_kron only       */
 #define ED_KRON2_ON  0x40 /* two-pass Kronecker tables below the size threshold too */
+#define ED_NO_SPLIT  0x80 /* stored: no two-segment form (one-pass k_spmv_pk only)          */
+#define ED_SPLIT_ON  0x100 /* stored: two-segment form below the size threshold too        */
 
 /* Kernel-selection options of a built sector (ed_sector_set_options): the
  * alternatives kept for parity tests and A/B measurements.  0 = the default
@@ -85,6 +87,8 @@ extern "C" {
 #define ED_OPT_TRLAN_NOLOCAL  0x1000 /* eigh: plain w = H v_j (no shifted three-term step)     */
 #define ED_OPT_TRLAN_NOSOLO   0x2000 /* eigh: multi-kernel CGS also on sectors <= 2048 rows     */
 #define ED_OPT_TRLAN_FULLUPD  0x4000 /* eigh: full CGS update every step (no local-only update) */
+#define ED_OPT_STORED_EXACT 0x100000 /* stored H·v: the one-pass kernel (spMatVec_cc's per-row order,
+                                        bit-identical) even where the two-segment form is built */
 
 /* status codes */
 #define ED_OK              0
@@ -146,6 +150,11 @@ typedef struct ed_sector_info {
   int32_t packed;   /* 1 if stored H·v reads 32-bit {col|value index} words */
   int32_t npdict;   /* distinct off-diagonal values (packed dictionary)  */
   int64_t row0, nrows;    /* rows held: [row0, row0+nrows) (whole: 0, dim) */
+  int32_t split;    /* 1 if the two-segment stored form is built (default stored H·v) */
+  int32_t pad_;
+  int64_t split_far;          /* cross-block elements (segment B)            */
+  int64_t split_far_uniform;  /* of which stored once per 64-row slice (U)   */
+  int64_t split_bytes;        /* device bytes of the two-segment form        */
 } ed_sector_info;
 
 typedef struct ed_sector ed_sector; /* opaque */

@@ -32,6 +32,8 @@ ap.add_argument("--complex", action="store_true", help="complex(8) H values (and
 ap.add_argument("--cvec", action="store_true", help="real H, complex vectors")
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--options", default="", help="comma-separated ED_OPT_* names")
+ap.add_argument("--split", default="default", choices=["default", "on", "off"],
+                help="two-segment stored form: library default, forced on, or not built")
 a = ap.parse_args()
 if a.sector == "c4r":   # bench.py's configs[3] parameters (Uloc=(2,2,0), Ust=1, Jh=0.5), (6,6)
     from golden.golden_configs import c4_config
@@ -41,7 +43,9 @@ else:
     cfg = make_config(bath="random", seed=20251015, **kw)
 real = not a.complex
 opts = tuple(o for o in a.options.split(",") if o)
-with Sector(cfg, q[0], q[1], stored=(a.path == 0), direct=(a.path != 0), real=real, options=opts) as S:
+split = {"default": None, "on": True, "off": False}[a.split]
+with Sector(cfg, q[0], q[1], stored=(a.path == 0), direct=(a.path != 0), real=real, split=split,
+            options=opts) as S:
     dt = torch.float64 if (real and not a.cvec) else torch.complex128
     i = torch.arange(1, S.dim + 1, dtype=torch.float64, device="cuda")
     x = torch.sin(i) if dt == torch.float64 else torch.complex(torch.sin(i), torch.cos(3 * i))
@@ -68,3 +72,5 @@ with Sector(cfg, q[0], q[1], stored=(a.path == 0), direct=(a.path != 0), real=re
     print(f"per-launch events: mean {sum(each) / len(each):.5f} min {each[0]:.5f} median {each[len(each) // 2]:.5f} ms")
     print(f"sector={a.sector} dim={S.dim} nnz={S.nnz} padded={S.info.padded} path={a.path} "
           f"real={real} cvec={a.cvec} packed={S.info.packed} ndict={S.info.npdict} ms/launch={ms:.5f}")
+    if S.info.split:
+        print(f"split: far={S.info.split_far} uniform={S.info.split_far_uniform} bytes={S.info.split_bytes}")
