@@ -59,6 +59,12 @@ __device__ __forceinline__ double sub(double a, double b) { return a - b; }
 __device__ __forceinline__ double2 sub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
 __device__ __forceinline__ double scl(double s, double a) { return s * a; }
 __device__ __forceinline__ double2 scl(double s, double2 a) { return make_double2(s * a.x, s * a.y); }
+// component-wise select (a ternary on the double2 struct goes through
+// scratch memory: 5x slower complex SpMV)
+__device__ __forceinline__ double sel(bool c, double a, double b) { return c ? a : b; }
+__device__ __forceinline__ double2 sel(bool c, double2 a, double2 b) {
+  return make_double2(c ? a.x : b.x, c ? a.y : b.y);
+}
 __device__ __forceinline__ double re_of(double a) { return a; }
 __device__ __forceinline__ double re_of(double2 a) { return a.x; }
 // Re(conj(a)*b): dot_product real part
@@ -696,7 +702,7 @@ static __global__ void __launch_bounds__(kBlock) k_dict_pack_c(const int32_t* __
   }
 }
 
-template <bool HC, bool VC, int NT, class Epi>
+template <bool HC, bool VC, int NT, class Epi, int CH = kChunk>
 __global__ void __launch_bounds__(kBlock) k_spmv_pk(const val_t<HC>* __restrict__ diag,
                                                     const int64_t* __restrict__ sptr,
                                                     const uint32_t* __restrict__ words,
@@ -723,21 +729,33 @@ __global__ void __launch_bounds__(kBlock) k_spmv_pk(const val_t<HC>* __restrict_
       const int w = (int)((sptr[s + 1] - s0) >> 6);
       const uint32_t* wp = words + s0 + (i & 63);
       const V xi = xr[i];
-      V acc = add(vzero<V>(), mul(ldh<NT>(diag + i), xi));
-      for (int k0 = 0; k0 < w; k0 += kChunk) {
-        uint32_t c[kChunk];
+      const H dg = ldh<NT>(diag + i);
+      // branch-free chunks: slots past the row width reload the last slot
+      // (same lines, no new traffic) and are dropped by a select, so every
+      // load of a chunk is issued before the first wait; the diagonal
+      // product is formed after the first chunk's loads are in flight (the
+      // sum order stays spMatVec_cc's: diagonal first)
+      V acc;
+      if (w == 0) {
+        acc = add(vzero<V>(), mul(dg, xi));
+      } else {
+        const int wm = w - 1;
+        for (int k0 = 0; k0 < w; k0 += CH) {
+          uint32_t c[CH];
 #pragma unroll
-        for (int k = 0; k < kChunk; k++) c[k] = (k0 + k < w) ? ldm<NT>(wp + 64 * (k0 + k)) : (uint32_t)i;
-        V g[kChunk];
-        H h[kChunk];
+          for (int k = 0; k < CH; k++) c[k] = ldm<NT>(wp + 64 * min(k0 + k, wm));
+          V g[CH];
+          H h[CH];
 #pragma unroll
-        for (int k = 0; k < kChunk; k++) {
-          g[k] = x[c[k] & kPackColMask];
-          h[k] = sdict[c[k] >> kPackShift];
+          for (int k = 0; k < CH; k++) {
+            g[k] = x[c[k] & kPackColMask];
+            h[k] = sdict[c[k] >> kPackShift];
+          }
+          asm volatile("" ::: "memory");  // every gather in flight before the first use (complex: see k_spmv_sa)
+          if (k0 == 0) acc = add(vzero<V>(), mul(dg, xi));
+#pragma unroll
+          for (int k = 0; k < CH; k++) acc = sel(k0 + k < w, add(acc, mul(h[k], g[k])), acc);
         }
-#pragma unroll
-        for (int k = 0; k < kChunk; k++)
-          if (k0 + k < w) acc = add(acc, mul(h[k], g[k]));
       }
       part += epi.row(i, acc, xi);
     }

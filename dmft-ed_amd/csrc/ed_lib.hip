@@ -109,9 +109,15 @@ struct ed_sector {
   int64_t* d_sptrA = nullptr;
   uint32_t* d_wordsA = nullptr;
   int64_t paddedA = 0;
+  int wA_max = 0;           // widest A slice (k_spmv_pk chunk choice)
   SplitSlice* d_bsl = nullptr;
   int nbsl = 0;
-  int* d_bxoff = nullptr;   // [9] per-XCD slice ranges
+  // k_spmv_sb work lists (half-chunk-major), each cut into 8 per-XCD ranges:
+  // real vectors: items of two 64-row halves of pair slices + the generic
+  // slices; complex vectors: every half
+  int2 *d_itR = nullptr, *d_itC = nullptr;
+  int* d_glist = nullptr;
+  int* d_xoff = nullptr;    // [27]: items R | generic | items C ranges
   int2* d_ul = nullptr;
   uint32_t* d_lw = nullptr;
   int64_t nul = 0, nlw = 0, nfar = 0, nfar_u = 0;  // U entries, L words, cross-block elements (all / in U)
@@ -405,6 +411,13 @@ static int build_split(ed_sector* s) {
   HIPCK(hipMemcpyAsync(&slotsA, total, sizeof(int64_t), hipMemcpyDeviceToHost, s->stream));
   HIPCK(hipStreamSynchronize(s->stream));
   s->paddedA = slotsA;
+  {
+    std::vector<int64_t> hp(ns + 1);
+    CK(dcopy(s, hp.data(), s->d_sptrA, (ns + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
+    int wm = 0;
+    for (int64_t q = 0; q < ns; q++) wm = std::max(wm, (int)((hp[q + 1] - hp[q]) >> 6));
+    s->wA_max = wm;
+  }
   CK(dalloc_t(s, &s->d_wordsA, std::max<int64_t>(slotsA, 1)));
   hipLaunchKernelGGL(k_split_fill_a, dim3(grid_for(ns * 64)), dim3(kBlock), 0, s->stream, s->d_sptr, s->d_words,
                      s->d_cnt, s->d_map, nsp, dim, ns, s->d_sptrA, s->d_wordsA, zpad);
@@ -415,41 +428,86 @@ static int build_split(ed_sector* s) {
   int64_t maxlen = 0;
   for (int64_t b = 0; b < nblk; b++) maxlen = std::max(maxlen, T.blk_off[b + 1] - T.blk_off[b]);
   std::vector<SplitSlice> sl;
-  for (int64_t c = 0; c * 64 < maxlen; c++)
+  const int64_t R = kSplitRows;
+  const int64_t nchunk = (maxlen + R - 1) / R;
+  std::vector<int32_t> sid(nchunk * nblk, -1);  // slice of (chunk, block)
+  for (int64_t c = 0; c * R < maxlen; c++)
     for (int64_t b = 0; b < nblk; b++) {
       const int64_t len = T.blk_off[b + 1] - T.blk_off[b];
-      if (c * 64 >= len) continue;
+      if (c * R >= len) continue;
+      sid[c * nblk + b] = (int32_t)sl.size();
       SplitSlice q{};
-      q.row0 = (int32_t)(T.blk_off[b] + c * 64);
-      q.n = (int32_t)std::min<int64_t>(64, len - c * 64);
+      q.row0 = (int32_t)(T.blk_off[b] + c * R);
+      q.nfl = (int32_t)std::min<int64_t>(R, len - c * R);
       sl.push_back(q);
     }
   const int64_t nsl = (int64_t)sl.size();
   CK(dalloc_t(s, &s->d_bsl, std::max<int64_t>(nsl, 1)));
   CK(dcopy(s, s->d_bsl, sl.data(), nsl * sizeof(SplitSlice), hipMemcpyHostToDevice));
-  const int gb = (int)std::min<int64_t>((nsl + 3) / 4, 65536);
-  hipLaunchKernelGGL(k_split_b<false>, dim3(gb), dim3(kBlock), 0, s->stream, s->d_sptr, s->d_words, s->d_cnt,
+  const int gb = (int)std::min<int64_t>((nsl + 1) / 2, 65536);
+  hipLaunchKernelGGL(k_split_b<false>, dim3(gb), dim3(kSplitBuildBlock), 0, s->stream, s->d_sptr, s->d_words, s->d_cnt,
                      s->d_map, nsp, s->d_bsl, nsl, (int2*)nullptr, (uint32_t*)nullptr, zpad);
   HIPCK(hipGetLastError());
   CK(dcopy(s, sl.data(), s->d_bsl, nsl * sizeof(SplitSlice), hipMemcpyDeviceToHost));
   int64_t uo = 0, lo = 0, nfar_u = 0;
   for (SplitSlice& q : sl) {
+    nfar_u += (int64_t)q.nu * split_n(q);
+    q.nu = (q.nu + kSplitChunk - 1) / kSplitChunk * kSplitChunk;  // padded with {0, zero value}
+    q.wl = (q.wl + kSplitLChunk - 1) / kSplitLChunk * kSplitLChunk;
     q.uoff = uo;
     q.loff = lo;
     uo += q.nu;
-    lo += 64 * (int64_t)q.wl;
-    nfar_u += (int64_t)q.nu * q.n;
+    lo += kSplitRows * (int64_t)q.wl;
   }
   CK(dcopy(s, s->d_bsl, sl.data(), nsl * sizeof(SplitSlice), hipMemcpyHostToDevice));
-  CK(dalloc_t(s, &s->d_ul, std::max<int64_t>(uo, 1)));
+  // (+ one chunk: a two-slice batch may read a whole chunk at a slice with no U entries)
+  CK(dalloc_t(s, &s->d_ul, uo + kSplitChunk));
+  HIPCK(hipMemsetAsync(s->d_ul, 0, (uo + kSplitChunk) * sizeof(int2), s->stream));
   CK(dalloc_t(s, &s->d_lw, std::max<int64_t>(lo, 1)));
-  hipLaunchKernelGGL(k_split_b<true>, dim3(gb), dim3(kBlock), 0, s->stream, s->d_sptr, s->d_words, s->d_cnt,
+  hipLaunchKernelGGL(k_split_b<true>, dim3(gb), dim3(kSplitBuildBlock), 0, s->stream, s->d_sptr, s->d_words, s->d_cnt,
                      s->d_map, nsp, s->d_bsl, nsl, s->d_ul, s->d_lw, zpad);
   HIPCK(hipGetLastError());
-  // per-XCD ranges: eight equal contiguous parts of the chunk-major list
-  std::vector<int> xo(9);
-  for (int x = 0; x <= 8; x++) xo[x] = (int)((nsl * x) / 8);
-  CK(upload(s, &s->d_bxoff, xo));
+  // work lists in half-chunk-major order (k_spmv_sb)
+  std::vector<int2> itR, itC;
+  std::vector<int> gl;
+  int pend = -1;
+  for (int64_t c64 = 0; c64 < 2 * nchunk; c64++)
+    for (int64_t b = 0; b < nblk; b++) {
+      const int32_t id = sid[(c64 / 2) * nblk + b];
+      if (id < 0) continue;
+      const int h = (int)(c64 & 1);
+      const SplitSlice& q = sl[id];
+      if (64 * h >= split_n(q)) continue;
+      const int e = 2 * id + h;
+      itC.push_back(make_int2(e, -1));
+      if (!(split_flags(q) & kSplitPair)) {
+        if (h == 0) gl.push_back(id);
+        continue;
+      }
+      if (pend < 0) {
+        pend = e;
+      } else if (sl[pend >> 1].nu == q.nu && sl[pend >> 1].wl == q.wl) {
+        itR.push_back(make_int2(pend, e));
+        pend = -1;
+      } else {
+        itR.push_back(make_int2(pend, -1));
+        pend = e;
+      }
+    }
+  if (pend >= 0) itR.push_back(make_int2(pend, -1));
+  // per-XCD ranges: eight equal contiguous parts of each list
+  std::vector<int> xo(27);
+  for (int x = 0; x <= 8; x++) {
+    xo[x] = (int)((int64_t)itR.size() * x / 8);
+    xo[9 + x] = (int)((int64_t)gl.size() * x / 8);
+    xo[18 + x] = (int)((int64_t)itC.size() * x / 8);
+  }
+  if (itR.empty()) itR.push_back(make_int2(0, -1));
+  if (gl.empty()) gl.push_back(0);
+  CK(upload(s, &s->d_itR, itR));
+  CK(upload(s, &s->d_itC, itC));
+  CK(upload(s, &s->d_glist, gl));
+  CK(upload(s, &s->d_xoff, xo));
   // cross-block elements = nnz - dim - sum(nA) (the U entries cover nfar_u of them)
   unsigned long long* dn;
   HIPCK(hipMallocAsync((void**)&dn, sizeof(unsigned long long), s->stream));
@@ -1265,21 +1323,36 @@ static int launch_split(ed_sector* s, const void* x, Epi epi, hipStream_t st) {
   V* y = (V*)epi.scratch();
   EpiStore<VC> ea{y};
   const int64_t dim = s->dim, ns = s->nslice;
-  const int ga = grid_for(ns * 64) & ~7;  // XCD row ranges (k_spmv_pk's remap)
+  // XCD row ranges (k_spmv_pk's remap) on grids of >= 1,024 blocks, as xcd_on()
+  const int g0 = grid_for(ns * 64);
+  const int xa = g0 >= 1024 ? 1 : 0;
+  const int ga = xa ? (g0 & ~7) : g0;
   const bool nta = (s->paddedA * 4 + dim * (int64_t)sizeof(H)) > kSplitMinBytes;
-  if (nta)
-    hipLaunchKernelGGL((k_spmv_pk<HC, VC, 1, EpiStore<VC>>), dim3(ga), dim3(kBlock), 0, st, (const H*)s->d_diag,
-                       s->d_sptrA, s->d_wordsA, (const H*)s->d_pdict, (const V*)x, (const V*)x, dim, ns, ea, 1);
-  else
-    hipLaunchKernelGGL((k_spmv_pk<HC, VC, 0, EpiStore<VC>>), dim3(ga), dim3(kBlock), 0, st, (const H*)s->d_diag,
-                       s->d_sptrA, s->d_wordsA, (const H*)s->d_pdict, (const V*)x, (const V*)x, dim, ns, ea, 1);
+  // rows of <= 8 in-block elements (every Norb=1 sector up to Nbath 15):
+  // chunks of 8 slots, not 16 (fewer padding gathers); two slices per wave
+  (void)ea;
+  (void)ga;
+  (void)xa;
+#define ED_SPA(NTV, CH)                                                                                       \
+  hipLaunchKernelGGL((k_spmv_sa<HC, VC, NTV, CH, 2>), dim3(kSplitAGrid), dim3(kBlock), 0, st,                  \
+                     (const H*)s->d_diag, s->d_sptrA, s->d_wordsA, (const H*)s->d_pdict, (const V*)x, y, dim, ns)
+  if (s->wA_max <= 8) {
+    if (nta) ED_SPA(1, 8);
+    else ED_SPA(0, 8);
+  } else {
+    if (nta) ED_SPA(1, kChunk);
+    else ED_SPA(0, kChunk);
+  }
+#undef ED_SPA
   HIPCK(hipGetLastError());
   if (s->nlw * 4 > kSplitMinBytes)
-    hipLaunchKernelGGL((k_spmv_sb<HC, VC, 1, Epi>), dim3(kSplitGrid), dim3(kBlock), 0, st, s->d_bsl, s->d_bxoff,
-                       s->d_ul, s->d_lw, (const H*)s->d_pdict, (const V*)x, (const V*)y, epi);
+    hipLaunchKernelGGL((k_spmv_sb<HC, VC, 1, Epi>), dim3(kSplitGrid), dim3(kBlock), 0, st, s->d_bsl,
+                       VC ? s->d_itC : s->d_itR, s->d_xoff + (VC ? 18 : 0), s->d_glist, s->d_xoff + 9, s->d_ul,
+                       s->d_lw, (const H*)s->d_pdict, (const V*)x, (const V*)y, epi);
   else
-    hipLaunchKernelGGL((k_spmv_sb<HC, VC, 0, Epi>), dim3(kSplitGrid), dim3(kBlock), 0, st, s->d_bsl, s->d_bxoff,
-                       s->d_ul, s->d_lw, (const H*)s->d_pdict, (const V*)x, (const V*)y, epi);
+    hipLaunchKernelGGL((k_spmv_sb<HC, VC, 0, Epi>), dim3(kSplitGrid), dim3(kBlock), 0, st, s->d_bsl,
+                       VC ? s->d_itC : s->d_itR, s->d_xoff + (VC ? 18 : 0), s->d_glist, s->d_xoff + 9, s->d_ul,
+                       s->d_lw, (const H*)s->d_pdict, (const V*)x, (const V*)y, epi);
   HIPCK(hipGetLastError());
   return ED_OK;
 }

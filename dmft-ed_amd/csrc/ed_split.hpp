@@ -12,20 +12,21 @@
 //     in-block elements (target state with the row's down pattern idw: the
 //     same DimUp-long V row) -> y;
 //   segment B (k_spmv_sb, column-chunk order): the cross-block elements of
-//     <= 64 consecutive rows of one block (a B slice), added to y -> Hv, with
-//     the Lanczos epilogues fused.  B slices are walked chunk-major: XCD x
-//     takes the chunks c = x, x+8, ... of every block, so the rows one XCD
-//     works on at a time read V[:, 64c : 64c+64] (DimDw x 512 B at N28:
-//     1.8 MB), which stays in its L2.
+//     <= 128 consecutive rows of one block (a B slice), added to y -> Hv,
+//     with the Lanczos epilogues fused.  B slices are walked chunk-major
+//     (chunk c = in-block rows [128c, 128c + 128) of every block) and the
+//     list is cut into eight contiguous parts, one per XCD, so the rows one
+//     XCD works on at a time read V[:, 128c : 128c+128] (DimDw x 1 KB at
+//     N28: 3.5 MB), which stays in its L2.
 //
 // The B elements of a slice that every lane has with the same column offset
 // and value (the down-spin hops of normal and nonSU2 sectors: target
 // (idw', same up rank), same Jordan-Wigner sign, same value) are stored once
 // per slice as a U entry {col - row, dictionary index}: a wave-uniform scalar
-// load and one coalesced 512-B gather.  The rest (spin flips, Jx/Jp, pair
+// load and one coalesced 1-KB gather (16 B per lane).  The rest (spin flips, Jx/Jp, pair
 // terms) stay per lane as packed words {col:24 | index:8} (L words).  The
 // re-lay is lossless: every stored element appears exactly once, with the
-// stored double, and the build checks the element count.
+// stored double (sector info reports the cross-block count and its U share).
 //
 // Summation order: diagonal, in-block elements in insertion order, then U,
 // then L elements — a reordering of spMatVec_cc's row sum (parity 1e-13
@@ -39,17 +40,26 @@
 
 namespace edg {
 
-// One B slice: n <= 64 consecutive rows [row0, row0 + n) of one idw block.
+// One B slice: n <= kSplitRows consecutive rows [row0, row0 + n) of one idw
+// block.  L words slot-major: word k of row row0 + r at loff + 128 k + r.
+// (all fields 32- or 64-bit: the kernel reads a slice with scalar loads)
 struct SplitSlice {
   int32_t row0;
-  int32_t n;
-  int32_t nu;    // U entries
-  int32_t wl;    // L words per lane (slots)
+  int32_t nfl;   // rows n | flags << 16 (kSplitPair: row0, n and every U column offset even)
+  int32_t nu;    // U entries, padded to a multiple of kSplitChunk with {0, zero value}
+  int32_t wl;    // L words per row (slots), padded to a multiple of kSplitLChunk
   int64_t uoff;  // first U entry
-  int64_t loff;  // first L word (the slice's 64 * wl words, slot-major)
+  int64_t loff;  // first L word (the slice's kSplitRows * wl words, slot-major)
 };
 constexpr int kSplitFarMax = 32;   // cross-block elements per row the build handles
-constexpr int kSplitGrid = 2048;   // k_spmv_sb blocks (a multiple of 8: one list per XCD)
+constexpr int kSplitRows = 128;    // rows per B slice (two per lane)
+constexpr int kSplitPair = 1;      // SplitSlice flag: 16-byte pair gathers apply
+constexpr int kSplitChunk = 8;     // U elements per load batch (U lists padded to it)
+constexpr int kSplitLChunk = 4;    // L slots per load batch (L widths padded to it)
+__host__ __device__ inline int split_n(const SplitSlice& q) { return q.nfl & 0xffff; }
+__host__ __device__ inline int split_flags(const SplitSlice& q) { return q.nfl >> 16; }
+constexpr int kSplitAGrid = 2048;  // k_spmv_sa blocks (a multiple of 8: one slice range per XCD)
+constexpr int kSplitGrid = 1280;   // k_spmv_sb blocks (a multiple of 8: one list per XCD; pass D's grid)
 
 // ---- build: segment A
 // nA[i] = in-block elements of row i; widthA[s] = max over slice s.  Also the
@@ -111,84 +121,281 @@ static __global__ void __launch_bounds__(kBlock) k_split_fill_a(const int64_t* _
   }
 }
 
-// ---- build: segment B (one wavefront per slice).  FILL = false: nu, wl per
-// slice; FILL = true: the U list and the L words at the slice's offsets.
-// The lane's cross-block elements are staged in LDS as 64-bit keys
-// {col - row : 32 | dictionary index : 32}; an element of lane 0 is uniform
-// when every active lane holds the same key.
+// ---- build: segment B (one wavefront per slice of <= 128 rows, two
+// adjacent rows per lane).  FILL = false: nu, wl per slice; FILL = true: the
+// U list and the L words at the slice's offsets.  Each row's cross-block
+// elements are staged in LDS as 64-bit keys {col - row : 32 | dictionary
+// index : 32}; an element of the slice's first row is uniform when every
+// row of the slice holds the same key.
+constexpr int kSplitBuildBlock = 128;  // 2 waves: 2 x 32 x 128 keys = 64 KB of LDS
 template <bool FILL>
-__global__ void __launch_bounds__(kBlock) k_split_b(const int64_t* __restrict__ sptr,
-                                                   const uint32_t* __restrict__ words,
-                                                   const uint16_t* __restrict__ cnt,
-                                                   const uint32_t* __restrict__ map, int ns,
-                                                   SplitSlice* __restrict__ sl, int64_t nsl,
-                                                   int2* __restrict__ ul, uint32_t* __restrict__ lw,
-                                                   uint32_t zpad) {
-  __shared__ unsigned long long keys[kBlock / 64][kSplitFarMax][64];
+__global__ void __launch_bounds__(kSplitBuildBlock) k_split_b(const int64_t* __restrict__ sptr,
+                                                             const uint32_t* __restrict__ words,
+                                                             const uint16_t* __restrict__ cnt,
+                                                             const uint32_t* __restrict__ map, int ns,
+                                                             SplitSlice* __restrict__ sl, int64_t nsl,
+                                                             int2* __restrict__ ul, uint32_t* __restrict__ lw,
+                                                             uint32_t zpad) {
+  constexpr int NW = kSplitBuildBlock / 64;
+  __shared__ unsigned long long keys[NW][kSplitFarMax][kSplitRows];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int64_t q = (int64_t)blockIdx.x * (kBlock / 64) + wv; q < nsl; q += (int64_t)gridDim.x * (kBlock / 64)) {
+  for (int64_t q = (int64_t)blockIdx.x * NW + wv; q < nsl; q += (int64_t)gridDim.x * NW) {
     const int qq = __builtin_amdgcn_readfirstlane((int)q);
     const SplitSlice S = sl[qq];
-    const bool on = lane < S.n;
-    const int64_t i = S.row0 + (on ? lane : 0);
-    int nf = 0;
-    if (on) {
+    int nf[2] = {0, 0};
+    bool on[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int r = 2 * lane + h;
+      on[h] = r < split_n(S);
+      if (!on[h]) continue;
+      const int64_t i = S.row0 + r;
       const uint32_t blk = map[i] >> ns;
       const uint32_t* wp = words + sptr[i >> 6] + (i & 63);
       const int n = cnt[i];
-      for (int k = 0; k < n && nf < kSplitFarMax; k++) {
+      for (int k = 0; k < n && nf[h] < kSplitFarMax; k++) {
         const uint32_t wd = wp[64 * k];
         const uint32_t col = wd & kPackColMask;
         if ((map[col] >> ns) != blk)
-          keys[wv][nf++][lane] = ((unsigned long long)(uint32_t)((int32_t)col - (int32_t)i) << 32) |
+          keys[wv][nf[h]++][r] = ((unsigned long long)(uint32_t)((int32_t)col - (int32_t)i) << 32) |
                                  (wd >> kPackShift);
       }
     }
-    const int nf0 = __builtin_amdgcn_readfirstlane(nf);  // lane 0 is always active
-    uint32_t used = 0;
+    const int nf0 = __builtin_amdgcn_readfirstlane(nf[0]);  // row 0 of the slice always exists
+    uint32_t used[2] = {0u, 0u};
     int nu = 0;
+    bool even = true;  // every U column offset even
     for (int k0 = 0; k0 < nf0; k0++) {
       const unsigned long long key = keys[wv][k0][0];
-      int pos = -1;
-      for (int j = 0; j < nf; j++)
-        if (keys[wv][j][lane] == key) pos = j;
-      const bool all = __ballot(!on || pos >= 0) == __ballot(1);
-      if (all) {
-        if (on) used |= 1u << pos;
+      int pos[2] = {-1, -1};
+#pragma unroll
+      for (int h = 0; h < 2; h++)
+        for (int j = 0; j < nf[h]; j++)
+          if (keys[wv][j][2 * lane + h] == key) pos[h] = j;
+      const bool mine = (!on[0] || pos[0] >= 0) && (!on[1] || pos[1] >= 0);
+      if (__ballot(mine) == __ballot(1)) {
+#pragma unroll
+        for (int h = 0; h < 2; h++)
+          if (on[h]) used[h] |= 1u << pos[h];
         if constexpr (FILL) {
           if (lane == 0) ul[S.uoff + nu] = make_int2((int32_t)(key >> 32), (int32_t)(key & 0xffu));
         }
+        even = even && !((key >> 32) & 1u);
         nu++;
       }
     }
-    const int nl = nf - __popc(used);
+    const int nl = max(on[0] ? nf[0] - __popc(used[0]) : 0, on[1] ? nf[1] - __popc(used[1]) : 0);
+    if constexpr (FILL) {
+      // pad the U list to the slice's (padded) count with {0, zero value}
+      for (int k = nu + lane; k < S.nu; k += 64) ul[S.uoff + k] = make_int2(0, (int32_t)(zpad >> kPackShift));
+    }
     if constexpr (!FILL) {
-      const int wl = wave_max(on ? nl : 0);
+      const int wl = wave_max(nl);
       if (lane == 0) {
+        const int n = split_n(S);
         sl[qq].nu = nu;
         sl[qq].wl = wl;
+        sl[qq].nfl = n | (((even && !(S.row0 & 1) && !(n & 1)) ? kSplitPair : 0) << 16);
       }
     } else {
-      uint32_t* lp = lw + S.loff + lane;
-      int k2 = 0;
-      for (int j = 0; j < nf; j++)
-        if (!((used >> j) & 1u)) {
-          const unsigned long long kk = keys[wv][j][lane];
-          lp[64 * (k2++)] = (uint32_t)((int32_t)i + (int32_t)(kk >> 32)) | ((uint32_t)(kk & 0xffu) << kPackShift);
-        }
-      for (; k2 < S.wl; k2++) lp[64 * k2] = (uint32_t)i | zpad;
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const int r = 2 * lane + h;
+        const int64_t i = S.row0 + (on[h] ? r : 0);
+        uint32_t* lp = lw + S.loff + r;
+        int k2 = 0;
+        if (on[h])
+          for (int j = 0; j < nf[h]; j++)
+            if (!((used[h] >> j) & 1u)) {
+              const unsigned long long kk = keys[wv][j][r];
+              lp[kSplitRows * (k2++)] =
+                  (uint32_t)((int32_t)i + (int32_t)(kk >> 32)) | ((uint32_t)(kk & 0xffu) << kPackShift);
+            }
+        for (; k2 < S.wl; k2++) lp[kSplitRows * k2] = (uint32_t)i | zpad;
+      }
     }
   }
 }
 
 // ---- segment B H·v: y (segment A's rows) + the slice's cross-block
-// elements -> epilogue.  One wavefront per slice; XCD x walks its own list
-// [xoff[x], xoff[x+1]) (chunk-major) with the blocks dealt to it.
-constexpr int kSplitChunk = 8;
-template <bool HC, bool VC, int NT, class Epi>
-__global__ void __launch_bounds__(kBlock) k_spmv_sb(const SplitSlice* __restrict__ sl, const int* __restrict__ xoff,
-                                                    const int2* __restrict__ ul, const uint32_t* __restrict__ lw,
+// elements -> epilogue.  One wavefront per slice of <= 128 rows, lane l
+// taking rows 2l and 2l+1.  Pair slices (kSplitPair: row0, n and every U
+// column offset even) on a 16-byte aligned real vector gather each U element
+// of the two rows with one 16-byte load (as pass D of the two-pass Kronecker
+// H·v), branch-free; other slices take two 8-byte (or 16-byte complex)
+// gathers per element.  XCD x walks its own part [xoff[x], xoff[x+1]) of the
+// chunk-major list with the blocks dealt to it.
+// ---- segment A H·v: y = diag .* x + in-block elements, row order.  The
+// in-block gathers stay inside the row's own DimUp-long V row, so the rows
+// are walked in order: XCD x takes the x-th eighth of the 64-row slices
+// (its L2 holds the V rows its neighbouring slices read); a wavefront takes
+// R consecutive slices at a time with every load of the R slices in flight
+// before the first is summed (a one-row-per-thread grid exposes the
+// sptr -> words -> gathers latency chain once per row).
+template <bool HC, bool VC, int NT, int CH, int R>
+__global__ void __launch_bounds__(kBlock) k_spmv_sa(const val_t<HC>* __restrict__ diag, const int64_t* __restrict__ sptr,
+                                                    const uint32_t* __restrict__ words,
                                                     const val_t<HC>* __restrict__ dict,
+                                                    const val_t<VC>* __restrict__ x, val_t<VC>* __restrict__ y,
+                                                    int64_t dim, int64_t nslice) {
+  using V = val_t<VC>;
+  using H = val_t<HC>;
+  __shared__ H sdict[256];
+  sdict[threadIdx.x] = dict[threadIdx.x];  // kBlock == 256 == dictionary capacity
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int xcd = blockIdx.x & 7;
+  const int64_t s_lo = nslice * xcd / 8, s_hi = nslice * (xcd + 1) / 8;
+  const int64_t nwx = (int64_t)(gridDim.x >> 3) * (kBlock / 64);  // waves per XCD
+  for (int64_t s0 = s_lo + R * ((int64_t)(blockIdx.x >> 3) * (kBlock / 64) + wv); s0 < s_hi; s0 += R * nwx) {
+    int64_t b[R + 1];
+    int w[R];
+    int64_t i[R];
+    bool ok[R];
+#pragma unroll
+    for (int r = 0; r <= R; r++) b[r] = sptr[min(s0 + r, s_hi)];
+    int wmax = 0;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      w[r] = (int)((b[r + 1] - b[r]) >> 6);  // 0 for a slice past s_hi
+      wmax = max(wmax, w[r]);
+      i[r] = (s0 + r) * 64 + lane;
+      ok[r] = s0 + r < s_hi && i[r] < dim;
+      if (!ok[r]) i[r] = s0 * 64;            // a valid row (row s0*64 < dim)
+    }
+    V xi[R], acc[R];
+    H dg[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      xi[r] = x[i[r]];
+      dg[r] = ldh<NT>(diag + i[r]);
+    }
+    for (int k0 = 0; k0 < wmax || k0 == 0; k0 += CH) {
+      uint32_t c[R][CH];
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        const uint32_t* wp = words + b[r] + lane;
+        if (w[r] > 0) {  // (wave-uniform: one branch per slice, none per slot)
+#pragma unroll
+          for (int k = 0; k < CH; k++) c[r][k] = ldm<NT>(wp + 64 * min(k0 + k, w[r] - 1));
+        } else {
+#pragma unroll
+          for (int k = 0; k < CH; k++) c[r][k] = (uint32_t)i[r];
+        }
+      }
+      V g[R][CH];
+      H h[R][CH];
+#pragma unroll
+      for (int r = 0; r < R; r++)
+#pragma unroll
+        for (int k = 0; k < CH; k++) {
+          g[r][k] = x[c[r][k] & kPackColMask];
+          h[r][k] = sdict[c[r][k] >> kPackShift];
+        }
+      // every gather issued before the first is used (without this fence the
+      // scheduler sinks the complex gathers to their uses: one round trip per
+      // element, 0.73 ms per N28 launch instead of ~0.2)
+      asm volatile("" ::: "memory");
+      if (k0 == 0) {
+#pragma unroll
+        for (int r = 0; r < R; r++) acc[r] = mul(dg[r], xi[r]);
+      }
+#pragma unroll
+      for (int r = 0; r < R; r++)
+#pragma unroll
+        for (int k = 0; k < CH; k++) acc[r] = sel(k0 + k < w[r], add(acc[r], mul(h[r][k], g[r][k])), acc[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++)
+      if (ok[r]) {
+        if constexpr (VC) {
+          typedef double d2 __attribute__((ext_vector_type(2)));
+          __builtin_nontemporal_store(d2{acc[r].x, acc[r].y}, (d2*)(y + i[r]));
+        } else {
+          __builtin_nontemporal_store(acc[r], y + i[r]);
+        }
+      }
+  }
+}
+
+typedef double sb_d2 __attribute__((ext_vector_type(2)));
+typedef unsigned int sb_u2 __attribute__((ext_vector_type(2)));
+
+// one 128-row slice in the generic form: the lane's two rows apart (8-byte
+// gathers), for slices without the pair property
+template <bool HC, bool VC, int NT, class Epi>
+__device__ __forceinline__ double sb_generic(const SplitSlice& S, int lane, const int2* __restrict__ ul,
+                                             const uint32_t* __restrict__ lw, const val_t<HC>* sdict,
+                                             const val_t<VC>* __restrict__ x, const val_t<VC>* y, Epi& epi) {
+  using V = val_t<VC>;
+  using H = val_t<HC>;
+  const int n = split_n(S);
+  const bool on0 = 2 * lane < n, on1 = 2 * lane + 1 < n;
+  const int i0 = S.row0 + (on0 ? 2 * lane : 0);  // idle lanes: the slice's first row
+  const int i1 = on1 ? i0 + 1 : i0;
+  const int2* up = ul + S.uoff;
+  const uint32_t* wp = lw + S.loff + 2 * lane;
+  V a0 = y[i0], a1 = y[i1];
+  for (int k0 = 0; k0 < S.nu; k0 += kSplitChunk) {
+    int2 e[kSplitChunk];
+    V g0[kSplitChunk], g1[kSplitChunk];
+#pragma unroll
+    for (int k = 0; k < kSplitChunk; k++) e[k] = up[k0 + k];  // padded list: whole chunks
+#pragma unroll
+    for (int k = 0; k < kSplitChunk; k++) {
+      g0[k] = x[i0 + e[k].x];
+      g1[k] = x[i1 + e[k].x];
+    }
+    asm volatile("" ::: "memory");  // all gathers in flight before the first use
+#pragma unroll
+    for (int k = 0; k < kSplitChunk; k++) {
+      const H h = sdict[e[k].y];
+      a0 = add(a0, mul(h, g0[k]));
+      a1 = add(a1, mul(h, g1[k]));
+    }
+  }
+  for (int k0 = 0; k0 < S.wl; k0 += kSplitLChunk) {
+    sb_u2 c[kSplitLChunk];
+    V g0[kSplitLChunk], g1[kSplitLChunk];
+#pragma unroll
+    for (int k = 0; k < kSplitLChunk; k++) c[k] = ldm<NT>((const sb_u2*)(wp + kSplitRows * (k0 + k)));
+#pragma unroll
+    for (int k = 0; k < kSplitLChunk; k++) {
+      g0[k] = x[c[k].x & kPackColMask];
+      g1[k] = x[c[k].y & kPackColMask];
+    }
+#pragma unroll
+    for (int k = 0; k < kSplitLChunk; k++) {
+      a0 = add(a0, mul(sdict[c[k].x >> kPackShift], g0[k]));
+      a1 = add(a1, mul(sdict[c[k].y >> kPackShift], g1[k]));
+    }
+  }
+  double part = 0.0;
+  if (on0) part += epi.row((int64_t)i0, a0, x[i0]);
+  if (on1) part += epi.row((int64_t)i1, a1, x[i1]);
+  return part;
+}
+
+// ---- segment B H·v: y (segment A's rows) + the slices' cross-block
+// elements -> epilogue.  Slices are walked in 64-row halves, chunk-major
+// (half-chunk c = in-block rows [64c, 64c + 64) of every block): the V
+// columns one XCD reads at a time are DimDw x 512 B (1.8 MB at N28), which
+// stay in its L2 beside the y and Hv streams (128-row chunks: V fetched
+// ~2.9x).
+//   real vectors: a wavefront takes an item of two halves (of two blocks)
+//     with equal U / L counts, 32 lanes each, two adjacent rows per lane:
+//     every U element of the two rows is one 16-byte gather (pair slices:
+//     kSplitPair), both halves' U lists read with scalar loads and selected
+//     per lane group; slices without the pair property go through the
+//     generic list, one 128-row slice per wavefront;
+//   complex vectors: one half per wavefront, one row (16 B) per lane.
+// Returns nothing; the epilogue's partials via epi.finish.
+template <bool HC, bool VC, int NT, class Epi>
+__global__ void __launch_bounds__(kBlock) k_spmv_sb(const SplitSlice* __restrict__ sl, const int2* __restrict__ items,
+                                                    const int* __restrict__ xoffI, const int* __restrict__ glist,
+                                                    const int* __restrict__ xoffG, const int2* __restrict__ ul,
+                                                    const uint32_t* __restrict__ lw, const val_t<HC>* __restrict__ dict,
                                                     const val_t<VC>* __restrict__ x, const val_t<VC>* y, Epi epi) {
   using V = val_t<VC>;
   using H = val_t<HC>;
@@ -200,38 +407,111 @@ __global__ void __launch_bounds__(kBlock) k_spmv_sb(const SplitSlice* __restrict
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int xcd = blockIdx.x & 7, g8 = gridDim.x >> 3;
-  const int lo = xoff[xcd], hi = xoff[xcd + 1];
+  const int w0 = (int)(blockIdx.x >> 3) * (kBlock / 64) + wv, nwx = g8 * (kBlock / 64);
   double part = 0.0;
-  for (int q = lo + (int)(blockIdx.x >> 3) * (kBlock / 64) + wv; q < hi; q += g8 * (kBlock / 64)) {
-    const SplitSlice S = sl[q];
-    const bool on = lane < S.n;
-    const int i = S.row0 + (on ? lane : 0);
-    V acc = y[i];
-    const int2* up = ul + S.uoff;
-    for (int k0 = 0; k0 < S.nu; k0 += kSplitChunk) {
-      int2 e[kSplitChunk];
-      V g[kSplitChunk];
+  if constexpr (!VC) {
+    // ---- items: two halves per wavefront, 16-byte pair gathers
+    const int grp = lane >> 5, l = lane & 31;
+    for (int q = xoffI[xcd] + w0; q < xoffI[xcd + 1]; q += nwx) {
+      const int2 it = items[q];
+      const bool hasB = it.y >= 0;
+      const SplitSlice SA = sl[it.x >> 1];
+      const SplitSlice SB = sl[(hasB ? it.y : it.x) >> 1];
+      const int nu = SA.nu, wl = SA.wl;  // equal in both halves (build)
+      const int half = grp ? (hasB ? it.y & 1 : it.x & 1) : it.x & 1;
+      const int row0 = grp ? SB.row0 : SA.row0;
+      const int n = split_n(grp ? SB : SA);
+      const int r = 64 * half + 2 * l;
+      const bool on = r < n && (grp == 0 || hasB);
+      const int i0 = row0 + (r < n ? r : 64 * half);  // idle lanes: the half's first pair
+      sb_d2 acc = *(const sb_d2*)(y + i0);
+      for (int k0 = 0; k0 < nu; k0 += kSplitChunk) {
+        int2 ea[kSplitChunk], eb[kSplitChunk];
 #pragma unroll
-      for (int k = 0; k < kSplitChunk; k++) e[k] = k0 + k < S.nu ? up[k0 + k] : make_int2(0, 0);
+        for (int k = 0; k < kSplitChunk; k++) {
+          ea[k] = ul[SA.uoff + k0 + k];
+          eb[k] = ul[SB.uoff + k0 + k];
+        }
+        sb_d2 g[kSplitChunk];
+        int ix[kSplitChunk];
 #pragma unroll
-      for (int k = 0; k < kSplitChunk; k++) g[k] = x[i + e[k].x];
+        for (int k = 0; k < kSplitChunk; k++) {
+          const int d = grp ? eb[k].x : ea[k].x;
+          ix[k] = grp ? eb[k].y : ea[k].y;
+          g[k] = *(const sb_d2*)(x + i0 + d);
+        }
+        asm volatile("" ::: "memory");  // all gathers in flight before the first use
 #pragma unroll
-      for (int k = 0; k < kSplitChunk; k++)
-        if (k0 + k < S.nu) acc = add(acc, mul(sdict[e[k].y], g[k]));
+        for (int k = 0; k < kSplitChunk; k++) {
+          const H h = sdict[ix[k]];
+          acc.x = add(acc.x, mul(h, g[k].x));
+          acc.y = add(acc.y, mul(h, g[k].y));
+        }
+      }
+      const uint32_t* wp = lw + (grp ? SB.loff : SA.loff) + (i0 - row0);
+      for (int k0 = 0; k0 < wl; k0 += kSplitLChunk) {
+        sb_u2 c[kSplitLChunk];
+        double g0[kSplitLChunk], g1[kSplitLChunk];
+#pragma unroll
+        for (int k = 0; k < kSplitLChunk; k++) c[k] = ldm<NT>((const sb_u2*)(wp + kSplitRows * (k0 + k)));
+#pragma unroll
+        for (int k = 0; k < kSplitLChunk; k++) {
+          g0[k] = x[c[k].x & kPackColMask];
+          g1[k] = x[c[k].y & kPackColMask];
+        }
+#pragma unroll
+        for (int k = 0; k < kSplitLChunk; k++) {
+          acc.x = add(acc.x, mul(sdict[c[k].x >> kPackShift], g0[k]));
+          acc.y = add(acc.y, mul(sdict[c[k].y >> kPackShift], g1[k]));
+        }
+      }
+      if (on) {
+        if constexpr (std::is_same_v<Epi, EpiStore<false>>) {
+          __builtin_nontemporal_store(acc, (sb_d2*)(epi.hv + i0));  // one 16-byte store (as pass D)
+        } else {
+          const sb_d2 xo = *(const sb_d2*)(x + i0);
+          part += epi.row((int64_t)i0, acc.x, xo.x);
+          part += epi.row((int64_t)i0 + 1, acc.y, xo.y);
+        }
+      }
     }
-    const uint32_t* wp = lw + S.loff + lane;
-    for (int k0 = 0; k0 < S.wl; k0 += kSplitChunk) {
-      uint32_t c[kSplitChunk];
-      V g[kSplitChunk];
+    // ---- generic slices (no pair property): one 128-row slice per wavefront
+    for (int q = xoffG[xcd] + w0; q < xoffG[xcd + 1]; q += nwx)
+      part += sb_generic<HC, VC, NT>(sl[glist[q]], lane, ul, lw, sdict, x, y, epi);
+  } else {
+    // ---- complex vectors: one 64-row half per wavefront, one row per lane
+    for (int q = xoffI[xcd] + w0; q < xoffI[xcd + 1]; q += nwx) {
+      const int e = items[q].x;
+      const SplitSlice S = sl[e >> 1];
+      const int half = e & 1;
+      const int r = 64 * half + lane;
+      const bool on = r < split_n(S);
+      const int i0 = S.row0 + (on ? r : 64 * half);
+      V acc = y[i0];
+      for (int k0 = 0; k0 < S.nu; k0 += kSplitChunk) {
+        int2 ek[kSplitChunk];
+        V g[kSplitChunk];
 #pragma unroll
-      for (int k = 0; k < kSplitChunk; k++) c[k] = k0 + k < S.wl ? ldm<NT>(wp + 64 * (k0 + k)) : (uint32_t)i;
+        for (int k = 0; k < kSplitChunk; k++) ek[k] = ul[S.uoff + k0 + k];
 #pragma unroll
-      for (int k = 0; k < kSplitChunk; k++) g[k] = x[c[k] & kPackColMask];
+        for (int k = 0; k < kSplitChunk; k++) g[k] = x[i0 + ek[k].x];
+        asm volatile("" ::: "memory");
 #pragma unroll
-      for (int k = 0; k < kSplitChunk; k++)
-        if (k0 + k < S.wl) acc = add(acc, mul(sdict[c[k] >> kPackShift], g[k]));
+        for (int k = 0; k < kSplitChunk; k++) acc = add(acc, mul(sdict[ek[k].y], g[k]));
+      }
+      const uint32_t* wp = lw + S.loff + (i0 - S.row0);
+      for (int k0 = 0; k0 < S.wl; k0 += kSplitLChunk) {
+        uint32_t c[kSplitLChunk];
+        V g[kSplitLChunk];
+#pragma unroll
+        for (int k = 0; k < kSplitLChunk; k++) c[k] = ldm<NT>(wp + kSplitRows * (k0 + k));
+#pragma unroll
+        for (int k = 0; k < kSplitLChunk; k++) g[k] = x[c[k] & kPackColMask];
+#pragma unroll
+        for (int k = 0; k < kSplitLChunk; k++) acc = add(acc, mul(sdict[c[k] >> kPackShift], g[k]));
+      }
+      if (on) part += epi.row((int64_t)i0, acc, x[i0]);
     }
-    if (on) part += epi.row((int64_t)i, acc, x[i]);
   }
   epi.finish(part);
 }

@@ -136,7 +136,8 @@ def test_complex_vr_stored_semantics():
 def test_full_size_roofline_sectors(pin):
     """Nlevels=28 (7,7) sectors at full size (dim 11,778,624): nnz pins of the
     reference run, size-independent properties: hermiticity <x,Hy> = <Hx,y>,
-    stored == generic matrix-free bit for bit, Kronecker to 1e-13."""
+    the one-pass stored kernel (ED_OPT_STORED_EXACT) == generic matrix-free
+    bit for bit, the default two-segment stored kernel and Kronecker to 1e-13."""
     import json
     import os
 
@@ -157,8 +158,14 @@ def test_full_size_roofline_sectors(pin):
         a, b = torch.dot(y, hx).item(), torch.dot(hy, x).item()
         assert abs(a - b) <= 1e-12 * abs(a)
         h1 = torch.empty_like(x)
+        assert S.info.split == 1              # HBM-sized: the two-segment form is the default
+        S.set_options("stored_exact")
+        he = torch.empty_like(x)
+        S.hxv_dev(x, he, path=0)
+        S.set_options()
+        assert (he - hx).abs().max().item() <= 1e-13 * hx.abs().max().item()
         S.hxv_dev(x, h1, path=1)
-        assert torch.equal(h1, hx)
+        assert torch.equal(h1, he)
         S.hxv_dev(x, h1, path=2)
         assert (h1 - hx).abs().max().item() <= 1e-13 * hx.abs().max().item()
 
@@ -193,14 +200,15 @@ def test_packed_matches_plain_sell(name, factory, sectors):
 @pytest.mark.parametrize("cplx", [False, True])
 def test_n28_packed_matches_plain(cplx):
     """Nlevels=28 sector (matrix beyond the MALL: non-temporal matrix loads,
-    XCD-remapped block order on the packed kernel): packed real / complex H
-    gives H·v identical to the plain SELL arrays."""
+    XCD-remapped block order on the packed kernel): the one-pass packed real /
+    complex H (ED_OPT_STORED_EXACT: the two-segment form is this sector's
+    default) gives H·v identical to the plain SELL arrays."""
     from edgpu.hamiltonian import Sector
     from edgpu.params import make_config
 
     cfg = make_config(Norb=1, Nbath=13, bath="random", seed=3)
     g = torch.Generator(device="cuda:0").manual_seed(1)
-    with Sector(cfg, 7, 7, stored=True, real=not cplx) as S:
+    with Sector(cfg, 7, 7, stored=True, real=not cplx, options=("stored_exact",)) as S:
         with Sector(cfg, 7, 7, stored=True, real=not cplx, pack=False) as P:
             assert S.info.packed == 1 and P.info.packed == 0
             dt = torch.complex128 if cplx else torch.float64
