@@ -53,9 +53,10 @@ def test_split_hxv_matches_oracle(name, factory, sectors):
         for real in reals:
             with Sector(cfg, q1, q2, stored=True, real=real, split=True) as S:
                 # (a sector without off-diagonal elements has no packed words
-                # and keeps the one-pass kernel)
+                # and keeps the one-pass kernel; complex(8) H keeps it too:
+                # the two-segment form serves real H on real vectors)
                 assert S.info.packed == (1 if S.nnz > S.dim else 0)
-                assert S.info.split == S.info.packed, "two-segment form not built"
+                assert S.info.split == (S.info.packed if real else 0), "two-segment form not built"
                 assert 0 <= S.info.split_far_uniform <= S.info.split_far <= S.nnz - S.dim
                 i = np.arange(1, S.dim + 1, dtype=np.float64)
                 xs = [start_vector(S.dim)]
@@ -68,7 +69,10 @@ def test_split_hxv_matches_oracle(name, factory, sectors):
                     y = torch.empty_like(xd)
                     S.hxv_dev(xd, y, path=0)
                     torch.cuda.synchronize()
-                    _check_rows(y.cpu().numpy(), ref, bound)
+                    if np.isrealobj(x):
+                        _check_rows(y.cpu().numpy(), ref, bound)
+                    else:  # complex vectors: the one-pass kernel, bit-exact
+                        np.testing.assert_array_equal(y.cpu().numpy(), ref)
                     S.set_options("stored_exact")                  # one-pass kernel: bit-exact
                     S.hxv_dev(xd, y, path=0)
                     torch.cuda.synchronize()
@@ -116,11 +120,12 @@ def test_split_lanczos_matches_oracle(real):
 
 def test_split_eigh_matches_dense():
     """Thick-restart eigh (shifted three-term epilogue in segment B) on a
-    split nonSU2 sector: the 6 lowest eigenvalues at 1e-10 vs dense eigh."""
+    split nonSU2 sector (spin flips: per-lane L words beside the U entries):
+    the 6 lowest eigenvalues at 1e-10 vs dense eigh."""
     from edgpu.hamiltonian import Sector
-    from cases import nonsu2_rand
+    from cases import c5
 
-    cfg = nonsu2_rand()
+    cfg = c5()
     orc = Oracle(cfg)
     hmap = orc.build_sector(6, 0)
     rp, cols, vals = orc.build_csr(hmap)
@@ -130,25 +135,30 @@ def test_split_eigh_matches_dense():
         for k in range(rp[r], rp[r + 1]):
             H[r, cols[k]] += vals[k]
     w = np.linalg.eigvalsh(H)
-    with Sector(cfg, 6, 0, stored=True, split=True) as S:
+    with Sector(cfg, 6, 0, stored=True, real=True, split=True) as S:
         assert S.info.split == 1
-        ev, _, nconv, _ = S.eigh(neigen=6, ncv=23, maxit=300, tol=1e-12, vectors=False)
+        assert S.info.split_far > S.info.split_far_uniform  # (spin flips: L words)
+        ev, _, nconv, _ = S.eigh(neigen=6, ncv=23, maxit=300, tol=1e-12, vectors=False, real=True)
         assert nconv == 6
         np.testing.assert_allclose(ev, w[:6], rtol=1e-10, atol=1e-10)
 
 
 @pytest.mark.parametrize("cplx", [False, True], ids=["real", "complex"])
 def test_n28_split_default(cplx):
-    """Nlevels=28 (7,7): the two-segment form is the default stored H·v; it
-    agrees with the one-pass kernel per element within 1e-13 of the row's
-    absolute sum, every cross-block element is uniform, and the H·v is
-    symmetric to rounding."""
+    """Nlevels=28 (7,7): the two-segment form is the default stored H·v of the
+    real(8) sector on real vectors; it agrees with the one-pass kernel per
+    element within 1e-13 of the row's absolute sum, every cross-block element
+    is uniform, and the H·v is symmetric to rounding.  Complex(8) H: one pass
+    (not built)."""
     from edgpu.hamiltonian import Sector
     from edgpu.params import make_config
 
     cfg = make_config(Norb=1, Nbath=13, bath="random", seed=3)
     g = torch.Generator(device="cuda:0").manual_seed(5)
     with Sector(cfg, 7, 7, stored=True, real=not cplx) as S:
+        if cplx:
+            assert S.info.split == 0
+            return
         assert S.info.split == 1
         assert S.info.split_far_uniform == S.info.split_far > 0
         dt = torch.complex128 if cplx else torch.float64

@@ -34,7 +34,11 @@ ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--options", default="", help="comma-separated ED_OPT_* names")
 ap.add_argument("--split", default="default", choices=["default", "on", "off"],
                 help="two-segment stored form: library default, forced on, or not built")
+ap.add_argument("--lib", default="", help="load this libedgpu.so build instead (A/B of kernel variants)")
 a = ap.parse_args()
+if a.lib:
+    import edgpu._lib as _edl
+    _edl.LIB_PATH = os.path.abspath(a.lib)
 if a.sector == "c4r":   # bench.py's configs[3] parameters (Uloc=(2,2,0), Ust=1, Jh=0.5), (6,6)
     from golden.golden_configs import c4_config
     cfg, q = c4_config("random"), (6, 6)
