@@ -50,7 +50,7 @@ import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 GOLD = os.path.join(ROOT, "tests", "golden")
-PROFILES = [os.path.join(ROOT, "profiles", r) for r in ("r4", "r3")]  # newest summary first
+PROFILES = [os.path.join(ROOT, "profiles", r) for r in ("r5", "r4", "r3")]  # newest summary first
 
 
 def spmv_bytes_real(nnz, dim):
@@ -96,12 +96,24 @@ def spmv_bytes_packed_complex(padded, dim):
     return 4 * padded + 8 * (nslice + 1) + 16 * dim + 32 * dim
 
 
-def measure_hxv(Sector, cfg, q, iters, path=0, warm=5, info=None, cplx=False, batch=False):
+def spmv_bytes_split(inf, dim):
+    """Bytes the two-segment stored H·v (k_spmv_sa + k_spmv_sb) moves: the
+    re-laid matrix (4-B A words, 8-B U entries, 4-B L words, A slice pointers),
+    segment B's work list and slice table, and 48·dim of vectors — A reads the
+    diagonal and v, writes y; B reads y and v, writes Hv (v is read by both
+    passes: every byte of both passes counted)."""
+    return inf["split_bytes"] + inf["split_list_bytes"] + 48 * dim
+
+
+def measure_hxv(Sector, cfg, q, iters, path=0, warm=5, info=None, cplx=False, batch=False, options=()):
     stored = path == 0
-    with Sector(cfg, q[0], q[1], stored=stored, direct=not stored, real=not cplx) as S:
+    with Sector(cfg, q[0], q[1], stored=stored, direct=not stored, real=not cplx, options=options) as S:
         dim, nnz = S.dim, S.nnz
         if info is not None:
-            info.update(packed=int(S.info.packed), padded=int(S.info.padded), npdict=int(S.info.npdict))
+            info.update(packed=int(S.info.packed), padded=int(S.info.padded), npdict=int(S.info.npdict),
+                        split=int(S.info.split) if (stored and not cplx and "stored_exact" not in options) else 0,
+                        split_bytes=int(S.info.split_bytes), split_list_bytes=int(S.info.split_list_bytes),
+                        split_far=int(S.info.split_far), split_far_uniform=int(S.info.split_far_uniform))
         i = torch.arange(1, dim + 1, dtype=torch.float64, device="cuda")
         x = (torch.complex(torch.sin(i), torch.cos(3 * i)) if cplx else torch.sin(i)).contiguous()
         y = torch.empty_like(x)
@@ -384,15 +396,21 @@ def roofline_sweep(Sector, make_config):
             cfg = make_config(bath="random", seed=SEED, **kw)
         inf = {}
         dim, nnz, ms = measure_hxv(Sector, cfg, q, 50, path=0, info=inf)
-        Bown = spmv_bytes_packed(inf["padded"], dim) if inf["packed"] else spmv_bytes_real(nnz, dim)
-        tr, tsrc = _traffic(f"spmv_{tname}_traffic.json")
+        if inf["split"]:
+            Bown = spmv_bytes_split(inf, dim)
+            tr, tsrc = _traffic(f"split_{tname}_traffic.json")
+            kern = "k_spmv_sa + k_spmv_sb<real> (two-segment stored)"
+        else:
+            Bown = spmv_bytes_packed(inf["padded"], dim) if inf["packed"] else spmv_bytes_real(nnz, dim)
+            tr, tsrc = _traffic(f"spmv_{tname}_traffic.json")
+            kern = "k_spmv_pk<real>" if inf["packed"] else "k_spmv<real,real>"
         row = {"dim": dim, "nnz": nnz, "ms_per_launch": round(ms, 4), "bytes_per_launch": Bown,
                "achieved": round(Bown / (ms * 1e-3) / 1e9, 1),
                "frac": round(Bown / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                "csr_equivalent_gbs": round(spmv_bytes_real(nnz, dim) / (ms * 1e-3) / 1e9, 1),
                "traffic": tr, "traffic_source": tsrc,
                "physical_gbs": round(tr / (ms * 1e-3) / 1e9, 1) if tr else None,
-               "kernel": "k_spmv_pk<real>" if inf["packed"] else "k_spmv<real,real>"}
+               "kernel": kern}
         _, _, msk = measure_hxv(Sector, cfg, q, 50, path=2)
         tk, tksrc = _traffic(f"kron_{tname}_traffic.json")
         two = dim >= (1 << 19)   # the library's two-pass threshold
@@ -453,27 +471,53 @@ def bench_roofline(Sector, make_config):
     cfg28 = make_config(Norb=1, Nbath=13, bath="random", seed=SEED)
     inf28 = {}
     dim28, nnz28, ms28 = measure_hxv(Sector, cfg28, (7, 7), 50, path=0, info=inf28)
-    # frac on the bytes the timed kernel moves (its own format: 4-B
-    # {col|value index} words when packed); SURVEY §8(d)'s CSR-equivalent
-    # rate is reported beside it and can exceed the physical rate
+    # frac on the bytes the timed kernels move (their own format: the
+    # two-segment form's A words / U entries, or the one-pass kernel's 4-B
+    # {col|value index} words); SURVEY §8(d)'s CSR-equivalent rate is
+    # reported beside it and can exceed the physical rate
     Bcsr = spmv_bytes_real(nnz28, dim28)
-    Bown = spmv_bytes_packed(inf28["padded"], dim28) if inf28["packed"] else Bcsr
+    split = bool(inf28.get("split"))
+    if split:
+        Bown = spmv_bytes_split(inf28, dim28)
+        tname = "split_n28"
+        kern = ("k_spmv_sa + k_spmv_sb<real> (two-segment stored H·v: diagonal + in-block elements in row "
+                "order -> y, then the cross-block elements — "
+                f"{inf28['split_far_uniform']} of {inf28['split_far']} stored once per 128-row slice — "
+                f"in column-chunk order, added to y; {inf28['npdict']}-value dictionary)")
+        basis = ("bytes the two timed kernels move: split_bytes (4-B A words, 8-B U entries, A slice pointers) + "
+                 "split_list_bytes (segment B's work list, slice table) + 48*dim (A: diagonal, v, y; B: y, v, Hv)")
+    else:
+        Bown = spmv_bytes_packed(inf28["padded"], dim28) if inf28["packed"] else Bcsr
+        tname = "spmv_n28"
+        kern = (("k_spmv_pk<real> (stored SELL-64, 32-bit {col|value index} words, "
+                 f"{inf28['npdict']}-value dictionary)") if inf28["packed"]
+                else "k_spmv<real,real> (stored SELL-64 H·v)")
+        basis = ("bytes the timed kernel moves: 4*padded slots + 8*(nslice+1) + 8*dim "
+                 "(diagonal) + 16*dim (read v, write Hv)") if inf28["packed"] else "12*nnz + 8*(dim+1) + 16*dim"
     ach = Bown / (ms28 * 1e-3) / 1e9
-    traffic, tsrc = _traffic("spmv_n28_traffic.json")
+    traffic, tsrc = _traffic(f"{tname}_traffic.json")
     roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
-            "achieved_basis": ("bytes the timed kernel moves: 4*padded slots + 8*(nslice+1) + 8*dim "
-                               "(diagonal) + 16*dim (read v, write Hv)") if inf28["packed"]
-                              else "12*nnz + 8*(dim+1) + 16*dim",
-            "kernel": ("k_spmv_pk<real> (stored SELL-64, 32-bit {col|value index} words, "
-                       f"{inf28['npdict']}-value dictionary)") if inf28["packed"]
-                      else "k_spmv<real,real> (stored SELL-64 H·v)",
+            "achieved_basis": basis, "kernel": kern,
             "workload": f"Nlevels=28 Norb=1 Nbath=13 (7,7) sector, dim {dim28}, nnz {nnz28}, real(8)",
             "ms_per_launch": round(ms28, 4), "bytes_per_launch": Bown,
             "csr_equivalent_bytes": Bcsr,
             "csr_equivalent_gbs": round(Bcsr / (ms28 * 1e-3) / 1e9, 1),
             "physical_gbs": round(traffic / (ms28 * 1e-3) / 1e9, 1) if traffic else None,
-            "profile": _profile_ms("spmv_n28")}
+            "traffic_over_own": round(traffic / Bown, 3) if traffic else None,
+            "profile": _profile_ms(tname)}
+    if split:
+        # the one-pass kernel in spMatVec_cc's per-row order (ED_OPT_STORED_EXACT,
+        # bit-identical to the oracle) on the same sector, for comparison
+        inf1 = {}
+        _, _, ms1 = measure_hxv(Sector, cfg28, (7, 7), 30, path=0, info=inf1, options=("stored_exact",))
+        B1 = spmv_bytes_packed(inf1["padded"], dim28)
+        t1, t1src = _traffic("spmv_n28_traffic.json")
+        roof["one_pass_exact"] = {"ms_per_launch": round(ms1, 4), "bytes_per_launch": B1,
+                                  "frac": round(B1 / (ms1 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                  "traffic": t1, "traffic_source": t1src,
+                                  "kernel": "k_spmv_pk<real> (one pass, bit-identical to spMatVec_cc)",
+                                  "profile": _profile_ms("spmv_n28")}
     dimk, _, msk = measure_hxv(Sector, cfg28, (7, 7), 50, path=2)
     Bk = 16 * dimk
     tk, tksrc = _traffic("kron_n28_traffic.json")

@@ -127,14 +127,15 @@ struct ed_sector {
   int64_t* d_sptrA = nullptr;
   uint32_t* d_wordsA = nullptr;
   int64_t paddedA = 0;
-  int wA_max = 0;           // widest A slice (k_spmv_pk chunk choice)
-  int64_t split_meta = 0, split_listR = 0, split_listC = 0;  // (ed_sector_info.split_bytes)
+  int wA_max = 0, wA_min = 0;  // widest / narrowest A slice (k_spmv_sa chunk choice)
+  int64_t split_meta = 0, split_listR = 0;  // (ed_sector_info.split_bytes)
+  int split_uch = 8;        // U batch of k_spmv_sb (7 or 8)
   SplitSlice* d_bsl = nullptr;
   int nbsl = 0;
   // k_spmv_sb work lists (half-chunk-major), each cut into 8 per-XCD ranges:
   // real vectors: items of two 64-row halves of pair slices + the generic
   // slices; complex vectors: every half
-  int2 *d_itR = nullptr, *d_itC = nullptr;
+  int2* d_itR = nullptr;
   int* d_glist = nullptr;
   int* d_xoff = nullptr;    // [27]: items R | generic | items C ranges
   int2* d_ul = nullptr;
@@ -447,8 +448,13 @@ static int build_split(ed_sector* s) {
     std::vector<int64_t> hp(ns + 1);
     CK(dcopy(s, hp.data(), s->d_sptrA, (ns + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
     int wm = 0;
-    for (int64_t q = 0; q < ns; q++) wm = std::max(wm, (int)((hp[q + 1] - hp[q]) >> 6));
+    int wn = 1 << 30;
+    for (int64_t q = 0; q < ns; q++) {
+      wm = std::max(wm, (int)((hp[q + 1] - hp[q]) >> 6));
+      wn = std::min(wn, (int)((hp[q + 1] - hp[q]) >> 6));
+    }
     s->wA_max = wm;
+    s->wA_min = wn;
   }
   CK(dalloc_t(s, &s->d_wordsA, std::max<int64_t>(slotsA, 1)));
   hipLaunchKernelGGL(k_split_fill_a, dim3(grid_for(ns * 64)), dim3(kBlock), 0, s->stream, s->d_sptr, s->d_words,
@@ -482,9 +488,15 @@ static int build_split(ed_sector* s) {
   HIPCK(hipGetLastError());
   CK(dcopy(s, sl.data(), s->d_bsl, nsl * sizeof(SplitSlice), hipMemcpyDeviceToHost));
   int64_t uo = 0, lo = 0, nfar_u = 0;
+  int numax = 0;
+  for (const SplitSlice& q : sl) numax = std::max(numax, q.nu);
+  // U batch of segment B: 7 where no slice has more (Nlevels=28 half
+  // filling: every row has 7 down-spin hops; a batch of 8 gathers the pad)
+  const int uch = numax == 7 ? 7 : kSplitChunk;
+  s->split_uch = uch;
   for (SplitSlice& q : sl) {
     nfar_u += (int64_t)q.nu * split_n(q);
-    q.nu = (q.nu + kSplitChunk - 1) / kSplitChunk * kSplitChunk;  // padded with {0, zero value}
+    q.nu = (q.nu + uch - 1) / uch * uch;  // padded with {0, zero value}
     q.wl = (q.wl + kSplitLChunk - 1) / kSplitLChunk * kSplitLChunk;
     q.uoff = uo;
     q.loff = lo;
@@ -494,9 +506,9 @@ static int build_split(ed_sector* s) {
   // Default policy: the two-segment form only where (nearly) every
   // cross-block element is uniform over its slice (normal-mode sectors
   // without Jx/Jp: the down-spin hops).  With per-row L words (spin flips,
-  // Jx/Jp) segment B's gathers outweigh the saved re-gathers: n28j 0.311 vs
-  // 0.283 ms one-pass, nonSU2 N26 0.493 vs 0.380 (profiles/r5).
-  if (!(s->flags & ED_SPLIT_ON) && (double)nfar_u < 0.9 * (double)nfar) {
+  // Jx/Jp) it is slower: N28 with Jx/Jp (95.7 % uniform) 0.308 vs 0.283 ms
+  // one-pass, nonSU2 N26 (39 %) 0.493 vs 0.380 (profiles/r5).
+  if (!(s->flags & ED_SPLIT_ON) && (double)nfar_u < 0.99 * (double)nfar) {
     scratch_free();
     dfree(s, (void**)&s->d_bsl, nsl * sizeof(SplitSlice));
     dfree(s, (void**)&s->d_wordsA, std::max<int64_t>(slotsA, 1) * sizeof(uint32_t));
@@ -513,7 +525,7 @@ static int build_split(ed_sector* s) {
                      s->d_map, nsp, s->d_bsl, nsl, s->d_ul, s->d_lw, zpad);
   HIPCK(hipGetLastError());
   // work lists in half-chunk-major order (k_spmv_sb)
-  std::vector<int2> itR, itC;
+  std::vector<int2> itR;
   std::vector<int> gl;
   int pend = -1;
   for (int64_t c64 = 0; c64 < 2 * nchunk; c64++)
@@ -524,7 +536,6 @@ static int build_split(ed_sector* s) {
       const SplitSlice& q = sl[id];
       if (64 * h >= split_n(q)) continue;
       const int e = 2 * id + h;
-      itC.push_back(make_int2(e, -1));
       if (!(split_flags(q) & kSplitPair)) {
         if (h == 0) gl.push_back(id);
         continue;
@@ -545,17 +556,14 @@ static int build_split(ed_sector* s) {
   for (int x = 0; x <= 8; x++) {
     xo[x] = (int)((int64_t)itR.size() * x / 8);
     xo[9 + x] = (int)((int64_t)gl.size() * x / 8);
-    xo[18 + x] = (int)((int64_t)itC.size() * x / 8);
   }
   if (itR.empty()) itR.push_back(make_int2(0, -1));
   if (gl.empty()) gl.push_back(0);
   CK(upload(s, &s->d_itR, itR));
-  CK(upload(s, &s->d_itC, itC));
   // bytes one launch reads besides the U / L entries: segment A's slice
   // pointers and the work list of the real (or complex) form
   s->split_meta = (ns + 1) * 8;
   s->split_listR = (int64_t)itR.size() * 8 + (int64_t)gl.size() * 4 + nsl * (int64_t)sizeof(SplitSlice);
-  s->split_listC = (int64_t)itC.size() * 8 + nsl * (int64_t)sizeof(SplitSlice);
   CK(upload(s, &s->d_glist, gl));
   CK(upload(s, &s->d_xoff, xo));
   scratch_free();
@@ -1364,44 +1372,48 @@ template <bool HC, bool VC, class Epi>
 static int launch_split(ed_sector* s, const void* x, Epi epi, hipStream_t st) {
   using V = val_t<VC>;
   using H = val_t<HC>;
-  V* y = (V*)epi.scratch();
-  EpiStore<VC> ea{y};
-  const int64_t dim = s->dim, ns = s->nslice;
-  // XCD row ranges (k_spmv_pk's remap) on grids of >= 1,024 blocks, as xcd_on()
-  const int g0 = grid_for(ns * 64);
-  const int xa = g0 >= 1024 ? 1 : 0;
-  const int ga = xa ? (g0 & ~7) : g0;
-  const bool nta = (s->paddedA * 4 + dim * (int64_t)sizeof(H)) > kSplitMinBytes;
-  // rows of <= 8 in-block elements (every Norb=1 sector up to Nbath 15):
-  // chunks of 8 slots, not 16 (fewer padding gathers); two slices per wave
-  (void)ea;
-  (void)ga;
-  (void)xa;
+  if constexpr (HC || VC) {
+    // (split_on(): real H on real vectors only; the complex forms are not instantiated)
+    return fail(ED_ERR_STATE, "two-segment stored H·v serves real H on real vectors");
+  } else {
+    V* y = (V*)epi.scratch();
+    const int64_t dim = s->dim, ns = s->nslice;
+    const bool nta = (s->paddedA * 4 + dim * (int64_t)sizeof(H)) > kSplitMinBytes;
+    // A: rows of exactly 7 in-block elements (Norb=1, Nbath=13 half filling)
+    // take 7-slot chunks, rows of <= 8 chunks of 8 slots (fewer padding
+    // gathers than 16); two slices per wave
 #define ED_SPA(NTV, CH)                                                                                       \
   hipLaunchKernelGGL((k_spmv_sa<HC, VC, NTV, CH, ED_SA_R>),                                                    \
                      dim3(resident_grid((const void*)k_spmv_sa<HC, VC, NTV, CH, ED_SA_R>, kBlock)), dim3(kBlock), 0, st, \
                      (const H*)s->d_diag, s->d_sptrA, s->d_wordsA, (const H*)s->d_pdict, (const V*)x, y, dim, ns)
-  if (s->wA_max <= 8) {
-    if (nta) ED_SPA(1, 8);
-    else ED_SPA(0, 8);
-  } else {
-    if (nta) ED_SPA(1, kChunk);
-    else ED_SPA(0, kChunk);
-  }
+    if (s->wA_max == 7 && s->wA_min == 7) {
+      if (nta) ED_SPA(1, 7);
+      else ED_SPA(0, 7);
+    } else if (s->wA_max <= 8) {
+      if (nta) ED_SPA(1, 8);
+      else ED_SPA(0, 8);
+    } else {
+      if (nta) ED_SPA(1, kChunk);
+      else ED_SPA(0, kChunk);
+    }
 #undef ED_SPA
-  HIPCK(hipGetLastError());
-  if (s->nlw * 4 > kSplitMinBytes)
-    hipLaunchKernelGGL((k_spmv_sb<HC, VC, 1, Epi>), dim3(kSplitGrid),
-                       dim3(kBlock), 0, st, s->d_bsl, VC ? s->d_itC : s->d_itR, s->d_xoff + (VC ? 18 : 0),
-                       s->d_glist, s->d_xoff + 9, s->d_ul, s->d_lw, (const H*)s->d_pdict, (const V*)x,
-                       (const V*)y, epi);
-  else
-    hipLaunchKernelGGL((k_spmv_sb<HC, VC, 0, Epi>), dim3(kSplitGrid),
-                       dim3(kBlock), 0, st, s->d_bsl, VC ? s->d_itC : s->d_itR, s->d_xoff + (VC ? 18 : 0),
-                       s->d_glist, s->d_xoff + 9, s->d_ul, s->d_lw, (const H*)s->d_pdict, (const V*)x,
-                       (const V*)y, epi);
-  HIPCK(hipGetLastError());
-  return ED_OK;
+    HIPCK(hipGetLastError());
+#define ED_SPB(NTV, U)                                                                                        \
+  hipLaunchKernelGGL((k_spmv_sb<HC, VC, NTV, Epi, U>), dim3(kSplitGrid), dim3(kBlock), 0, st, s->d_bsl, s->d_itR, \
+                     s->d_xoff, s->d_glist, s->d_xoff + 9, s->d_ul, s->d_lw, (const H*)s->d_pdict, (const V*)x,   \
+                     (const V*)y, epi)
+    const bool ntb = s->nlw * 4 > kSplitMinBytes;
+    if (s->split_uch == 7) {
+      if (ntb) ED_SPB(1, 7);
+      else ED_SPB(0, 7);
+    } else {
+      if (ntb) ED_SPB(1, kSplitChunk);
+      else ED_SPB(0, kSplitChunk);
+    }
+#undef ED_SPB
+    HIPCK(hipGetLastError());
+    return ED_OK;
+  }
 }
 
 template <bool HC, bool VC, class Epi>
@@ -3082,7 +3094,6 @@ int ed_sector_get_info(const ed_sector* s, ed_sector_info* info) {
   info->split_far_uniform = s->nfar_u;
   info->split_bytes = s->split ? (s->paddedA + s->nlw) * 4 + s->nul * 8 + s->split_meta : 0;
   info->split_list_bytes = s->split ? s->split_listR : 0;
-  info->split_list_bytes_c = s->split ? s->split_listC : 0;
   return ED_OK;
 }
 

@@ -327,7 +327,7 @@ typedef unsigned int sb_u2 __attribute__((ext_vector_type(2)));
 
 // one 128-row slice in the generic form: the lane's two rows apart (8-byte
 // gathers), for slices without the pair property
-template <bool HC, bool VC, int NT, class Epi>
+template <bool HC, bool VC, int NT, int UCH, class Epi>
 __device__ __forceinline__ double sb_generic(const SplitSlice& S, int lane, const int2* __restrict__ ul,
                                              const uint32_t* __restrict__ lw, const val_t<HC>* sdict,
                                              const val_t<VC>* __restrict__ x, const val_t<VC>* y, Epi& epi) {
@@ -340,19 +340,19 @@ __device__ __forceinline__ double sb_generic(const SplitSlice& S, int lane, cons
   const int2* up = ul + S.uoff;
   const uint32_t* wp = lw + S.loff + 2 * lane;
   V a0 = y[i0], a1 = y[i1];
-  for (int k0 = 0; k0 < S.nu; k0 += kSplitChunk) {
-    int2 e[kSplitChunk];
-    V g0[kSplitChunk], g1[kSplitChunk];
+  for (int k0 = 0; k0 < S.nu; k0 += UCH) {
+    int2 e[UCH];
+    V g0[UCH], g1[UCH];
 #pragma unroll
-    for (int k = 0; k < kSplitChunk; k++) e[k] = up[k0 + k];  // padded list: whole chunks
+    for (int k = 0; k < UCH; k++) e[k] = up[k0 + k];  // padded list: whole chunks
 #pragma unroll
-    for (int k = 0; k < kSplitChunk; k++) {
+    for (int k = 0; k < UCH; k++) {
       g0[k] = x[i0 + e[k].x];
       g1[k] = x[i1 + e[k].x];
     }
     asm volatile("" ::: "memory");  // all gathers in flight before the first use
 #pragma unroll
-    for (int k = 0; k < kSplitChunk; k++) {
+    for (int k = 0; k < UCH; k++) {
       const H h = sdict[e[k].y];
       a0 = add(a0, mul(h, g0[k]));
       a1 = add(a1, mul(h, g1[k]));
@@ -394,7 +394,9 @@ __device__ __forceinline__ double sb_generic(const SplitSlice& S, int lane, cons
 //     generic list, one 128-row slice per wavefront;
 //   complex vectors: one half per wavefront, one row (16 B) per lane.
 // Returns nothing; the epilogue's partials via epi.finish.
-template <bool HC, bool VC, int NT, class Epi>
+// UCH: U entries per load batch (the U lists are padded to a multiple of it:
+// the sector's largest U count when that is 7, else kSplitChunk)
+template <bool HC, bool VC, int NT, class Epi, int UCH = kSplitChunk>
 __global__ void __launch_bounds__(kBlock) k_spmv_sb(const SplitSlice* __restrict__ sl, const int2* __restrict__ items,
                                                     const int* __restrict__ xoffI, const int* __restrict__ glist,
                                                     const int* __restrict__ xoffG, const int2* __restrict__ ul,
@@ -428,24 +430,24 @@ __global__ void __launch_bounds__(kBlock) k_spmv_sb(const SplitSlice* __restrict
       const bool on = r < n && (grp == 0 || hasB);
       const int i0 = row0 + (r < n ? r : 64 * half);  // idle lanes: the half's first pair
       sb_d2 acc = *(const sb_d2*)(y + i0);
-      for (int k0 = 0; k0 < nu; k0 += kSplitChunk) {
-        int2 ea[kSplitChunk], eb[kSplitChunk];
+      for (int k0 = 0; k0 < nu; k0 += UCH) {
+        int2 ea[UCH], eb[UCH];
 #pragma unroll
-        for (int k = 0; k < kSplitChunk; k++) {
+        for (int k = 0; k < UCH; k++) {
           ea[k] = ul[SA.uoff + k0 + k];
           eb[k] = ul[SB.uoff + k0 + k];
         }
-        sb_d2 g[kSplitChunk];
-        int ix[kSplitChunk];
+        sb_d2 g[UCH];
+        int ix[UCH];
 #pragma unroll
-        for (int k = 0; k < kSplitChunk; k++) {
+        for (int k = 0; k < UCH; k++) {
           const int d = grp ? eb[k].x : ea[k].x;
           ix[k] = grp ? eb[k].y : ea[k].y;
           g[k] = *(const sb_d2*)(x + i0 + d);
         }
         asm volatile("" ::: "memory");  // all gathers in flight before the first use
 #pragma unroll
-        for (int k = 0; k < kSplitChunk; k++) {
+        for (int k = 0; k < UCH; k++) {
           const H h = sdict[ix[k]];
           acc.x = add(acc.x, mul(h, g[k].x));
           acc.y = add(acc.y, mul(h, g[k].y));
@@ -480,7 +482,7 @@ __global__ void __launch_bounds__(kBlock) k_spmv_sb(const SplitSlice* __restrict
     }
     // ---- generic slices (no pair property): one 128-row slice per wavefront
     for (int q = xoffG[xcd] + w0; q < xoffG[xcd + 1]; q += nwx)
-      part += sb_generic<HC, VC, NT>(sl[glist[q]], lane, ul, lw, sdict, x, y, epi);
+      part += sb_generic<HC, VC, NT, UCH>(sl[glist[q]], lane, ul, lw, sdict, x, y, epi);
   } else {
     // ---- complex vectors: one 64-row half per wavefront, one row per lane
     for (int q = xoffI[xcd] + w0; q < xoffI[xcd + 1]; q += nwx) {
@@ -491,16 +493,16 @@ __global__ void __launch_bounds__(kBlock) k_spmv_sb(const SplitSlice* __restrict
       const bool on = r < split_n(S);
       const int i0 = S.row0 + (on ? r : 64 * half);
       V acc = y[i0];
-      for (int k0 = 0; k0 < S.nu; k0 += kSplitChunk) {
-        int2 ek[kSplitChunk];
-        V g[kSplitChunk];
+      for (int k0 = 0; k0 < S.nu; k0 += UCH) {
+        int2 ek[UCH];
+        V g[UCH];
 #pragma unroll
-        for (int k = 0; k < kSplitChunk; k++) ek[k] = ul[S.uoff + k0 + k];
+        for (int k = 0; k < UCH; k++) ek[k] = ul[S.uoff + k0 + k];
 #pragma unroll
-        for (int k = 0; k < kSplitChunk; k++) g[k] = x[i0 + ek[k].x];
+        for (int k = 0; k < UCH; k++) g[k] = x[i0 + ek[k].x];
         asm volatile("" ::: "memory");
 #pragma unroll
-        for (int k = 0; k < kSplitChunk; k++) acc = add(acc, mul(sdict[ek[k].y], g[k]));
+        for (int k = 0; k < UCH; k++) acc = add(acc, mul(sdict[ek[k].y], g[k]));
       }
       const uint32_t* wp = lw + S.loff + (i0 - S.row0);
       for (int k0 = 0; k0 < S.wl; k0 += kSplitLChunk) {

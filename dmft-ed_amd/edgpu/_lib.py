@@ -81,7 +81,7 @@ class SectorInfo(ctypes.Structure):
                 ("dimup", _i64), ("dimdw", _i64), ("device_bytes", _i64),
                 ("packed", _i32), ("npdict", _i32), ("row0", _i64), ("nrows", _i64),
                 ("split", _i32), ("pad_", _i32), ("split_far", _i64), ("split_far_uniform", _i64),
-                ("split_bytes", _i64), ("split_list_bytes", _i64), ("split_list_bytes_c", _i64)]
+                ("split_bytes", _i64), ("split_list_bytes", _i64)]
 
 
 class EDGPUError(RuntimeError):

@@ -156,8 +156,7 @@ typedef struct ed_sector_info {
   int64_t split_far_uniform;  /* of which stored once per 64-row slice (U)   */
   int64_t split_bytes;        /* bytes one two-segment launch reads of the re-laid matrix:
                                  4 * (A words + L words) + 8 * U entries + A slice pointers */
-  int64_t split_list_bytes;   /* + segment B's work list, real vectors         */
-  int64_t split_list_bytes_c; /* + segment B's work list, complex vectors      */
+  int64_t split_list_bytes;   /* + segment B's work list and slice table       */
 } ed_sector_info;
 
 typedef struct ed_sector ed_sector; /* opaque */

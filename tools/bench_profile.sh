@@ -9,7 +9,7 @@
 #    profiles/TAG): bench_kernel_stats.csv, bench_trace_{spmv,spmv_cplx,kron,direct}.json
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-TAG=${1:-r4}; shift
+TAG=${1:-r5}; shift
 OUT=$R/gpurun_out/bprof_$TAG
 P=$OUT/profiles
 mkdir -p "$OUT" "$P"
@@ -23,8 +23,8 @@ s=$(find "$OUT/st" -name "*kernel_stats.csv" | head -1)
 # (persist: the headline configs[1] launches — one 512-thread workgroup,
 # grid 512 — apart from the batched ones of the same instantiation, whose
 # grids are K x 512: the runs split them)
-for e in "spmv|k_spmv_pk<false, false" "spmv_cplx|k_spmv_pk<true, true" "kron|k_kron_(up|dw)" "direct|k_direct<" \
-         "persist|k_lanc_persist<"; do
+for e in "split|k_spmv_s[ab]<false, false" "spmv|k_spmv_pk<false, false" "spmv_cplx|k_spmv_pk<true, true" \
+         "kron|k_kron_(up|dw)" "direct|k_direct<" "persist|k_lanc_persist<"; do
   IFS='|' read -r name pat <<< "$e"
   python3 "$R/tools/trace_summary.py" "$t" "$pat" 5 "$P/bench_trace_$name.json" \
     --note "rocprofv3 of bench.py $*: per (kernel, grid) group, 5 warm-up launches dropped" \

@@ -16,9 +16,9 @@ mkdir -p "$OUT" "$PROF"
 ENTRIES=(
   "spmv_n28|--sector n28 --path 0 --split off|k_spmv_pk<false"
   "split_n28|--sector n28 --path 0 --split on|k_spmv_s[ab]<false"
-  "split_cplx_n28|--sector n28 --path 0 --complex --split on|k_spmv_s[ab]<true"
   "split_n28j|--sector n28j --path 0 --split on|k_spmv_s[ab]<false"
   "split_n26s|--sector n26s --path 0 --split on|k_spmv_s[ab]<false"
+  "split_n28b|--sector n28b --path 0 --split on|k_spmv_s[ab]<false"
   "spmv_cplx_n28|--sector n28 --path 0 --complex --split off|k_spmv_pk<true"
   "kron_n28|--sector n28 --path 2|k_kron"
   "direct_n28|--sector n28 --path 1|k_direct"
