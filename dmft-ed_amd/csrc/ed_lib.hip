@@ -1392,6 +1392,9 @@ static int launch_split(ed_sector* s, const void* x, Epi epi, hipStream_t st) {
     } else if (s->wA_max <= 8) {
       if (nta) ED_SPA(1, 8);
       else ED_SPA(0, 8);
+    } else if (s->wA_max <= 12) {  // (Norb=2: up to 12 in-block elements per row)
+      if (nta) ED_SPA(1, 12);
+      else ED_SPA(0, 12);
     } else {
       if (nta) ED_SPA(1, kChunk);
       else ED_SPA(0, kChunk);
