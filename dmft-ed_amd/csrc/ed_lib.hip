@@ -96,6 +96,7 @@ struct LancWS {
 
 struct ed_sector {
   int device = 0;
+  std::mutex build_mu;  // lazy table builds (ensure_direct)
   hipStream_t stream = nullptr;  // private stream for synchronous entry points
   EdModel Mh;
   EdModel* Md = nullptr;
@@ -928,8 +929,17 @@ static int build_direct(ed_sector* s) {
 
 // the k_direct tables on first use of path 1 (build_direct), ordered before
 // the caller's stream by a sync of the sector's stream
-static int ensure_direct(ed_sector* s, int path) {
-  if (path != 1 || s->d_dchunk || s->nrows == 0) return ED_OK;
+static int ensure_direct(ed_sector* s, int path, hipStream_t caller = nullptr) {
+  if (path != 1 || s->nrows == 0) return ED_OK;
+  // one builder per sector (two threads' first path-1 H·v would race on the
+  // tables); a stream being graph-captured cannot take the build's syncs
+  std::lock_guard<std::mutex> lk(s->build_mu);
+  if (s->d_dchunk) return ED_OK;
+  if (caller) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(caller, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+      return fail(ED_ERR_STATE, "first generic matrix-free H·v inside a graph capture: run one outside first");
+  }
   if (!(s->flags & ED_DIRECT)) return fail(ED_ERR_ARG, "generic matrix-free path needs ED_DIRECT");
   CK(build_direct(s));
   HIPCK(hipStreamSynchronize(s->stream));
@@ -3107,7 +3117,7 @@ int ed_sector_hxv_dev_path(ed_sector* s, int32_t path, int32_t vtype, const void
   int pth = resolve_path(s, path);
   if (pth < 0) return fail(ED_ERR_ARG, "H·v path not available for this sector");
   HIPCK(hipSetDevice(s->device));
-  CK(ensure_direct(s, pth));
+  CK(ensure_direct(s, pth, (hipStream_t)stream));
   hipStream_t st = (hipStream_t)stream;
   if (vtype == 1) {
     EpiStore<true> e{(double2*)hv};

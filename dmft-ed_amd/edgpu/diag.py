@@ -223,11 +223,19 @@ def solve_many(cfg: EDConfig, secs: List[SectorId], opt: DiagOptions, device: in
 
     take_global: the farm's multi-rank work queue — a callable returning the
     next index into `secs` (already in schedule order) or None; the result
-    list then holds the sectors this process solved, None elsewhere."""
+    list then holds the sectors this process solved, None elsewhere.  The
+    cache budget applies to the single-rank and LPT schedules only: a worker
+    on the global queue takes the next index unconditionally (a warning says
+    so when a budget is set)."""
     solver = solver or solve_sector
     import threading
 
     if take_global is not None:
+        if opt.cache_budget_mb > 0:
+            import warnings
+
+            warnings.warn("DiagOptions.cache_budget_mb is not applied on the multi-rank dynamic queue "
+                          "(farm_schedule='lpt' applies it per rank)", RuntimeWarning, stacklevel=2)
         out_g: List[Optional[SectorResult]] = [None] * len(secs)
         errs: List[BaseException] = []
 
