@@ -101,3 +101,4 @@ def test_eigh_step_variants(opts, real):
     assert 2 * NCV < H.shape[0] <= 2048
     with Sector(cfg, 3, 4, stored=True, real=True, options=opts) as S:
         _check(S, H, True, vt_real=real)
+

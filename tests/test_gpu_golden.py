@@ -71,3 +71,34 @@ def test_c5_gf_matches_fixture(bath):
     print(f"c5 {bath}: G(iw) max relative deviation {rel:.2e}")
     assert rel < 1e-10
     assert np.max(np.abs(ref[0, 1, 0, 0])) > 1e-8 * np.max(np.abs(ref))   # spin-mixed part present
+
+
+def test_c4_flat_probe_recovers_missed_copies():
+    """The degeneracy probe on the sectors where it matters: with the flat
+    bath, a single-vector Krylov solve (ED_OPT_EIGH_NO_VERIFY: no probe)
+    misses degenerate copies in some configs[3] sectors — it returns a
+    spectrum that differs from the dense fixture there — and the default
+    solve (screen with the residual-interval exit, then the thick-restart
+    probe on the flagged complement) matches the fixture on every one of
+    those sectors."""
+    from edgpu.diag import DiagOptions
+    from edgpu.farm import farm_diag
+    from golden.golden_configs import c4_config
+
+    gold = _load("c4_diag_flat.json")
+    cfg = c4_config("flat")
+    nov = farm_diag(cfg, DiagOptions(kernel_options=("eigh_no_verify",)))
+    dflt = farm_diag(cfg, DiagOptions())
+    scale = abs(gold["E0"])
+    missed = []
+    for k, g in gold["sectors"].items():
+        ref = np.asarray(g["eigenvalues"])
+        a = np.asarray(nov.eigenvalues[int(k)])[: len(ref)]
+        if np.max(np.abs(a - ref)) / scale > 1e-10:
+            missed.append(int(k))
+    assert missed, "no sector with a missed degenerate copy: the probe is untested here"
+    for k in missed:
+        ref = np.asarray(gold["sectors"][str(k)]["eigenvalues"])
+        b = np.asarray(dflt.eigenvalues[k])[: len(ref)]
+        assert np.max(np.abs(b - ref)) / scale < 1e-10, k
+    print(f"c4 flat: {len(missed)} sectors with missed copies without the probe, all recovered")
