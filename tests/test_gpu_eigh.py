@@ -86,14 +86,21 @@ def test_eigh_large_sector_vs_plain_lanczos():
             assert r < 1e-8 * max(1.0, abs(w[k]))
 
 
-@pytest.mark.parametrize("opts", [("trlan_nolocal",), ("trlan_nosolo",), ("trlan_nolocal", "trlan_nosolo")],
-                         ids=["nolocal", "nosolo", "plain"])
+@pytest.mark.parametrize("opts", [("trlan_nolocal",), ("trlan_nosolo",), ("trlan_nolocal", "trlan_nosolo"),
+                                  ("trlan_nosolo", "trlan_fullupd"), ("trlan_nosolo", "trlan_nofold"),
+                                  ("trlan_nosolo", "trlan_unfused"), ("no_graph",)],
+                         ids=["nolocal", "nosolo", "plain", "fullupd", "nofold", "unfused", "no_graph"])
 @pytest.mark.parametrize("real", [True, False], ids=["real", "complex"])
 def test_eigh_step_variants(opts, real):
     """The thick-restart step's alternatives against dense diagonalisation:
     without the shifted three-term H·v epilogue (ED_OPT_TRLAN_NOLOCAL), with
     the multi-kernel CGS on a small sector instead of the one-workgroup
-    orthogonalisation (ED_OPT_TRLAN_NOSOLO), and both (the round-2 step)."""
+    orthogonalisation (ED_OPT_TRLAN_NOSOLO), and both (the round-2 step);
+    on the multi-kernel path also the full update every step
+    (ED_OPT_TRLAN_FULLUPD), the separate coefficient kernels
+    (ED_OPT_TRLAN_NOFOLD) and the four-sweep CGS2 (ED_OPT_TRLAN_UNFUSED);
+    and the sweeps launched without graphs (ED_OPT_NO_GRAPH): every accepted
+    option bit of the eigensolver runs once against the oracle."""
     from edgpu.params import make_config
 
     cfg = make_config(Norb=1, Nbath=6, bath="random", seed=5)
