@@ -98,6 +98,7 @@ struct ed_sector {
   int device = 0;
   std::mutex build_mu;  // lazy table builds (ensure_direct)
   hipStream_t stream = nullptr;  // private stream for synchronous entry points
+  bool own_stream = true;        // false: the caller's stream (ed_sector_create's argument)
   EdModel Mh;
   EdModel* Md = nullptr;
   SectorTables T;
@@ -260,7 +261,7 @@ static void sector_free(ed_sector* s) {
   if (s->stream) {
     for (void* p : s->allocs) (void)hipFreeAsync(p, s->stream);
     (void)hipStreamSynchronize(s->stream);
-    (void)hipStreamDestroy(s->stream);
+    if (s->own_stream) (void)hipStreamDestroy(s->stream);
   }
   pinned_put(s->ws.h_ab);  // after the stream sync above: no copy into it is in flight
   delete s;
@@ -2948,7 +2949,7 @@ static bool jz_conserved(const EdModel& M, const SectorTables& T) {
 }
 
 static int sector_create(const ed_params* p, int32_t q1, int32_t q2, int32_t flags, int64_t row0,
-                         int64_t nrows, int32_t device, ed_sector** out) {
+                         int64_t nrows, int32_t device, hipStream_t stream, ed_sector** out) {
   if (!out) return fail(ED_ERR_ARG, "out == NULL");
   *out = nullptr;
   if (!(flags & (ED_STORED | ED_DIRECT))) return fail(ED_ERR_ARG, "flags need ED_STORED or ED_DIRECT");
@@ -3005,7 +3006,15 @@ static int sector_create(const ed_params* p, int32_t q1, int32_t q2, int32_t fla
       return r2_;         \
     }                     \
   } while (0)
-  hipError_t he = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+  // a caller's stream (a farm worker's, reused for every sector it solves)
+  // or a private non-blocking one
+  hipError_t he = hipSuccess;
+  if (stream) {
+    s->stream = stream;
+    s->own_stream = false;
+  } else {
+    he = hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking);
+  }
   if (he != hipSuccess) {
     delete s;
     return fail(ED_ERR_HIP, "hipStreamCreate");
@@ -3054,14 +3063,12 @@ static int sector_create(const ed_params* p, int32_t q1, int32_t q2, int32_t fla
 
 int ed_sector_create(const ed_params* p, int32_t q1, int32_t q2, int32_t flags, int32_t device,
                      void* stream, ed_sector** out) {
-  (void)stream;
-  return sector_create(p, q1, q2, flags, 0, -1, device, out);
+  return sector_create(p, q1, q2, flags, 0, -1, device, (hipStream_t)stream, out);
 }
 
 int ed_sector_create_rows(const ed_params* p, int32_t q1, int32_t q2, int32_t flags, int64_t row0,
                           int64_t nrows, int32_t device, void* stream, ed_sector** out) {
-  (void)stream;
-  return sector_create(p, q1, q2, flags, row0, nrows, device, out);
+  return sector_create(p, q1, q2, flags, row0, nrows, device, (hipStream_t)stream, out);
 }
 
 int ed_sector_destroy(ed_sector* s) {

@@ -54,6 +54,9 @@ class DiagOptions:
     # sectors solved concurrently on one GPU (host threads, one HIP stream per
     # sector; ctypes releases the GIL): small sectors are launch-latency bound
     workers: int = 8
+    # each worker thread keeps one HIP stream for every sector it solves
+    # (False: every sector creates and destroys a private stream)
+    worker_streams: bool = True
     # ED_OPT_* kernel alternatives (Sector.set_options names) for every sector
     # of the diagonalisation (A/B runs; the defaults are the measured best)
     kernel_options: Tuple[str, ...] = ()
@@ -130,15 +133,39 @@ def _start_vector(dim: int, cplx: bool) -> np.ndarray:
     return (np.sin(i) + 1j * np.cos(3.0 * i)) if cplx else np.sin(i)
 
 
+_tls = None
+
+
+def _worker_stream(opt: DiagOptions, device: int):
+    """The calling thread's own stream on `device` (DiagOptions.worker_streams),
+    created on first use and reused for every sector the thread solves."""
+    global _tls
+    import torch
+
+    if not opt.worker_streams or not torch.cuda.is_available():
+        return None
+    if _tls is None:
+        import threading
+
+        _tls = threading.local()
+    d = getattr(_tls, "streams", None)
+    if d is None:
+        d = _tls.streams = {}
+    if device not in d:
+        d[device] = torch.cuda.Stream(device=device)
+    return d[device]
+
+
 def solve_sector(cfg: EDConfig, sec: SectorId, opt: DiagOptions, device: int = 0) -> SectorResult:
     dim = sec.dim
+    st = _worker_stream(opt, device)
     neigen, nitermax, nblock = lanczos_params(dim, opt)
     lanc_solve = not (neigen == dim or dim <= max(opt.lanc_dim_threshold, opt.mpi_size))
     real = cfg.is_real()
     q = (sec.q1, sec.q2)
     if not lanc_solve:
         with Sector(cfg, sec.q1, sec.q2, stored=True, real=real, device=device,
-                    options=opt.kernel_options) as S:
+                    options=opt.kernel_options, stream=st) as S:
             rp, cols, vals = S.dump_csr()
         H = np.zeros((dim, dim), dtype=np.complex128)
         rows = np.repeat(np.arange(dim), np.diff(rp))
@@ -149,7 +176,7 @@ def solve_sector(cfg: EDConfig, sec: SectorId, opt: DiagOptions, device: int = 0
         vec = v[:, :neigen] if opt.keep_vectors else None
         return SectorResult(sec.isector, q, dim, w, neigen, vec, "dense")
     with Sector(cfg, sec.q1, sec.q2, stored=True, real=real, device=device,
-                options=opt.kernel_options) as S:
+                options=opt.kernel_options, stream=st) as S:
         if opt.lanc_method == "lanczos":
             e0, vec, _ = S.lanc_eigh(nitermax=nitermax, threshold=opt.lanc_tolerance,
                                      v0=_start_vector(dim, not real), vector=opt.keep_vectors,

@@ -50,14 +50,17 @@ class Sector:
     def __init__(self, cfg: EDConfig, q1: int, q2: int = 0, *, stored: bool = True,
                  direct: bool = False, real: bool = False, device: int = 0, rows=None,
                  pack: bool = True, kron2: Optional[bool] = None, split: Optional[bool] = None,
-                 options=()):
+                 options=(), stream=None):
         """rows=(row0, nrows): hold only those rows of H (ed_sector_create_rows,
         the reference's MPI row split); H·v then maps a whole-sector vector to
         the nrows local entries.  pack=False keeps the plain SELL arrays only;
         kron2 forces the two-pass Kronecker tables on (True) or off (False);
         split forces the two-segment stored form on (True, any size) or off
         (False; default: built for stored matrices beyond the Infinity Cache);
-        options: names of ED_OPT_* kernel alternatives (see set_options)."""
+        options: names of ED_OPT_* kernel alternatives (see set_options);
+        stream: a torch.cuda.Stream (or raw hipStream_t) the sector runs its
+        build and synchronous entry points on, kept by the caller and alive
+        longer than the sector (default: a private stream per sector)."""
         lib = _lib.load()
         self.cfg = cfg
         self._params = cfg.to_ctypes()
@@ -69,11 +72,11 @@ class Sector:
             flags |= _lib.ED_SPLIT_ON if split else _lib.ED_NO_SPLIT
         h = ctypes.c_void_p()
         if rows is None:
-            check(lib.ed_sector_create(ctypes.byref(self._params), q1, q2, flags, device, None,
-                                       ctypes.byref(h)), "ed_sector_create")
+            check(lib.ed_sector_create(ctypes.byref(self._params), q1, q2, flags, device,
+                                       _stream_ptr(stream), ctypes.byref(h)), "ed_sector_create")
         else:
             check(lib.ed_sector_create_rows(ctypes.byref(self._params), q1, q2, flags, int(rows[0]),
-                                            int(rows[1]), device, None, ctypes.byref(h)),
+                                            int(rows[1]), device, _stream_ptr(stream), ctypes.byref(h)),
                   "ed_sector_create_rows")
         self._h = h
         self.device = device

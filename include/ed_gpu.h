@@ -163,7 +163,13 @@ typedef struct ed_sector ed_sector; /* opaque */
 
 /* ------------------------------------------------------------ handle API */
 /* Build the sector basis and (ED_STORED) the Hamiltonian on `device`.
- * q1,q2: (nup,ndw) for normal, (sz,-) for superc, (n,-) for nonsu2. */
+ * q1,q2: (nup,ndw) for normal, (sz,-) for superc, (n,-) for nonsu2.
+ * stream: NULL — the sector creates (and destroys) a private non-blocking
+ * stream for its build and its synchronous entry points (eigh, lanczos, ...);
+ * non-NULL — that stream is used instead and stays the caller's (it must
+ * outlive the sector; a farm worker passes its own stream to every sector it
+ * solves).  Do not pass the legacy default stream: it serialises with every
+ * other stream of the device. */
 int ed_sector_create(const ed_params* p, int32_t q1, int32_t q2, int32_t flags,
                      int32_t device, void* stream, ed_sector** out);
 /* The reference's MPI row split of one sector (build_Hv_sector with

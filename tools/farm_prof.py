@@ -30,6 +30,8 @@ ap.add_argument("--workers", type=int, default=8)
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--serial-stats", default="")
 ap.add_argument("--options", default="", help="comma-separated ED_OPT_* names for every sector")
+ap.add_argument("--private-streams", action="store_true",
+                help="DiagOptions.worker_streams=False: a private stream per sector (A/B)")
 ap.add_argument("--budget", type=float, default=None, help="DiagOptions.cache_budget_mb (default: the library default)")
 ap.add_argument("--timeline", default="", help="write per-sector (start, end, thread, dim) of the last rep")
 ap.add_argument("--maps", default="", help="write the process's shared-object mappings (for symbolising a crash)")
@@ -63,7 +65,7 @@ if a.serial_stats:
         json.dump(dict(config="configs[3] random bath, Lanczos sectors, one thread", options=list(opts),
                        totals=tot, sectors=rows), f, indent=1)
 
-opt = DiagOptions(workers=a.workers, kernel_options=opts)
+opt = DiagOptions(workers=a.workers, kernel_options=opts, worker_streams=not a.private_streams)
 if a.budget is not None:
     opt.cache_budget_mb = a.budget
 if a.maps:
