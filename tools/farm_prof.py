@@ -30,13 +30,14 @@ ap.add_argument("--workers", type=int, default=8)
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--serial-stats", default="")
 ap.add_argument("--options", default="", help="comma-separated ED_OPT_* names for every sector")
+ap.add_argument("--bath", default="random", help="configs[3] bath: random | flat")
 ap.add_argument("--private-streams", action="store_true",
                 help="DiagOptions.worker_streams=False: a private stream per sector (A/B)")
 ap.add_argument("--budget", type=float, default=None, help="DiagOptions.cache_budget_mb (default: the library default)")
 ap.add_argument("--timeline", default="", help="write per-sector (start, end, thread, dim) of the last rep")
 ap.add_argument("--maps", default="", help="write the process's shared-object mappings (for symbolising a crash)")
 a = ap.parse_args()
-cfg = c4_config("random")
+cfg = c4_config(a.bath)
 opts = tuple(x for x in a.options.split(",") if x)
 
 if a.serial_stats:
