@@ -109,3 +109,26 @@ def test_eigh_step_variants(opts, real):
     with Sector(cfg, 3, 4, stored=True, real=True, options=opts) as S:
         _check(S, H, True, vt_real=real)
 
+
+
+def test_eigh_on_caller_stream():
+    """ed_sector_create with a caller's stream (the farm's worker streams):
+    two sectors solved one after the other on the same torch stream give the
+    exact eigenvalues, and the stream outlives both (it is the caller's, not
+    destroyed with a sector)."""
+    import torch
+
+    cfg = CASES[0][1]()
+    real = cfg.is_real()
+    st = torch.cuda.Stream()
+    qs = [q for q in CASES[0][2] if NCV < _oracle_H(cfg, q).shape[0] <= 5000][:2]
+    assert qs, "no sector in the thick-restart range"
+    for q in qs:
+        H = _oracle_H(cfg, q)
+        with Sector(cfg, q[0], q[1], stored=True, real=real, stream=st) as S:
+            _check(S, H, real)
+    with torch.cuda.stream(st):
+        x = torch.ones(1024, device="cuda", dtype=torch.float64)
+        y = (2.0 * x).sum()
+    st.synchronize()
+    assert float(y) == 2048.0
