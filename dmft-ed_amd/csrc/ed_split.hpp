@@ -171,11 +171,14 @@ __global__ void __launch_bounds__(kSplitBuildBlock) k_split_b(const int64_t* __r
     bool even = true;  // every U column offset even
     for (int k0 = 0; k0 < nf0; k0++) {
       const unsigned long long key = keys[wv][k0][0];
+      // the first not yet matched slot with this key: a row holding the same
+      // (col, value) key twice matches it once per occurrence (k_fill does
+      // not merge duplicate columns the way sp_insert_element would)
       int pos[2] = {-1, -1};
 #pragma unroll
       for (int h = 0; h < 2; h++)
-        for (int j = 0; j < nf[h]; j++)
-          if (keys[wv][j][2 * lane + h] == key) pos[h] = j;
+        for (int j = nf[h] - 1; j >= 0; j--)
+          if (!((used[h] >> j) & 1u) && keys[wv][j][2 * lane + h] == key) pos[h] = j;
       const bool mine = (!on[0] || pos[0] >= 0) && (!on[1] || pos[1] >= 0);
       if (__ballot(mine) == __ballot(1)) {
 #pragma unroll

@@ -14,13 +14,14 @@ LIB_PATH = os.path.join(_PKG_ROOT, "libedgpu.so")
 
 ED_STORED, ED_DIRECT, ED_REAL = 0x1, 0x2, 0x4
 ED_NO_PACK, ED_KRON2_OFF, ED_KRON2_ON, ED_NO_SPLIT, ED_SPLIT_ON = 0x10, 0x20, 0x40, 0x80, 0x100
+ED_FUSED_ON, ED_NO_FUSED = 0x200, 0x400
 # kernel alternatives of a built sector (ed_sector_set_options, include/ed_gpu.h)
 OPTIONS = {
     "no_persist": 0x001, "persist_stored": 0x002, "no_preg": 0x004, "no_pkron": 0x008,
     "split_simple": 0x020, "no_batch": 0x040, "eigh_no_verify": 0x080,
     "trlan_unfused": 0x100, "trlan_nofold": 0x200, "no_graph": 0x800,
     "trlan_nolocal": 0x1000, "trlan_nosolo": 0x2000, "trlan_fullupd": 0x4000,
-    "stored_exact": 0x100000,
+    "stored_exact": 0x100000, "eigh_fullprobe": 0x200000, "no_fused": 0x400000,
 }
 ED_OK = 0
 ERRORS = {1: "ED_ERR_ARG", 2: "ED_ERR_STATE", 3: "ED_ERR_HIP", 4: "ED_ERR_OOM",
@@ -81,7 +82,9 @@ class SectorInfo(ctypes.Structure):
                 ("dimup", _i64), ("dimdw", _i64), ("device_bytes", _i64),
                 ("packed", _i32), ("npdict", _i32), ("row0", _i64), ("nrows", _i64),
                 ("split", _i32), ("pad_", _i32), ("split_far", _i64), ("split_far_uniform", _i64),
-                ("split_bytes", _i64), ("split_list_bytes", _i64)]
+                ("split_bytes", _i64), ("split_list_bytes", _i64),
+                ("fused", _i32), ("pad2_", _i32), ("fused_far", _i64), ("fused_far_uniform", _i64),
+                ("fused_bytes", _i64)]
 
 
 class EDGPUError(RuntimeError):

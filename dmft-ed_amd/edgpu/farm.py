@@ -128,8 +128,13 @@ def farm_diag(cfg: EDConfig, opt: Optional[DiagOptions] = None, *, device: int =
     owner_of: Dict[int, int] = {}
     for rk, t in enumerate(allt):
         for k, v in t.items():
+            if k in merged:
+                raise RuntimeError(f"farm_diag: sector {k} solved by ranks {owner_of[k]} and {rk}")
             merged[k] = v
             owner_of[k] = rk
+    missing = sorted({s.isector for s in secs} - set(merged))
+    if missing:
+        raise RuntimeError(f"farm_diag: sectors {missing[:8]} (of {len(missing)}) solved by no rank")
     if assignment is None:
         assignment = [sorted(k for k, o in owner_of.items() if o == r) for r in range(world)]
     shadows = []
@@ -152,7 +157,9 @@ def _queue_store(dist):
     torch.distributed.TCPStore API: MASTER_ADDR:MASTER_PORT is the server that
     torchrun's agent (or rank 0's env:// init) keeps alive for the whole job.
     Every rank connects as a client (is_master=False); keys live under the
-    prefix "edgpu_farm/".  None (and the reason recorded) when the variables are
+    prefix "edgpu_farm/<TORCHELASTIC_RUN_ID>/<TORCHELASTIC_RESTART_COUNT>/" (the
+    agent's store outlives an elastic restart; each farm call's counter key
+    is moreover unique, _global_queue).  None (and the reason recorded) when the variables are
     absent or the connection fails: the farm then runs the static LPT
     partition, which needs no store."""
     if _QUEUE_STORE:
@@ -168,7 +175,9 @@ def _queue_store(dist):
     else:
         try:
             tcp = dist.TCPStore(addr, int(port), is_master=False, timeout=datetime.timedelta(seconds=60))
-            store = dist.PrefixStore("edgpu_farm/", tcp)
+            run = os.environ.get("TORCHELASTIC_RUN_ID", "none")
+            attempt = os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")
+            store = dist.PrefixStore(f"edgpu_farm/{run}/{attempt}/", tcp)
         except Exception as e:   # noqa: BLE001 - any connection failure means: no dynamic queue
             why = f"TCPStore({addr}:{port}) client failed: {type(e).__name__}: {e}"
     if store is None:
@@ -184,11 +193,14 @@ def _global_queue(dist, n: int):
     next of n indices (0, 1, ...) or None.  One counter key per farm call
     (every rank makes the same sequence of farm_diag calls, so the keys
     agree); the store's add is atomic, each index goes to exactly one taker.
-    A barrier first, so no rank takes from the counter of a call the others
+    The key carries a token rank 0 draws and broadcasts per call, so a
+    counter left on the store by an earlier call or job attempt is never
+    reused.  A barrier first, so no rank takes from the counter of a call the others
     have not reached.  Returns None when no store is reachable (every rank
     decides the same way: a collective agreement on the store's availability
     precedes the first use, so ranks never mix the two schedules)."""
     import threading
+    import uuid
 
     import torch
 
@@ -199,8 +211,12 @@ def _global_queue(dist, n: int):
     dist.all_reduce(ok, op=dist.ReduceOp.MIN)
     if int(ok.item()) == 0:
         return None
+    # a counter key no earlier call (nor an earlier incarnation of this job
+    # on the same store) can have used: rank 0's random token, broadcast
     _QUEUE_CALLS[0] += 1
-    key = f"queue_{_QUEUE_CALLS[0]}"
+    tok = [uuid.uuid4().hex if dist.get_rank() == 0 else None]
+    dist.broadcast_object_list(tok, src=0)
+    key = f"queue_{_QUEUE_CALLS[0]}_{tok[0]}"
     dist.barrier()
     lock = threading.Lock()   # one store client per process: serialise its use
     done = [False]

@@ -50,13 +50,14 @@ class Sector:
     def __init__(self, cfg: EDConfig, q1: int, q2: int = 0, *, stored: bool = True,
                  direct: bool = False, real: bool = False, device: int = 0, rows=None,
                  pack: bool = True, kron2: Optional[bool] = None, split: Optional[bool] = None,
-                 options=(), stream=None):
+                 fused: Optional[bool] = None, options=(), stream=None):
         """rows=(row0, nrows): hold only those rows of H (ed_sector_create_rows,
         the reference's MPI row split); H·v then maps a whole-sector vector to
         the nrows local entries.  pack=False keeps the plain SELL arrays only;
         kron2 forces the two-pass Kronecker tables on (True) or off (False);
         split forces the two-segment stored form on (True, any size) or off
         (False; default: built for stored matrices beyond the Infinity Cache);
+        fused likewise for the fused one-pass re-laid form (ed_fused.hpp);
         options: names of ED_OPT_* kernel alternatives (see set_options);
         stream: a torch.cuda.Stream (or raw hipStream_t) the sector runs its
         build and synchronous entry points on, kept by the caller and alive
@@ -70,6 +71,8 @@ class Sector:
             flags |= ED_KRON2_ON if kron2 else ED_KRON2_OFF
         if split is not None:
             flags |= _lib.ED_SPLIT_ON if split else _lib.ED_NO_SPLIT
+        if fused is not None:
+            flags |= _lib.ED_FUSED_ON if fused else _lib.ED_NO_FUSED
         h = ctypes.c_void_p()
         if rows is None:
             check(lib.ed_sector_create(ctypes.byref(self._params), q1, q2, flags, device,
@@ -95,7 +98,8 @@ class Sector:
         """Select kernel alternatives by name (ED_OPT_*: no_persist,
         persist_stored, no_preg, no_pkron, split_simple, no_batch,
         eigh_no_verify, trlan_unfused, trlan_nofold, no_graph, trlan_nolocal,
-        trlan_nosolo, trlan_fullupd; edgpu._lib.OPTIONS); no names
+        trlan_nosolo, trlan_fullupd, stored_exact, eigh_fullprobe, no_fused;
+        edgpu._lib.OPTIONS); no names
         restores the defaults."""
         bits = 0
         for n in names:

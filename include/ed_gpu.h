@@ -67,6 +67,8 @@ extern "C" {
 #define ED_KRON2_ON  0x40 /* two-pass Kronecker tables below the size threshold too */
 #define ED_NO_SPLIT  0x80 /* stored: no two-segment form (one-pass k_spmv_pk only)          */
 #define ED_SPLIT_ON  0x100 /* stored: two-segment form below the size threshold too        */
+#define ED_FUSED_ON  0x200 /* stored: fused one-pass re-laid form below the size threshold too */
+#define ED_NO_FUSED  0x400 /* stored: no fused one-pass re-laid form                       */
 
 /* Kernel-selection options of a built sector (ed_sector_set_options): the
  * alternatives kept for parity tests and A/B measurements.  0 = the default
@@ -89,6 +91,10 @@ extern "C" {
 #define ED_OPT_TRLAN_FULLUPD  0x4000 /* eigh: full CGS update every step (no local-only update) */
 #define ED_OPT_STORED_EXACT 0x100000 /* stored H·v: the one-pass kernel (spMatVec_cc's per-row order,
                                         bit-identical) even where the two-segment form is built */
+#define ED_OPT_NO_FUSED     0x400000 /* stored H·v: not the fused re-laid one-pass kernel (the
+                                        two-segment form where built, else the one-pass one) */
+#define ED_OPT_EIGH_FULLPROBE 0x200000 /* eigh: no plain-Lanczos screen before the thick-restart
+                                          degeneracy probe (every probe round runs it in full) */
 
 /* status codes */
 #define ED_OK              0
@@ -157,6 +163,12 @@ typedef struct ed_sector_info {
   int64_t split_bytes;        /* bytes one two-segment launch reads of the re-laid matrix:
                                  4 * (A words + L words) + 8 * U entries + A slice pointers */
   int64_t split_list_bytes;   /* + segment B's work list and slice table       */
+  int32_t fused;    /* 1 if the fused one-pass re-laid form is built (default stored H·v) */
+  int32_t pad2_;
+  int64_t fused_far;          /* cross-block elements                         */
+  int64_t fused_far_uniform;  /* of which stored once per 64-row unit (U)     */
+  int64_t fused_bytes;        /* bytes one fused launch reads of the re-laid matrix:
+                                 4 * (A words + L words) + 8 * U entries + 40 * units */
 } ed_sector_info;
 
 typedef struct ed_sector ed_sector; /* opaque */

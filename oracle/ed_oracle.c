@@ -495,16 +495,29 @@ static int stored_row(const model_t* M, const uint32_t* map, int64_t dim, int64_
  * cols/vals (complex interleaved) of capacity `cap`.  With cols == NULL only
  * counts.  Returns nnz, or <0 on error.
  */
+int64_t orc_build_csr_rows(const ed_params* p, const uint32_t* map, int64_t dim, int64_t row0, int64_t nrows,
+                           int64_t* rowptr, int32_t* cols, double* vals, int64_t cap);
 int64_t orc_build_csr(const ed_params* p, const uint32_t* map, int64_t dim, int64_t* rowptr,
                       int32_t* cols, double* vals, int64_t cap) {
+  return orc_build_csr_rows(p, map, dim, 0, dim, rowptr, cols, vals, cap);
+}
+
+/* Rows [row0, row0+nrows) of the same CSR (columns index the whole sector):
+ * the sampled-row parity of the full-size sectors, whose whole CSR the tests
+ * do not build on the host (ED_HAMILTONIAN_STORED_HxV.f90:28-113 restricted
+ * to the rows of one MPI rank, as the reference's own row split does at
+ * ED_HAMILTONIAN.f90:55-62).  rowptr has nrows+1 entries, starting at 0. */
+int64_t orc_build_csr_rows(const ed_params* p, const uint32_t* map, int64_t dim, int64_t row0, int64_t nrows,
+                           int64_t* rowptr, int32_t* cols, double* vals, int64_t cap) {
   model_t M;
   if (model_init(&M, p)) return -1;
+  if (row0 < 0 || nrows < 0 || row0 + nrows > dim) return -5;
   enum { RMAX = 4096 };
   int32_t* rc = (int32_t*)malloc(sizeof(int32_t) * RMAX);
   cplx* rv = (cplx*)malloc(sizeof(cplx) * RMAX);
   int64_t nnz = 0;
   if (rowptr) rowptr[0] = 0;
-  for (int64_t i = 0; i < dim; i++) {
+  for (int64_t i = row0; i < row0 + nrows; i++) {
     rowbuf R = {0, RMAX, rc, rv, 0};
     int st = stored_row(&M, map, dim, i, &R);
     if (st) { free(rc); free(rv); return st; }
@@ -517,7 +530,7 @@ int64_t orc_build_csr(const ed_params* p, const uint32_t* map, int64_t dim, int6
       }
     }
     nnz += R.n;
-    if (rowptr) rowptr[i + 1] = nnz;
+    if (rowptr) rowptr[i - row0 + 1] = nnz;
   }
   free(rc);
   free(rv);

@@ -33,6 +33,8 @@ def lib():
         L.orc_ns.argtypes = [P]; L.orc_ns.restype = ctypes.c_int
         L.orc_build_sector.argtypes = [P, i32, i32, P]; L.orc_build_sector.restype = i64
         L.orc_build_csr.argtypes = [P, P, i64, P, P, P, i64]; L.orc_build_csr.restype = i64
+        L.orc_build_csr_rows.argtypes = [P, P, i64, i64, i64, P, P, P, i64]
+        L.orc_build_csr_rows.restype = i64
         L.orc_spmv.argtypes = [i64, P, P, P, P, P]; L.orc_spmv.restype = None
         L.orc_spmv_real.argtypes = [i64, P, P, P, P, P]; L.orc_spmv_real.restype = None
         L.orc_direct_hxv.argtypes = [P, P, i64, P, P]; L.orc_direct_hxv.restype = ctypes.c_int
@@ -76,6 +78,21 @@ class Oracle:
         cols = np.zeros(nnz, dtype=np.int32)
         vals = np.zeros(nnz, dtype=np.complex128)
         r = L.orc_build_csr(self._pp, _p(hmap), dim, _p(rowptr), _p(cols), _p(vals), nnz)
+        assert r == nnz
+        return rowptr, cols, vals
+
+    # rows [row0, row0+nrows) of ed_buildH_c's CSR (ED_HAMILTONIAN_STORED_HxV.f90:28-113)
+    def build_csr_rows(self, hmap: np.ndarray, row0: int, nrows: int):
+        L = lib()
+        dim = len(hmap)
+        hmap = np.ascontiguousarray(hmap, dtype=np.uint32)
+        rowptr = np.zeros(nrows + 1, dtype=np.int64)
+        nnz = L.orc_build_csr_rows(self._pp, _p(hmap), dim, row0, nrows, _p(rowptr), None, None, 0)
+        if nnz < 0:
+            raise RuntimeError(f"orc_build_csr_rows failed ({nnz})")
+        cols = np.zeros(nnz, dtype=np.int32)
+        vals = np.zeros(nnz, dtype=np.complex128)
+        r = L.orc_build_csr_rows(self._pp, _p(hmap), dim, row0, nrows, _p(rowptr), _p(cols), _p(vals), nnz)
         assert r == nnz
         return rowptr, cols, vals
 

@@ -18,3 +18,20 @@ def c4_config(bath="random"):
 
 def c5_config(bath="random"):
     return make_config(bath=bath, seed=SEED, **C5_KW)
+
+
+# Adversarial degeneracy-probe sector (tests/golden/make_adversarial.py): the
+# configs[3] model with orbital 2's bath set equal to orbital 1's ("equal bath
+# pairs": the orbital swap is then a symmetry and every level of the (1,3)
+# sector is an exact pair) and an orbital-symmetric impurity level `ed` tuned
+# so that two pairs from different swap blocks lie a chosen distance apart.
+ADV_SECTOR = (1, 3)
+
+
+def adv_config(ed):
+    cfg = make_config(bath="random", seed=SEED, **C4_KW)
+    cfg.bath.e[:, 1, :] = cfg.bath.e[:, 0, :]
+    cfg.bath.v[:, 1, :] = cfg.bath.v[:, 0, :]
+    cfg.impHloc[0, 0, 0, 0] = ed
+    cfg.impHloc[0, 0, 1, 1] = ed
+    return cfg

@@ -76,7 +76,7 @@ def _worker(rank, world, port, q, cfg_kw, method, schedule="dynamic", init="env"
     from oracle_solver import solve_sector_oracle
     from edgpu.farm import QUEUE_FALLBACK, broadcast_vector
 
-    if init == "env":
+    if init in ("env", "stale"):
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -85,7 +85,20 @@ def _worker(rank, world, port, q, cfg_kw, method, schedule="dynamic", init="env"
         os.environ.pop("MASTER_PORT", None)
         dist.init_process_group("gloo", rank=rank, world_size=world, init_method=init)
     cfg = make_config(**cfg_kw)
+    if init == "stale":
+        # counters an earlier attempt of the job left on the agent's store
+        # under the old fixed keys (queue_1, queue_2, ...): exhausted
+        import datetime
+
+        if rank == 0:
+            tcp = dist.TCPStore("127.0.0.1", port, is_master=False, timeout=datetime.timedelta(seconds=30))
+            old = dist.PrefixStore("edgpu_farm/none/0/", tcp)
+            for k in range(1, 4):
+                old.add(f"queue_{k}", 10_000)
+        dist.barrier()
     res = farm_diag(cfg, DiagOptions(lanc_method=method, farm_schedule=schedule), solver=solve_sector_oracle)
+    if init == "stale":   # a second farm call in the same job takes a fresh counter too
+        res = farm_diag(cfg, DiagOptions(lanc_method=method, farm_schedule=schedule), solver=solve_sector_oracle)
     gs_owner = res.owners[0]
     v = res.states.vectors[0] if rank == gs_owner else None
     dim = [s for s in setup_pointers(cfg) if s.isector == res.states.sectors[0]][0].dim
@@ -111,31 +124,33 @@ def _run_ranks(world, cfg_kw, method, schedule, init="env"):
     return sorted(out, key=lambda o: o[0])
 
 
-@pytest.mark.parametrize("world,init", [(4, "env"), (2, "file")])
+@pytest.mark.parametrize("world,init", [(4, "env"), (2, "file"), (2, "stale")])
 def test_gloo_dynamic_queue(world, init, tmp_path):
     """The dynamic sector queue through the public TCPStore client: 4 ranks
     (processes) take sectors from one counter and reproduce the serial state
     list; with a file rendezvous (no MASTER_ADDR/PORT) every rank falls back
-    to the LPT partition, says why, and still reproduces it."""
+    to the LPT partition, says why, and still reproduces it; with exhausted
+    counters left on the store by an earlier job attempt ("stale") each call
+    still takes a fresh per-call key and solves every sector."""
     from oracle_solver import solve_sector_oracle
 
     cfg_kw, method = dict(Norb=1, Nbath=5), "lanczos"
     cfg = make_config(**cfg_kw)
     serial = farm_diag(cfg, DiagOptions(lanc_method=method), solver=solve_sector_oracle)
-    init_arg = "env" if init == "env" else f"file://{tmp_path}/rdzv"
+    init_arg = init if init in ("env", "stale") else f"file://{tmp_path}/rdzv"
     out = _run_ranks(world, cfg_kw, method, "dynamic", init_arg)
     for rank, en, secs, owners, assignment, vnorm, fallback in out:
         assert secs == serial.states.sectors
         np.testing.assert_allclose(en, serial.states.energies, rtol=0, atol=1e-12)
         assert abs(vnorm - 1.0) < 1e-10
-        if init == "env":
+        if init in ("env", "stale"):
             assert fallback == []
         else:
             assert len(fallback) == 1 and "MASTER_ADDR" in fallback[0]
     assign = out[0][4]
     assert all(o[4] == assign for o in out)
     assert sorted(i for a in assign for i in a) == sorted(s.isector for s in setup_pointers(cfg))
-    if init != "env":    # LPT: every rank got work
+    if init == "file":    # LPT: every rank got work
         assert all(len(a) > 0 for a in assign)
 
 

@@ -73,3 +73,28 @@ def test_c5_gf_fixture_shape():
         assert g["Gm"].shape == (2, 2, 1, 1, 100) and g["iw_index"][1] == 50
         # causality: Im G_ss(iw_n) < 0 on the positive Matsubara axis
         assert np.all(g["Gm"][0, 0, 0, 0].imag < 0) and np.all(g["Gm"][1, 1, 0, 0].imag < 0)
+
+
+@pytest.mark.parametrize("case", [0, 3])
+def test_adversarial_probe_fixture(case):
+    """tests/golden/adversarial_probe.json: the dense spectrum of the tuned
+    sector is reproduced from the oracle's CSR, every level is an exact pair,
+    and the pairs at positions 4-5 and 6-7 lie the fixture's gap apart."""
+    import scipy.sparse as sp
+
+    from golden.golden_configs import ADV_SECTOR, adv_config
+    from oracle.oracle import Oracle
+
+    d = _load("adversarial_probe.json")
+    c = d["cases"][case]
+    orc = Oracle(adv_config(c["ed"]))
+    hmap = orc.build_sector(*ADV_SECTOR)
+    rp, cols, vals = orc.build_csr(hmap)
+    H = sp.csr_matrix((vals.real, cols, rp), shape=(len(hmap), len(hmap)))
+    w = np.linalg.eigvalsh(H.toarray())[:10]
+    ref = np.asarray(c["eigenvalues"])
+    e = abs(ref[0])
+    assert np.max(np.abs(w - ref)) < 1e-12 * e
+    assert np.max(np.abs(ref[0::2] - ref[1::2])) < 1e-12 * e
+    assert abs((ref[6] - ref[4]) - abs(c["gap"])) < 1e-3 * abs(c["gap"])
+    assert abs(c["gap"]) <= 1.01e-8 * e

@@ -132,3 +132,46 @@ def test_eigh_on_caller_stream():
         y = (2.0 * x).sum()
     st.synchronize()
     assert float(y) == 2048.0
+
+
+def _adversarial():
+    import json
+    import os
+
+    with open(os.path.join(os.path.dirname(__file__), "golden", "adversarial_probe.json")) as fh:
+        return json.load(fh)
+
+
+@pytest.mark.parametrize("case", range(6), ids=["-1e-8", "-3e-9", "-3e-10", "+3e-10", "+3e-9", "+1e-8"])
+def test_probe_near_cut_degenerate_pair(case):
+    """Adversarial sector for the degeneracy probe (tests/golden/
+    make_adversarial.py): every level is an exact pair and two pairs from
+    different symmetry blocks lie |delta| = 3e-10..1e-8 of |E| apart at
+    positions 4-7, so after the probe has recovered the two lower pairs' copies
+    the complement holds the missed copy of the lower pair just under the cut
+    and a copy of the upper pair just above it.  Without the probe
+    (ED_OPT_EIGH_NO_VERIFY) the solve misses copies; the default (screen +
+    probe) and the full thick-restart probe (ED_OPT_EIGH_FULLPROBE) both return
+    the dense spectrum within 1e-10 (ED_DIAG.f90:88-101 Neigen=6, Nblock=23)."""
+    from golden.golden_configs import ADV_SECTOR, adv_config
+
+    fx = _adversarial()
+    c = fx["cases"][case]
+    ref = np.asarray(c["eigenvalues"][:NEV])
+    scale = max(1.0, float(np.max(np.abs(ref))))
+    cfg = adv_config(c["ed"])
+    with Sector(cfg, *ADV_SECTOR, stored=True, real=True) as S:
+        assert S.dim == fx["dim"]
+        S.set_options("eigh_no_verify")
+        w, _, _, _ = S.eigh(neigen=NEV, ncv=NCV, maxit=512, tol=1e-12, vectors=False)
+        assert np.max(np.abs(w - ref)) > 1e-6 * scale, "no copy missed: the probe is untested here"
+        got = {}
+        for opts in ((), ("eigh_fullprobe",)):
+            S.set_options(*opts)
+            w, _, nconv, nhv = S.eigh(neigen=NEV, ncv=NCV, maxit=512, tol=1e-12, vectors=False)
+            err = float(np.max(np.abs(w - ref))) / scale
+            got[opts] = (err, nhv)
+            assert nconv == NEV
+            assert err < 1e-10, (opts, err, w - ref)
+    print(f"delta_rel {c['delta_rel']:+.0e}: screen+probe {got[()][1]} H·v (err {got[()][0]:.1e}), "
+          f"full probe {got[('eigh_fullprobe',)][1]} H·v")

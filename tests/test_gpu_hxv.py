@@ -135,7 +135,9 @@ def test_complex_vr_stored_semantics():
 @pytest.mark.parametrize("pin", ["n28_norb1", "n28_norb2"])
 def test_full_size_roofline_sectors(pin):
     """Nlevels=28 (7,7) sectors at full size (dim 11,778,624): nnz pins of the
-    reference run, size-independent properties: hermiticity <x,Hy> = <Hx,y>,
+    reference run, the default stored H·v against the oracle on >= 16,384
+    sampled rows (1e-13 of the row's absolute sum, tests/sampled_rows.py),
+    size-independent properties: hermiticity <x,Hy> = <Hx,y>,
     the one-pass stored kernel (ED_OPT_STORED_EXACT) == generic matrix-free
     bit for bit, the default two-segment stored kernel and Kronecker to 1e-13."""
     import json
@@ -147,6 +149,10 @@ def test_full_size_roofline_sectors(pin):
     pins = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "survey_pins.json")))
     p = [x for x in pins["sectors"] if x["name"] == pin][0]
     cfg = make_config(bath="random", seed=1, **p["config"])
+    from sampled_rows import check_rows, sample_starts
+
+    orc = Oracle(cfg)
+    hmap = orc.build_sector(*p["sector"])
     with Sector(cfg, *p["sector"], stored=True, direct=True, real=True) as S:
         assert S.dim == p["dim"] and S.nnz == p["nnz"]
         g = torch.Generator(device="cuda:0").manual_seed(0)
@@ -155,6 +161,9 @@ def test_full_size_roofline_sectors(pin):
         hx, hy = torch.empty_like(x), torch.empty_like(x)
         S.hxv_dev(x, hx, path=0)
         S.hxv_dev(y, hy, path=0)
+        # the default (two-segment) stored H·v against the oracle's rows
+        worst = check_rows(orc, hmap, x.cpu().numpy(), hx.cpu().numpy(), sample_starts(S.dim, seed=1))
+        print(f"{pin}: worst sampled-row error {worst:.1e} of sum|H_ij x_j|")
         a, b = torch.dot(y, hx).item(), torch.dot(hy, x).item()
         assert abs(a - b) <= 1e-12 * abs(a)
         h1 = torch.empty_like(x)

@@ -153,3 +153,30 @@ def test_jz_sectors_partition_and_targets():
             assert (t.q1, t.q2) == (7, 2 * lz[iorb] + sz)
             t = c_sector(cfg, sec, ispin, iorb)
             assert (t.q1, t.q2) == (5, -(2 * lz[iorb] + sz))
+
+
+def test_build_csr_rows_and_sampled_check():
+    """orc_build_csr_rows equals the matching slice of orc_build_csr, and the
+    sampled-row check of the full-size GPU tests (tests/sampled_rows.py)
+    accepts spMatVec_cc's own result and rejects a perturbed one."""
+    from cases import CASES
+    from oracle.oracle import spmv
+    from sampled_rows import check_rows, sample_starts
+
+    cfg = CASES[0][1]()
+    orc = Oracle(cfg)
+    hmap = orc.build_sector(*CASES[0][2][0])
+    csr = orc.build_csr(hmap)
+    rp, cols, vals = csr
+    r0, n = 37, 101
+    rp2, c2, v2 = orc.build_csr_rows(hmap, r0, n)
+    np.testing.assert_array_equal(rp2, rp[r0:r0 + n + 1] - rp[r0])
+    np.testing.assert_array_equal(c2, cols[rp[r0]:rp[r0 + n]])
+    np.testing.assert_array_equal(v2, vals[rp[r0]:rp[r0 + n]])
+    x = start_vector(len(hmap))
+    y = spmv(csr, x)
+    starts = sample_starts(len(hmap), nblocks=16, block=640)
+    assert check_rows(orc, hmap, x, y, starts, block=640) <= 1e-15
+    y[starts[3] + 5] += 1e-6
+    with pytest.raises(AssertionError):
+        check_rows(orc, hmap, x, y, starts, block=640)
