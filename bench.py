@@ -50,7 +50,7 @@ import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 GOLD = os.path.join(ROOT, "tests", "golden")
-PROFILES = [os.path.join(ROOT, "profiles", r) for r in ("r5", "r4", "r3")]  # newest summary first
+PROFILES = [os.path.join(ROOT, "profiles", r) for r in ("r6", "r5", "r4", "r3")]  # newest summary first
 
 
 def spmv_bytes_real(nnz, dim):
@@ -96,6 +96,15 @@ def spmv_bytes_packed_complex(padded, dim):
     return 4 * padded + 8 * (nslice + 1) + 16 * dim + 32 * dim
 
 
+def spmv_bytes_fused(inf, dim, cplx):
+    """Bytes the fused one-pass re-laid stored H·v (k_spmv_fu) moves: the
+    re-laid matrix (4-B A and L words, 8-B U entries, 40-B unit descriptors),
+    the diagonal (8 B real H, 16 B complex), read v and write Hv (8 or 16 B)."""
+    hd = 8 if inf["real_h"] else 16
+    vb = 16 if cplx else 8
+    return inf["fused_bytes"] + hd * dim + 2 * vb * dim
+
+
 def spmv_bytes_split(inf, dim):
     """Bytes the two-segment stored H·v (k_spmv_sa + k_spmv_sb) moves: the
     re-laid matrix (4-B A words, 8-B U entries, 4-B L words, A slice pointers),
@@ -105,15 +114,24 @@ def spmv_bytes_split(inf, dim):
     return inf["split_bytes"] + inf["split_list_bytes"] + 48 * dim
 
 
-def measure_hxv(Sector, cfg, q, iters, path=0, warm=5, info=None, cplx=False, batch=False, options=()):
+def measure_hxv(Sector, cfg, q, iters, path=0, warm=5, info=None, cplx=False, batch=False, options=(),
+                real_h=None):
+    """Average ms per H·v launch.  cplx: complex(8) vectors, and complex(8) H
+    values unless real_h=True (complex vectors on the real H)."""
     stored = path == 0
-    with Sector(cfg, q[0], q[1], stored=stored, direct=not stored, real=not cplx, options=options) as S:
+    real = (not cplx) if real_h is None else real_h
+    with Sector(cfg, q[0], q[1], stored=stored, direct=not stored, real=real, options=options) as S:
         dim, nnz = S.dim, S.nnz
         if info is not None:
+            exact = "stored_exact" in options
+            fused = int(S.info.fused) if (stored and not exact and "no_fused" not in options) else 0
             info.update(packed=int(S.info.packed), padded=int(S.info.padded), npdict=int(S.info.npdict),
-                        split=int(S.info.split) if (stored and not cplx and "stored_exact" not in options) else 0,
+                        split=int(S.info.split) if (stored and not cplx and not exact) else 0,
                         split_bytes=int(S.info.split_bytes), split_list_bytes=int(S.info.split_list_bytes),
-                        split_far=int(S.info.split_far), split_far_uniform=int(S.info.split_far_uniform))
+                        split_far=int(S.info.split_far), split_far_uniform=int(S.info.split_far_uniform),
+                        fused=fused if (cplx or not S.info.split) else 0, fused_bytes=int(S.info.fused_bytes),
+                        fused_far=int(S.info.fused_far), fused_far_uniform=int(S.info.fused_far_uniform),
+                        real_h=int(real))
         i = torch.arange(1, dim + 1, dtype=torch.float64, device="cuda")
         x = (torch.complex(torch.sin(i), torch.cos(3 * i)) if cplx else torch.sin(i)).contiguous()
         y = torch.empty_like(x)
@@ -431,18 +449,21 @@ def roofline_sweep(Sector, make_config):
         for cplx in (False, True):
             inf = {}
             dim, nnz, ms = measure_hxv(Sector, cfg, q, 30, path=0, info=inf, cplx=cplx)
-            if inf["packed"]:
+            if inf["fused"]:
+                Bown = spmv_bytes_fused(inf, dim, cplx)
+            elif inf["packed"]:
                 Bown = (spmv_bytes_packed_complex if cplx else spmv_bytes_packed)(inf["padded"], dim)
             else:
                 Bown = (20 * nnz + 8 * (dim + 1) + 32 * dim) if cplx else spmv_bytes_real(nnz, dim)
-            tr, tsrc = _traffic(f"spmv_{name}{'_cplx' if cplx else ''}_traffic.json")
+            tr, tsrc = _traffic(f"{'fused' if inf['fused'] else 'spmv'}_{name}{'_cplx' if cplx else ''}_traffic.json")
             row["stored_complex" if cplx else "stored"] = {
                 "dim": dim, "nnz": nnz, "ms_per_launch": round(ms, 4), "bytes_per_launch": Bown,
                 "achieved": round(Bown / (ms * 1e-3) / 1e9, 1),
                 "frac": round(Bown / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                 "traffic": tr, "traffic_source": tsrc,
                 "physical_gbs": round(tr / (ms * 1e-3) / 1e9, 1) if tr else None,
-                "kernel": ("k_spmv_pk" if inf["packed"] else "k_spmv") + ("<complex>" if cplx else "<real>")}
+                "kernel": ("k_spmv_fu" if inf["fused"] else "k_spmv_pk" if inf["packed"] else "k_spmv") +
+                          ("<complex>" if cplx else "<real>")}
         _, _, msd = measure_hxv(Sector, cfg, q, 20, path=1)
         td, tdsrc = _traffic(f"direct_{name}_traffic.json")
         row["direct_generic"] = {"ms_per_hxv": round(msd, 4),
@@ -542,19 +563,43 @@ def bench_roofline(Sector, make_config):
                               "own_bytes": 24 * dimk,  # v read, Hv written, diagonal vector read
                               "frac_own": round(24 * dimk / (msd * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                               "traffic": td, "traffic_source": tdsrc, "profile": _profile_ms("direct_n28")}
-    infc = {}
-    _, _, msc = measure_hxv(Sector, cfg28, (7, 7), 20, path=0, info=infc, cplx=True)
-    Bc = spmv_bytes_packed_complex(infc["padded"], dim28)
-    tc, tcsrc = _traffic("spmv_cplx_n28_traffic.json")
-    roof["complex"] = {"ms_per_launch": round(msc, 4), "bytes_per_launch": Bc,
-                       "achieved": round(Bc / (msc * 1e-3) / 1e9, 1),
-                       "frac": round(Bc / (msc * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                       "csr_equivalent_gbs": round((20 * nnz28 + 8 * (dim28 + 1) + 32 * dim28)
-                                                   / (msc * 1e-3) / 1e9, 1),
-                       "traffic": tc, "traffic_source": tcsrc, "profile": _profile_ms("spmv_cplx_n28"),
-                       "kernel": f"k_spmv_pk<complex> ({infc['npdict']}-value dictionary of (re, im) "
-                                 "pairs; the reference's complex(8) arithmetic)",
-                       "achieved_basis": "4*padded + 8*(nslice+1) + 16*dim (diagonal) + 32*dim (v, Hv)"}
+    # complex(8): H values and vectors (the reference's arithmetic), and
+    # complex vectors on the real H (the cpu_baseline's arithmetic)
+    for key, real_h, tn in (("complex", False, "cplx_n28"), ("complex_vectors_real_h", True, "cvec_n28")):
+        infc = {}
+        _, _, msc = measure_hxv(Sector, cfg28, (7, 7), 20, path=0, info=infc, cplx=True, real_h=real_h)
+        inf1 = {}
+        _, _, ms1 = measure_hxv(Sector, cfg28, (7, 7), 20, path=0, info=inf1, cplx=True, real_h=real_h,
+                                options=("stored_exact",))
+        B1 = spmv_bytes_packed_complex(inf1["padded"], dim28) - (8 * dim28 if real_h else 0)
+        if infc["fused"]:
+            Bc = spmv_bytes_fused(infc, dim28, True)
+            tc, tcsrc = _traffic(f"fused_{tn}_traffic.json")
+            kern = (f"k_spmv_fu<{'real' if real_h else 'complex'} H, complex v> (fused one-pass re-laid stored "
+                    f"H·v: 64-row units, in-block words, {infc['fused_far_uniform']} of {infc['fused_far']} "
+                    f"cross-block elements once per unit; {infc['npdict']}-value dictionary)")
+            basis = ("fused_bytes (4-B A and L words, 8-B U entries, unit descriptors) + diagonal "
+                     f"({8 if real_h else 16}*dim) + 32*dim (v, Hv)")
+            prof = _profile_ms(f"fused_{tn}")
+        else:
+            Bc, tc, tcsrc, prof = B1, *_traffic(f"spmv_{tn}_traffic.json"), _profile_ms(f"spmv_{tn}")
+            kern = f"k_spmv_pk<{'real' if real_h else 'complex'} H, complex v>"
+            basis = "4*padded + 8*(nslice+1) + diagonal + 32*dim (v, Hv)"
+        t1, t1src = _traffic(f"spmv_{tn}_traffic.json")
+        roof[key] = {"ms_per_launch": round(msc, 4), "bytes_per_launch": Bc,
+                     "achieved": round(Bc / (msc * 1e-3) / 1e9, 1),
+                     "frac": round(Bc / (msc * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "one_pass_bytes_gbs": round(B1 / (msc * 1e-3) / 1e9, 1),
+                     "frac_on_one_pass_bytes": round(B1 / (msc * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "csr_equivalent_gbs": round((20 * nnz28 + 8 * (dim28 + 1) + 32 * dim28)
+                                                 / (msc * 1e-3) / 1e9, 1),
+                     "traffic": tc, "traffic_source": tcsrc,
+                     "traffic_over_own": round(tc / Bc, 3) if tc else None, "profile": prof,
+                     "kernel": kern, "achieved_basis": basis,
+                     "one_pass_exact": {"ms_per_launch": round(ms1, 4), "bytes_per_launch": B1,
+                                        "frac": round(B1 / (ms1 * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                        "traffic": t1, "traffic_source": t1src,
+                                        "kernel": "k_spmv_pk (one pass, bit-identical to spMatVec_cc)"}}
     roof["sweep"] = roofline_sweep(Sector, make_config)
     return roof, kron
 

@@ -48,7 +48,18 @@ struct FuUnit {
 };
 constexpr int kFuFarMax = 32;    // cross-block elements per row the build stages
 constexpr int kFuUChunk = 8;     // U entries per load batch (lists padded to it, or to 7)
-constexpr int kFuLChunk = 4;     // L slots per load batch
+#ifndef ED_FU_LCH
+#define ED_FU_LCH 4
+#endif
+#ifndef ED_FU_CHMAX
+#define ED_FU_CHMAX 8
+#endif
+constexpr int kFuLChunk = ED_FU_LCH;  // L slots per load batch
+// widest A batch: rows of up to 12 in-block elements (Norb=2) take a batch of
+// 8 and one of 4 rather than one of 12 — complex vectors on real H 0.37 ->
+// 0.30 ms at N28b, 0.42 -> 0.33 at N28 with Jx/Jp, real vectors -4 %
+// (gpurun_out r6c, A/B builds -DED_FU_CHMAX=16 / 8)
+constexpr int kFuChMax = ED_FU_CHMAX;
 constexpr int kFuBuildBlock = 256;  // 4 waves: 4 x 32 x 64 keys of 8 B = 64 KB of LDS
 
 // ---- build: one wavefront per unit, one row per lane.  FILL = false: the

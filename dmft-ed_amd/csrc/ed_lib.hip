@@ -661,6 +661,14 @@ static int build_fused(ed_sector* s) {
     uo += u.nu;
     lo += 64 * (int64_t)u.wl;
   }
+  // Default policy: only where (nearly) every cross-block element is
+  // unit-uniform.  nonSU2 spin flips stay per-lane L words: N26 (41 % in U)
+  // 0.394 vs 0.380 ms one-pass for real vectors, 0.556 vs 0.530 complex H
+  // (gpurun_out r6c); N28 with Jx/Jp (95.7 %) gains (0.242 vs 0.275).
+  if (!(s->flags & ED_FUSED_ON) && (double)far_u < 0.9 * (double)far_all) {
+    dfree(s, (void**)&s->d_fu, nu * sizeof(FuUnit));
+    return ED_OK;
+  }
   CK(dcopy(s, s->d_fu, un.data(), nu * sizeof(FuUnit), hipMemcpyHostToDevice));
   CK(dalloc_t(s, &s->d_fa, std::max<int64_t>(ao, 1)));
   CK(dalloc_t(s, &s->d_ful, uo + kFuUChunk));
@@ -1359,19 +1367,22 @@ static int kron_dw_grid(const ed_sector* s, bool vc) {
   return s->K.dimup % 2 == 0 ? kKronDwGrid2 : kKronDwGrid;
 }
 // the two-segment stored kernels serve path 0 unless ED_OPT_STORED_EXACT
-static bool fused_on(const ed_sector* s, int path) {
-  return path == 0 && s->fused && !(s->opts & (ED_OPT_STORED_EXACT | ED_OPT_NO_FUSED));
+// The fused form serves complex(8) vectors, and real vectors where the
+// two-segment form is not built (its y round trip stays in the Infinity Cache
+// for real vectors: N28 0.182 ms against 0.186 fused, gpurun_out r6b).
+static bool fused_on(const ed_sector* s, int path, int vc) {
+  return path == 0 && s->fused && !(s->opts & (ED_OPT_STORED_EXACT | ED_OPT_NO_FUSED)) && (vc || !s->split);
 }
 static bool split_on(const ed_sector* s, int path, int vc = 0) {
   // (real vectors only: with complex(8) vectors x and y do not fit the
   // Infinity Cache together and the split is slower than one pass, N28 0.359
   // against 0.316 ms)
-  return path == 0 && s->split && !vc && !(s->opts & ED_OPT_STORED_EXACT) && !fused_on(s, path);
+  return path == 0 && s->split && !vc && !(s->opts & ED_OPT_STORED_EXACT);
 }
 static int fused_grid(const ed_sector* s, int vc);
 static int hxv_blocks(const ed_sector* s, int path, int vc = 0) {
   if (kron2_on(s, path, vc)) return kron_dw_grid(s, vc);
-  if (fused_on(s, path)) return fused_grid(s, vc);
+  if (fused_on(s, path, vc)) return fused_grid(s, vc);
   if (split_on(s, path, vc)) return kSplitGrid;
   if (path == 1) return s->dir_grid;
   const int g = grid_for(s->nslice * 64);
@@ -1565,8 +1576,8 @@ static int launch_fused(ed_sector* s, const void* x, Epi epi, hipStream_t st) {
 #define ED_FU_CH(NTV, U)                                                   \
   do {                                                                     \
     if (s->fu_wa_max == 7 && s->fu_wa_min == 7) ED_FU(NTV, 7, U);          \
-    else if (s->fu_wa_max <= 8) ED_FU(NTV, 8, U);                          \
-    else if (s->fu_wa_max <= 12) ED_FU(NTV, 12, U);                        \
+    else if (s->fu_wa_max <= 8 || kFuChMax <= 8) ED_FU(NTV, 8, U);         \
+    else if (s->fu_wa_max <= 12 || kFuChMax <= 12) ED_FU(NTV, 12, U);      \
     else ED_FU(NTV, kChunk, U);                                            \
   } while (0)
   if (s->fu_uch == 7) {
@@ -1595,7 +1606,7 @@ static int launch_hxv_t(ed_sector* s, int path, const void* x, Epi epi, hipStrea
   // (segment B's pair items load x and y and store the plain epilogue's Hv
   // = y 16 bytes at a time: an 8-byte aligned view, e.g. a torch slice at an
   // odd offset, takes the one-pass kernel)
-  if (fused_on(s, path)) return launch_fused<HC, VC>(s, x, epi, st);
+  if (fused_on(s, path, VC)) return launch_fused<HC, VC>(s, x, epi, st);
   if (split_on(s, path, VC) && !(((uintptr_t)x | (uintptr_t)epi.scratch()) & 15))
     return launch_split<HC, VC>(s, x, epi, st);
   if (path == 0 && s->d_words) {

@@ -164,7 +164,9 @@ def test_probe_near_cut_degenerate_pair(case):
         assert S.dim == fx["dim"]
         S.set_options("eigh_no_verify")
         w, _, _, _ = S.eigh(neigen=NEV, ncv=NCV, maxit=512, tol=1e-12, vectors=False)
-        assert np.max(np.abs(w - ref)) > 1e-6 * scale, "no copy missed: the probe is untested here"
+        # (a single-vector solve returns hi in place of lo's second copy: off
+        # by |delta|, beyond the 1e-10 bar in every case)
+        assert np.max(np.abs(w - ref)) > 1e-10 * scale, "no copy missed: the probe is untested here"
         got = {}
         for opts in ((), ("eigh_fullprobe",)):
             S.set_options(*opts)

@@ -32,7 +32,11 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--iters", type=int, default=10)
 ap.add_argument("--sectors", default="n28,n26s,n28b,n28j")
 ap.add_argument("--json", default="")
+ap.add_argument("--lib", default="", help="load this libedgpu.so build instead (A/B of kernel variants)")
 a = ap.parse_args()
+if a.lib:
+    import edgpu._lib as _edl
+    _edl.LIB_PATH = os.path.abspath(a.lib)
 
 
 def timed(S, x, y, st, n):

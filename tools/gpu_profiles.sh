@@ -14,23 +14,28 @@ PROF=$OUT/profiles
 mkdir -p "$OUT" "$PROF"
 # name | spmv_probe arguments | kernel-name regex
 ENTRIES=(
-  "spmv_n28|--sector n28 --path 0 --split off|k_spmv_pk<false"
+  "spmv_n28|--sector n28 --path 0 --split off --fused off|k_spmv_pk<false"
   "split_n28|--sector n28 --path 0 --split on|k_spmv_s[ab]<false"
   "split_n28j|--sector n28j --path 0 --split on|k_spmv_s[ab]<false"
   "split_n26s|--sector n26s --path 0 --split on|k_spmv_s[ab]<false"
   "split_n28b|--sector n28b --path 0 --split on|k_spmv_s[ab]<false"
-  "spmv_cplx_n28|--sector n28 --path 0 --complex --split off|k_spmv_pk<true"
+  "spmv_cplx_n28|--sector n28 --path 0 --complex --split off --fused off|k_spmv_pk<true"
+  "fused_cplx_n28|--sector n28 --path 0 --complex|k_spmv_fu"
+  "spmv_cvec_n28|--sector n28 --path 0 --cvec --split off --fused off|k_spmv_pk<false"
+  "fused_cvec_n28|--sector n28 --path 0 --cvec|k_spmv_fu"
   "kron_n28|--sector n28 --path 2|k_kron"
   "direct_n28|--sector n28 --path 1|k_direct"
-  "spmv_n28b|--sector n28b --path 0 --split off|k_spmv_pk<false"
+  "spmv_n28b|--sector n28b --path 0 --split off --fused off|k_spmv_pk<false"
   "kron_n28b|--sector n28b --path 2|k_kron"
   "spmv_c4|--sector c4r --path 0 --split off|k_spmv_pk<false"
   "kron_c4|--sector c4r --path 2|k_kron"
-  "spmv_n28j|--sector n28j --path 0 --split off|k_spmv_pk<false"
-  "spmv_n28j_cplx|--sector n28j --path 0 --complex --split off|k_spmv"
+  "spmv_n28j|--sector n28j --path 0 --split off --fused off|k_spmv_pk<false"
+  "spmv_n28j_cplx|--sector n28j --path 0 --complex --split off --fused off|k_spmv"
+  "fused_n28j|--sector n28j --path 0|k_spmv_fu"
+  "fused_n28j_cplx|--sector n28j --path 0 --complex|k_spmv_fu"
   "direct_n28j|--sector n28j --path 1|k_direct"
-  "spmv_n26s|--sector n26s --path 0 --split off|k_spmv_pk<false"
-  "spmv_n26s_cplx|--sector n26s --path 0 --complex --split off|k_spmv"
+  "spmv_n26s|--sector n26s --path 0 --split off --fused off|k_spmv_pk<false"
+  "spmv_n26s_cplx|--sector n26s --path 0 --complex --split off --fused off|k_spmv"
   "direct_n26s|--sector n26s --path 1|k_direct"
 )
 want=" $* "

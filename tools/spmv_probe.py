@@ -34,6 +34,8 @@ ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--options", default="", help="comma-separated ED_OPT_* names")
 ap.add_argument("--split", default="default", choices=["default", "on", "off"],
                 help="two-segment stored form: library default, forced on, or not built")
+ap.add_argument("--fused", default="default", choices=["default", "on", "off"],
+                help="fused one-pass re-laid stored form: library default, forced on, or not built")
 ap.add_argument("--lib", default="", help="load this libedgpu.so build instead (A/B of kernel variants)")
 a = ap.parse_args()
 if a.lib:
@@ -48,8 +50,9 @@ else:
 real = not a.complex
 opts = tuple(o for o in a.options.split(",") if o)
 split = {"default": None, "on": True, "off": False}[a.split]
+fused = {"default": None, "on": True, "off": False}[a.fused]
 with Sector(cfg, q[0], q[1], stored=(a.path == 0), direct=(a.path != 0), real=real, split=split,
-            options=opts) as S:
+            fused=fused, options=opts) as S:
     dt = torch.float64 if (real and not a.cvec) else torch.complex128
     i = torch.arange(1, S.dim + 1, dtype=torch.float64, device="cuda")
     x = torch.sin(i) if dt == torch.float64 else torch.complex(torch.sin(i), torch.cos(3 * i))
