@@ -680,7 +680,9 @@ def north_star_scalars(out, mode2_ips, direct_ips, cplx_ips, cplxh_ips):
         "nonsu2_c5_diag_s": c5.get("diag_s"),
         "nonsu2_c5_gf_s": c5.get("gf_s"),
         "roofline_frac": roof.get("frac"),
+        "roofline_complex_ms": cplx.get("ms_per_launch"),
         "roofline_complex_frac": cplx.get("frac"),
+        "roofline_complex_frac_on_one_pass_bytes": cplx.get("frac_on_one_pass_bytes"),
         "farm_c4_wall_s": farm.get("wall_s"),
         "farm_c4_speedup_vs_1gpu": farm.get("speedup_vs_1gpu"),
     }

@@ -1557,11 +1557,14 @@ static int launch_split(ed_sector* s, const void* x, Epi epi, hipStream_t st) {
 
 // Fused one-pass re-laid stored H·v (ed_fused.hpp).  Grid: resident blocks,
 // a multiple of 8 (one unit range per XCD).
+#ifndef ED_FU_GRID_DIV
+#define ED_FU_GRID_DIV 1
+#endif
 static int fused_grid(const ed_sector* s, int vc) {
   const int g = vc ? resident_grid((const void*)k_spmv_fu<false, true, 1, EpiStore<true>, 8, 8>, kBlock)
                    : resident_grid((const void*)k_spmv_fu<false, false, 1, EpiStore<false>, 8, 8>, kBlock);
   (void)s;
-  return std::max(8, g & ~7);
+  return std::max(8, (g / ED_FU_GRID_DIV) & ~7);
 }
 
 template <bool HC, bool VC, class Epi>
