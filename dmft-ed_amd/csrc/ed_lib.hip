@@ -1557,8 +1557,12 @@ static int launch_split(ed_sector* s, const void* x, Epi epi, hipStream_t st) {
 
 // Fused one-pass re-laid stored H·v (ed_fused.hpp).  Grid: resident blocks,
 // a multiple of 8 (one unit range per XCD).
+// half the resident grid: 16 waves per CU keep the window of units an XCD
+// works on (and the neighbour V rows its cross-block gathers read) smaller —
+// N28 complex H 0.281 -> 0.269 ms, complex vectors on real H 0.275 -> 0.262,
+// N28 Jx/Jp real 0.239 -> 0.228; a quarter measured slower (gpurun_out r6f)
 #ifndef ED_FU_GRID_DIV
-#define ED_FU_GRID_DIV 1
+#define ED_FU_GRID_DIV 2
 #endif
 static int fused_grid(const ed_sector* s, int vc) {
   const int g = vc ? resident_grid((const void*)k_spmv_fu<false, true, 1, EpiStore<true>, 8, 8>, kBlock)
@@ -2861,8 +2865,16 @@ static int trlan_core(Trlan<VC>& T, int k0, int nev, int maxit, double tol, cons
 constexpr int kScreenChunk = 10;
 constexpr int kScreenMaxSteps = 400;
 constexpr double kProbeMargin = 1e-11;
+// hint: column k0 holds the next Ritz vector of the main solve (round 0 of
+// the probe) — the start vector is then the hash vector plus that Ritz
+// vector at equal norm.  Where nothing was missed the complement's lowest
+// eigenvector is the next one, which the mixed start already carries with
+// weight ~1/2, so theta converges in fewer steps; a missed copy lies outside
+// the main solve's Krylov space (in exact arithmetic) and is reached through
+// the hash part, whose overlap with it is 1/sqrt(2) of a pure hash start's.
 template <bool VC>
-static int probe_screen(Trlan<VC>& T, int k0, int maxsteps, double tol, double cut, uint64_t seed, int* below) {
+static int probe_screen(Trlan<VC>& T, int k0, int maxsteps, double tol, double cut, uint64_t seed, int* below,
+                        bool hint = false) {
   using V = val_t<VC>;
   const int64_t dim = T.dim;
   hipStream_t st = T.st;
@@ -2885,6 +2897,9 @@ static int probe_screen(Trlan<VC>& T, int k0, int maxsteps, double tol, double c
   T.beta = pb;
   HIPCK(hipMemsetAsync(T.col(T.Vb, cb), 0, dim * sizeof(V), st));  // v_{-1} = 0
   hipLaunchKernelGGL(k_hash_vec, dim3(grid_for(nd)), dim3(kBlock), 0, st, (double*)T.w, nd, seed);
+  if (hint)  // |hash|^2 ~ nd / 3 (uniform in [-1, 1)); the Ritz vector has unit norm
+    hipLaunchKernelGGL(k_mix_hint, dim3(grid_for(nd)), dim3(kBlock), 0, st, (double*)T.w,
+                       (const double*)T.col(T.Vb, ca), nd, sqrt((double)nd / 3.0));
   CK(T.orth(k0, T.w, -1));  // against the locked columns; the norm -> beta[m]
   hipLaunchKernelGGL(k_scale_into<VC>, dim3(grid_for(dim)), dim3(kBlock), 0, st, T.w, T.col(T.Vb, ca),
                      T.beta + T.m, dim);
@@ -2994,10 +3009,12 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
   int conv = 0;
   CK(trlan_core(T, 0, nev, maxit, tol, v0, 0, theta, Z, &conv));
   // Ritz vectors -> Vb[0, nev): the result vectors live there from here on
-  // (locked columns of the deflated solves)
+  // (locked columns of the deflated solves); with the probe also the next
+  // Ritz vector -> Vb[nev] (the screen's start hint)
   std::copy(Z.begin(), Z.begin() + (size_t)m * m, T.hp + 144);
   HIPCK(hipMemcpyAsync(T.Y, T.hp + 144, (size_t)m * m * sizeof(double), hipMemcpyHostToDevice, st));
-  CK(T.rotate(0, m, nev, g));
+  const bool hint = verify && conv == nev && nev + 1 < m && !(s->opts & ED_OPT_EIGH_NOHINT);
+  CK(T.rotate(0, m, hint ? nev + 1 : nev, g));
   std::vector<double> ev(theta.begin(), theta.begin() + nev);
   if (verify && conv == nev) {
     for (int round = 0; round < nev; round++) {
@@ -3021,7 +3038,7 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
         // runs only when it finds one or cannot decide
         int scr = -1;
         CK(probe_screen(T, nev, (int)std::min<int64_t>(dim - nev, kScreenMaxSteps), tprobe, cut, 3000 + round,
-                        &scr));
+                        &scr, hint && round == 0));
         if (scr == 0) break;
       }
       // the thick-restart probe at the full tolerance: its converged Ritz
@@ -3258,7 +3275,7 @@ static constexpr int32_t kOptKnown =
     ED_OPT_NO_PERSIST | ED_OPT_PERSIST_STORED | ED_OPT_NO_PREG | ED_OPT_NO_PKRON | ED_OPT_SPLIT_SIMPLE |
     ED_OPT_NO_BATCH | ED_OPT_EIGH_NO_VERIFY | ED_OPT_TRLAN_UNFUSED | ED_OPT_TRLAN_NOFOLD | ED_OPT_NO_GRAPH |
     ED_OPT_TRLAN_NOLOCAL | ED_OPT_TRLAN_NOSOLO | ED_OPT_TRLAN_FULLUPD | ED_OPT_STORED_EXACT |
-    ED_OPT_EIGH_FULLPROBE | ED_OPT_NO_FUSED;
+    ED_OPT_EIGH_FULLPROBE | ED_OPT_NO_FUSED | ED_OPT_EIGH_NOHINT;
 
 int ed_sector_set_options(ed_sector* s, int32_t opts) {
   if (!s) return fail(ED_ERR_ARG, "null");

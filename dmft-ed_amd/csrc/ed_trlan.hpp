@@ -260,6 +260,14 @@ __global__ void __launch_bounds__(kBlock) k_scale_into(const val_t<VC>* __restri
     y[i] = scl(inv, x[i]);
 }
 
+// w += a * x on the raw doubles (complex vectors as interleaved pairs): the
+// degeneracy screen's start vector, a hash vector plus the next Ritz vector
+__global__ void __launch_bounds__(kBlock) k_mix_hint(double* __restrict__ w, const double* __restrict__ x,
+                                                     int64_t nd, double a) {
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nd; i += (int64_t)gridDim.x * kBlock)
+    w[i] = w[i] + a * x[i];
+}
+
 // k_trl_coef + k_scale_into in one launch (grid-strided): every block forms
 // the same fixed-order sum of the norm partials; block 0 stores alpha/beta,
 // all blocks write out = x / ||x|| (zeros for a zero norm).

@@ -21,7 +21,7 @@ OPTIONS = {
     "split_simple": 0x020, "no_batch": 0x040, "eigh_no_verify": 0x080,
     "trlan_unfused": 0x100, "trlan_nofold": 0x200, "no_graph": 0x800,
     "trlan_nolocal": 0x1000, "trlan_nosolo": 0x2000, "trlan_fullupd": 0x4000,
-    "stored_exact": 0x100000, "eigh_fullprobe": 0x200000, "no_fused": 0x400000,
+    "stored_exact": 0x100000, "eigh_fullprobe": 0x200000, "no_fused": 0x400000, "eigh_nohint": 0x800000,
 }
 ED_OK = 0
 ERRORS = {1: "ED_ERR_ARG", 2: "ED_ERR_STATE", 3: "ED_ERR_HIP", 4: "ED_ERR_OOM",

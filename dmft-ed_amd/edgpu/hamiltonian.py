@@ -98,7 +98,7 @@ class Sector:
         """Select kernel alternatives by name (ED_OPT_*: no_persist,
         persist_stored, no_preg, no_pkron, split_simple, no_batch,
         eigh_no_verify, trlan_unfused, trlan_nofold, no_graph, trlan_nolocal,
-        trlan_nosolo, trlan_fullupd, stored_exact, eigh_fullprobe, no_fused;
+        trlan_nosolo, trlan_fullupd, stored_exact, eigh_fullprobe, no_fused, eigh_nohint;
         edgpu._lib.OPTIONS); no names
         restores the defaults."""
         bits = 0

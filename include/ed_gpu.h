@@ -93,6 +93,8 @@ extern "C" {
                                         bit-identical) even where the two-segment form is built */
 #define ED_OPT_NO_FUSED     0x400000 /* stored H·v: not the fused re-laid one-pass kernel (the
                                         two-segment form where built, else the one-pass one) */
+#define ED_OPT_EIGH_NOHINT  0x800000 /* eigh: degeneracy screen from a pure hash start (no next
+                                        Ritz vector mixed in) */
 #define ED_OPT_EIGH_FULLPROBE 0x200000 /* eigh: no plain-Lanczos screen before the thick-restart
                                           degeneracy probe (every probe round runs it in full) */
 
