@@ -2528,7 +2528,10 @@ struct Trlan {
   double2 *h = nullptr, *coef = nullptr, *part = nullptr, *part2 = nullptr;
   // grids up to this fold the coefficient reduction into the next CGS pass
   // (every block re-reads G x ncol partials; 0 with ED_OPT_TRLAN_NOFOLD: A/B)
-  int kFinFoldG = 128;
+#ifndef ED_FOLD_G
+#define ED_FOLD_G 128
+#endif
+  int kFinFoldG = ED_FOLD_G;
   bool graphs_on = true;  // false (ED_OPT_NO_GRAPH): sweeps launched directly
   bool solo = true;       // false (ED_OPT_TRLAN_NOSOLO): multi-kernel CGS on small sectors too (A/B)
   bool locupd = true;     // false (ED_OPT_TRLAN_FULLUPD): full CGS update every step (A/B)
@@ -2742,7 +2745,10 @@ static double* trlan_pinned() {
 }
 
 // blocks of the O(dim) Krylov sweeps
-static constexpr int kTrlanGridCap = 512;  // (1024 until round 4: 512 measured 13 % faster per large-sector solve, tools/trlan_ab.py --grid)
+#ifndef ED_TRLAN_GRIDCAP
+#define ED_TRLAN_GRIDCAP 512
+#endif
+static constexpr int kTrlanGridCap = ED_TRLAN_GRIDCAP;  // (1024 until round 4: 512 measured 13 % faster per large-sector solve, tools/trlan_ab.py --grid)
 // One thick-restart Lanczos solve on the columns [k0, m) of the basis; the
 // columns [0, k0) are locked (deflation: every new vector is orthogonalised
 // against them, their coefficients are not part of the projected matrix).

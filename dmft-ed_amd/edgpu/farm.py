@@ -49,12 +49,13 @@ def _dist():
 def sector_cost(cfg: EDConfig, sec: SectorId, opt: DiagOptions) -> float:
     """Work model in seconds of one MI355X: a fixed cost per sector (build,
     launches, host syncs) plus a part proportional to the H·v work.
-    Dense sectors: 2 ms + dim^3 x 1e-10 (LAPACK); Lanczos sectors: 6.7 ms +
-    9.8e-12 x Nitermax x dim x (1 + elements per row), elements/row ~ 1 +
+    Dense sectors: 2 ms + dim^3 x 1e-10 (LAPACK); Lanczos sectors: 7.0 ms +
+    9.1e-12 x Nitermax x dim x (1 + elements per row), elements/row ~ 1 +
     Norb*Nbath.  Least-squares fit to the 136 serial Lanczos sector times of
-    configs[3] (create + eigh + close; round 5 with the residual-interval
-    exit of the degeneracy screen: profiles/r5/farm_c4_serial_stats.json, the
-    first sector's one-off library warm-up left out; round 4: 8.0 ms +
+    configs[3] (create + eigh + close; round 6 with the converged-and-interval
+    screen seeded by the next Ritz vector: profiles/r6/farm_c4_serial_stats.json,
+    the first sector's one-off library warm-up left out; round 5: 6.7 ms +
+    9.8e-12 with the residual-interval exit; round 4: 8.0 ms +
     9.8e-12, earlier 8.5 ms + 1.18e-11, round 3: 9.4 ms + 1.13e-11, round 2:
     11.2 ms + 1.34e-11): small Lanczos sectors are dominated by the fixed
     part, which a purely proportional model gave to the ranks holding many
@@ -63,7 +64,7 @@ def sector_cost(cfg: EDConfig, sec: SectorId, opt: DiagOptions) -> float:
     if neigen == sec.dim or sec.dim <= max(opt.lanc_dim_threshold, opt.mpi_size):
         return 2e-3 + float(sec.dim) ** 3 * 1e-10
     per_row = 1.0 + cfg.Norb * cfg.Nbath
-    return 6.7e-3 + 9.78e-12 * float(nitermax) * sec.dim * per_row
+    return 7.0e-3 + 9.06e-12 * float(nitermax) * sec.dim * per_row
 
 
 def lpt_partition(costs: Sequence[float], nranks: int) -> List[List[int]]:

@@ -24,6 +24,7 @@ s=$(find "$OUT/st" -name "*kernel_stats.csv" | head -1)
 # grid 512 — apart from the batched ones of the same instantiation, whose
 # grids are K x 512: the runs split them)
 for e in "split|k_spmv_s[ab]<false, false" "spmv|k_spmv_pk<false, false" "spmv_cplx|k_spmv_pk<true, true" \
+         "fused_cplx|k_spmv_fu<true, true" "fused_cvec|k_spmv_fu<false, true" \
          "kron|k_kron_(up|dw)" "direct|k_direct<" "persist|k_lanc_persist<"; do
   IFS='|' read -r name pat <<< "$e"
   python3 "$R/tools/trace_summary.py" "$t" "$pat" 5 "$P/bench_trace_$name.json" \

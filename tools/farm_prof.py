@@ -36,7 +36,11 @@ ap.add_argument("--private-streams", action="store_true",
 ap.add_argument("--budget", type=float, default=None, help="DiagOptions.cache_budget_mb (default: the library default)")
 ap.add_argument("--timeline", default="", help="write per-sector (start, end, thread, dim) of the last rep")
 ap.add_argument("--maps", default="", help="write the process's shared-object mappings (for symbolising a crash)")
+ap.add_argument("--lib", default="", help="load this libedgpu.so build instead (A/B of kernel variants)")
 a = ap.parse_args()
+if a.lib:
+    import edgpu._lib as _edl  # noqa: E402
+    _edl.LIB_PATH = os.path.abspath(a.lib)
 cfg = c4_config(a.bath)
 opts = tuple(x for x in a.options.split(",") if x)
 

@@ -30,6 +30,8 @@ for v in $vars; do
   echo "=== $v rc=$rc" | tee -a "$SUM"
   grep -E "farm workers|c5 diag|Segmentation|signal|Error|error|Abort" "$OUT/fp_$v.log" | head -20 | tee -a "$SUM"
   tail -5 "$OUT/fp_$v.log" >> "$SUM"
+  t=$(find "$OUT/fp_$v" -name "*kernel_trace.csv" | head -1)
+  [ -n "$t" ] && python3 "$R/tools/timeline.py" "$t" "$OUT/fp_${v}_timeline.json" | tee -a "$SUM"
   find "$OUT/fp_$v" -name "*kernel_trace.csv" -size +2M -delete 2>/dev/null
   # after a crash, abort, time limit or kill: no further GPU work in this call
   if [ $rc -ne 0 ]; then exit $rc; fi
