@@ -194,7 +194,7 @@ def _global_queue(dist, n: int):
     next of n indices (0, 1, ...) or None.  One counter key per farm call
     (every rank makes the same sequence of farm_diag calls, so the keys
     agree); the store's add is atomic, each index goes to exactly one taker.
-    The key carries a token rank 0 draws and broadcasts per call, so a
+    The key carries a token rank 0 draws and all-reduces per call, so a
     counter left on the store by an earlier call or job attempt is never
     reused.  A barrier first, so no rank takes from the counter of a call the others
     have not reached.  Returns None when no store is reachable (every rank
@@ -206,18 +206,19 @@ def _global_queue(dist, n: int):
     import torch
 
     store = _queue_store(dist)
+    # [store reachable (MIN over ranks), rank 0's random token (the others add
+    # 0)]: a counter key no earlier call — nor an earlier incarnation of this
+    # job on the same store — can have used; one all_reduce per flag
     ok = torch.tensor([1 if store is not None else 0], dtype=torch.int64)
+    tok = torch.tensor([uuid.uuid4().int & ((1 << 62) - 1) if dist.get_rank() == 0 else 0], dtype=torch.int64)
     if dist.get_backend() == "nccl":
-        ok = ok.cuda()
+        ok, tok = ok.cuda(), tok.cuda()
     dist.all_reduce(ok, op=dist.ReduceOp.MIN)
     if int(ok.item()) == 0:
         return None
-    # a counter key no earlier call (nor an earlier incarnation of this job
-    # on the same store) can have used: rank 0's random token, broadcast
+    dist.all_reduce(tok, op=dist.ReduceOp.SUM)
     _QUEUE_CALLS[0] += 1
-    tok = [uuid.uuid4().hex if dist.get_rank() == 0 else None]
-    dist.broadcast_object_list(tok, src=0)
-    key = f"queue_{_QUEUE_CALLS[0]}_{tok[0]}"
+    key = f"queue_{_QUEUE_CALLS[0]}_{int(tok.item()):x}"
     dist.barrier()
     lock = threading.Lock()   # one store client per process: serialise its use
     done = [False]
