@@ -1555,12 +1555,12 @@ static int launch_split(ed_sector* s, const void* x, Epi epi, hipStream_t st) {
   }
 }
 
-// Fused one-pass re-laid stored H·v (ed_fused.hpp).  Grid: resident blocks,
-// a multiple of 8 (one unit range per XCD).
-// half the resident grid: 16 waves per CU keep the window of units an XCD
-// works on (and the neighbour V rows its cross-block gathers read) smaller —
-// N28 complex H 0.281 -> 0.269 ms, complex vectors on real H 0.275 -> 0.262,
-// N28 Jx/Jp real 0.239 -> 0.228; a quarter measured slower (gpurun_out r6f)
+// Fused one-pass re-laid stored H·v (ed_fused.hpp).  Grid: half the
+// resident blocks, a multiple of 8 (one unit range per XCD) — 16 waves per
+// CU keep the window of units an XCD works on (and the neighbour V rows its
+// cross-block gathers read) smaller than the full resident grid does: N28
+// complex H 0.281 -> 0.269 ms, complex vectors on real H 0.275 -> 0.262, N28
+// Jx/Jp real 0.239 -> 0.228; a quarter measured slower (gpurun_out r6f)
 #ifndef ED_FU_GRID_DIV
 #define ED_FU_GRID_DIV 2
 #endif
@@ -2528,10 +2528,9 @@ struct Trlan {
   double2 *h = nullptr, *coef = nullptr, *part = nullptr, *part2 = nullptr;
   // grids up to this fold the coefficient reduction into the next CGS pass
   // (every block re-reads G x ncol partials; 0 with ED_OPT_TRLAN_NOFOLD: A/B)
-#ifndef ED_FOLD_G
-#define ED_FOLD_G 128
-#endif
-  int kFinFoldG = ED_FOLD_G;
+  // (round 6, in the 8-worker farm: folding at 256 or 512 blocks, with the
+  // sweep grid at 512 or 256, within noise of this, gpurun_out r6k)
+  int kFinFoldG = 128;
   bool graphs_on = true;  // false (ED_OPT_NO_GRAPH): sweeps launched directly
   bool solo = true;       // false (ED_OPT_TRLAN_NOSOLO): multi-kernel CGS on small sectors too (A/B)
   bool locupd = true;     // false (ED_OPT_TRLAN_FULLUPD): full CGS update every step (A/B)
@@ -2745,10 +2744,10 @@ static double* trlan_pinned() {
 }
 
 // blocks of the O(dim) Krylov sweeps
-#ifndef ED_TRLAN_GRIDCAP
-#define ED_TRLAN_GRIDCAP 512
-#endif
-static constexpr int kTrlanGridCap = ED_TRLAN_GRIDCAP;  // (1024 until round 4: 512 measured 13 % faster per large-sector solve, tools/trlan_ab.py --grid)
+// (1024 until round 4: 512 measured 13 % faster per large-sector solve,
+// tools/trlan_ab.py --grid; round 6 in the 8-worker farm: 128 and 256 within
+// noise of 512, gpurun_out r6j)
+static constexpr int kTrlanGridCap = 512;
 // One thick-restart Lanczos solve on the columns [k0, m) of the basis; the
 // columns [0, k0) are locked (deflation: every new vector is orthogonalised
 // against them, their coefficients are not part of the projected matrix).
