@@ -2787,8 +2787,12 @@ static int trlan_core(Trlan<VC>& T, int k0, int nev, int maxit, double tol, cons
     int j0 = jstart;
     for (;;) {  // expansion j0..m-1, restarted past an invariant subspace
       CK(T.sweep(j0));
-      HIPCK(hipMemcpyAsync(hal, T.alpha, m * sizeof(double), hipMemcpyDeviceToHost, st));
-      HIPCK(hipMemcpyAsync(hbe, T.beta, m * sizeof(double), hipMemcpyDeviceToHost, st));
+      if (T.beta == T.alpha + (hbe - hal)) {
+        HIPCK(hipMemcpyAsync(hal, T.alpha, ((hbe - hal) + m) * sizeof(double), hipMemcpyDeviceToHost, st));
+      } else {
+        HIPCK(hipMemcpyAsync(hal, T.alpha, m * sizeof(double), hipMemcpyDeviceToHost, st));
+        HIPCK(hipMemcpyAsync(hbe, T.beta, m * sizeof(double), hipMemcpyDeviceToHost, st));
+      }
       HIPCK(hipStreamSynchronize(st));
       std::copy(hal, hal + m, al.begin());
       std::copy(hbe, hbe + m, be.begin());
@@ -3004,8 +3008,10 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
   CK(T.alloc((void**)&T.npA, (size_t)T.G * sizeof(double)));
   CK(T.alloc((void**)&T.npB, (size_t)T.G * sizeof(double)));
   CK(T.alloc((void**)&T.lof, sizeof(int)));
-  CK(T.alloc((void**)&T.alpha, (kTrlanMaxCols + 8) * sizeof(double)));
-  CK(T.alloc((void**)&T.beta, (kTrlanMaxCols + 8) * sizeof(double)));
+  // alpha | beta in one block laid out as the pinned staging (72 apart): one
+  // copy down per restart
+  CK(T.alloc((void**)&T.alpha, 2 * (kTrlanMaxCols + 8) * sizeof(double)));
+  T.beta = T.alpha + (kTrlanMaxCols + 8);
   CK(T.alloc((void**)&T.Y, (size_t)mcap * mcap * sizeof(double)));
   hipStream_t st = T.st;
   const int g = grid_for(dim);

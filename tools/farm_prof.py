@@ -36,6 +36,7 @@ ap.add_argument("--private-streams", action="store_true",
 ap.add_argument("--budget", type=float, default=None, help="DiagOptions.cache_budget_mb (default: the library default)")
 ap.add_argument("--timeline", default="", help="write per-sector (start, end, thread, dim) of the last rep")
 ap.add_argument("--maps", default="", help="write the process's shared-object mappings (for symbolising a crash)")
+ap.add_argument("--dim-range", default="", help="lo:hi — farm only the sectors with lo <= dim < hi (where the wall goes)")
 ap.add_argument("--lib", default="", help="load this libedgpu.so build instead (A/B of kernel variants)")
 a = ap.parse_args()
 if a.lib:
@@ -108,11 +109,17 @@ def timed_solver(cfg_, sec, opt_, device):
     return r
 
 
+subset = None
+if a.dim_range:
+    lo, hi = (float(x) if x else None for x in a.dim_range.split(":"))
+    subset = [s.isector for s in setup_pointers(cfg)
+              if (lo is None or s.dim >= lo) and (hi is None or s.dim < hi)]
+    print(f"dim range {a.dim_range}: {len(subset)} sectors", flush=True)
 for rep in range(a.reps):
     events.clear()
     torch.cuda.synchronize()
     t = time.perf_counter()
-    res = farm_diag(cfg, opt, solver=timed_solver)
+    res = farm_diag(cfg, opt, solver=timed_solver, sectors=subset)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t
     print(f"farm workers={a.workers} wall {wall:.4f} s states={res.states.size}", flush=True)
