@@ -54,6 +54,13 @@ class DiagOptions:
     # sectors solved concurrently on one GPU (host threads, one HIP stream per
     # sector; ctypes releases the GIL): small sectors are launch-latency bound
     workers: int = 8
+    # of those, this many take the smallest pending sector instead of the
+    # largest (single-rank schedule; at least one worker stays on the largest):
+    # the launch-latency-bound small sectors run beside the HBM-bound large
+    # ones instead of after them.  configs[3] on one MI355X, alternating runs:
+    # 6 → median 0.707 s, 0 (largest first for all) → 0.752 s; 2 or 4 within
+    # noise of 0 (gpurun_out r6sw*)
+    small_workers: int = 6
     # each worker thread keeps one HIP stream for every sector it solves
     # (False: every sector creates and destroys a private stream)
     worker_streams: bool = True
@@ -242,8 +249,9 @@ def working_set_bytes(cfg: EDConfig, sec: SectorId, opt: DiagOptions) -> float:
 def solve_many(cfg: EDConfig, secs: List[SectorId], opt: DiagOptions, device: int = 0,
                solver=None, cost=None, take_global=None) -> List[SectorResult]:
     """Solve a list of sectors on one GPU with `opt.workers` host threads,
-    largest first; results in the order of `secs` (each sector's result does
-    not depend on the schedule).  With `opt.cache_budget_mb` a worker takes
+    largest first (`opt.small_workers` of them smallest first); results in
+    the order of `secs` (each sector's result does not depend on the
+    schedule).  With `opt.cache_budget_mb` a worker takes
     the largest pending sector whose working set fits beside those in flight
     (a sector larger than the budget only when nothing else big runs), else
     waits for one to finish.
@@ -299,19 +307,21 @@ def solve_many(cfg: EDConfig, secs: List[SectorId], opt: DiagOptions, device: in
     used = [0.0]
     cv = threading.Condition()
 
-    def take() -> Optional[int]:
+    def take(small: bool) -> Optional[int]:
         with cv:
             while pending and not err:
-                for k, i in enumerate(pending):
+                ks = range(len(pending) - 1, -1, -1) if small else range(len(pending))
+                for k in ks:
+                    i = pending[k]
                     if ws[i] == 0.0 or used[0] + ws[i] <= budget or used[0] == 0.0:
                         used[0] += ws[i]
                         return pending.pop(k)
                 cv.wait()
             return None
 
-    def worker():
+    def worker(small: bool):
         while True:
-            i = take()
+            i = take(small)
             if i is None:
                 return
             try:
@@ -326,7 +336,9 @@ def solve_many(cfg: EDConfig, secs: List[SectorId], opt: DiagOptions, device: in
                         used[0] = 0.0
                     cv.notify_all()
 
-    threads = [threading.Thread(target=worker, daemon=True) for _ in range(min(opt.workers, len(secs)))]
+    nw = min(opt.workers, len(secs))
+    threads = [threading.Thread(target=worker, args=(w < min(opt.small_workers, nw - 1),), daemon=True)
+               for w in range(nw)]
     for t in threads:
         t.start()
     for t in threads:

@@ -65,6 +65,45 @@ def test_solve_many_cache_budget(budget_mb):
         assert max(n for _, n in peaks) > 1
 
 
+@pytest.mark.parametrize("small", [0, 2])
+def test_solve_many_small_workers(small):
+    """DiagOptions.small_workers: that many workers start from the cheapest
+    pending sector, the rest from the most expensive; results in input order
+    and each sector solved once either way."""
+    import threading
+    import time
+
+    from edgpu.diag import SectorResult, solve_many
+
+    cfg = make_config(Norb=2, Nbath=5)
+    opt = DiagOptions(workers=4, small_workers=small)
+    secs = setup_pointers(cfg)
+    cost = {s.isector: sector_cost(cfg, s, opt) for s in secs}
+    lock = threading.Lock()
+    started = []
+    gate = threading.Barrier(4)
+
+    def solver(c, sec, o, device):
+        with lock:
+            started.append(sec.isector)
+            first = len(started) <= 4
+        if first:
+            gate.wait(timeout=30)   # the four first picks are made before any finishes
+        time.sleep(2e-4)
+        return SectorResult(sec.isector, (sec.q1, sec.q2), sec.dim, np.zeros(1), 1)
+
+    out = solve_many(cfg, secs, opt, solver=solver, cost=lambda s: cost[s.isector])
+    assert [r.isector for r in out] == [s.isector for s in secs]
+    assert sorted(started) == sorted(s.isector for s in secs)
+    ranked = sorted(cost, key=lambda k: -cost[k])
+    first = set(started[:4])
+    assert set(ranked[:4 - small]) <= first
+    if small:
+        assert set(ranked[-small:]) <= first    # the cheapest ones start at once
+    else:
+        assert first == set(ranked[:4])
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))

@@ -37,6 +37,7 @@ ap.add_argument("--budget", type=float, default=None, help="DiagOptions.cache_bu
 ap.add_argument("--timeline", default="", help="write per-sector (start, end, thread, dim) of the last rep")
 ap.add_argument("--maps", default="", help="write the process's shared-object mappings (for symbolising a crash)")
 ap.add_argument("--dim-range", default="", help="lo:hi — farm only the sectors with lo <= dim < hi (where the wall goes)")
+ap.add_argument("--small-workers", type=int, default=None, help="DiagOptions.small_workers (default: the library's)")
 ap.add_argument("--lib", default="", help="load this libedgpu.so build instead (A/B of kernel variants)")
 a = ap.parse_args()
 if a.lib:
@@ -72,6 +73,8 @@ if a.serial_stats:
                        totals=tot, sectors=rows), f, indent=1)
 
 opt = DiagOptions(workers=a.workers, kernel_options=opts, worker_streams=not a.private_streams)
+if a.small_workers is not None:
+    opt.small_workers = a.small_workers
 if a.budget is not None:
     opt.cache_budget_mb = a.budget
 if a.maps:
