@@ -14,7 +14,9 @@ from edgpu.hamiltonian import Sector  # noqa: E402
 
 cfg = make_config(Norb=2, Nbath=5, bath="random", seed=20251015)
 q1, q2 = (int(sys.argv[1]), int(sys.argv[2])) if len(sys.argv) > 2 else (6, 6)
-with Sector(cfg, q1, q2, stored=True, real=True) as S:
+mf = os.environ.get("ED_FORM") == "direct"   # matrix-free H·v (the Kronecker two-pass form when the sector has it)
+with Sector(cfg, q1, q2, stored=not mf, direct=mf, real=True) as S:
+    print(f"form {'matrix-free' if mf else 'stored'} kron={S.info.kron}", flush=True)
     S.eigh(vectors=False)
     for _ in range(3):
         torch.cuda.synchronize(); t = time.perf_counter()

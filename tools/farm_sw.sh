@@ -1,6 +1,10 @@
-# farm A/B: small_workers 0 vs 6 (8 workers), alternating runs, 4 reps each
-mkdir -p gpurun_out/r6sw3
-for i in 1 2 3 4 5; do for sw in 0 6; do
-  echo "== small_workers $sw" >> gpurun_out/r6sw3/sw.log
-  timeout -k 10 150 python tools/farm_prof.py --reps 4 --small-workers $sw >> gpurun_out/r6sw3/sw.log 2>&1 || exit 1
+# farm A/B over (workers, small_workers[, cache_budget_mb]), alternating
+# configurations, 3 runs x 4 reps each:
+#   bash tools/farm_sw.sh OUTNAME "8 6" "8 0" "8 6 256" ...
+O=gpurun_out/$1; shift
+mkdir -p $O
+CFGS=("$@")
+for i in 1 2 3; do for c in "${CFGS[@]}"; do read -r w s b <<< "$c"
+  echo "== workers $w small_workers $s budget ${b:-default}" >> $O/sw.log
+  timeout -k 10 150 python tools/farm_prof.py --reps 4 --workers $w --small-workers $s ${b:+--budget $b} >> $O/sw.log 2>&1 || exit 1
 done; done
