@@ -16,7 +16,10 @@ cfg = make_config(Norb=2, Nbath=5, bath="random", seed=20251015)
 q1, q2 = (int(sys.argv[1]), int(sys.argv[2])) if len(sys.argv) > 2 else (6, 6)
 mf = os.environ.get("ED_FORM") == "direct"   # matrix-free H·v (the Kronecker two-pass form when the sector has it)
 with Sector(cfg, q1, q2, stored=not mf, direct=mf, real=True) as S:
-    print(f"form {'matrix-free' if mf else 'stored'} kron={S.info.kron}", flush=True)
+    opts = [o for o in os.environ.get("ED_OPTS", "").split(",") if o]   # ED_OPT_* names (A/B)
+    if opts:
+        S.set_options(*opts)
+    print(f"form {'matrix-free' if mf else 'stored'} kron={S.info.kron} options {opts}", flush=True)
     S.eigh(vectors=False)
     for _ in range(3):
         torch.cuda.synchronize(); t = time.perf_counter()
