@@ -20,6 +20,7 @@
 #include "ed_kernels.hpp"
 #include "ed_persist.hpp"
 #include "ed_trlan.hpp"
+#include "ed_trlbatch.hpp"
 #include "ed_fused.hpp"
 #include "ed_split.hpp"
 #include "ed_tables.hpp"
@@ -3088,6 +3089,319 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
   return ED_OK;
 }
 
+// ------------------------------------------- batched small-sector eigh
+// ed_sectors_eigh_batch: trlan_run's algorithm for many small stored sectors
+// at once (ed_trlbatch.hpp): every restart cycle of every sector still in its
+// main solve, and every 10-step chunk of every degeneracy screen, goes into
+// one k_trl_batch launch; the host runs trlan_core's / probe_screen's
+// decisions per sector on the mailbox values.  A sector the batch cannot
+// finish (an invariant Krylov subspace, a screen that finds an eigenvalue
+// below the cut or cannot decide, ED_OPT_EIGH_FULLPROBE) or cannot take
+// (complex, not stored, beyond kTbMaxDim rows or kTbMaxCols columns) is
+// solved afterwards by trlan_run on its own stream, from the same start.
+struct TbSec {
+  ed_sector* s = nullptr;
+  int64_t dim = 0;
+  int m = 0, it = 0, j0 = 0, conv = 0, nhv = 0;
+  int state = 0;  // 0 main solve, 1 screen, 2 final rotation pending, 3 done, 4 fall back
+  std::vector<double> Tm, theta, Z, ev, sal, sbe;
+  int maxsteps = 0, sk = 0;
+  double cut = 0.0, tprobe = 0.0;
+  bool hint = false;
+  TrlTask task{};
+  int ny = 0;  // next launch's rotation: the first ny entries of Z (ld m)
+};
+
+static double host_default_start(int64_t r) {  // k_default_start's value
+  uint64_t z = (uint64_t)(r + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z = z ^ (z >> 31);
+  return (double)(z >> 11) * (1.0 / 9007199254740992.0) * 2.0 - 1.0;
+}
+static char* tb_pinned(size_t n) {  // per host thread, grown on demand, kept
+  static thread_local char* buf = nullptr;
+  static thread_local size_t cap = 0;
+  if (n > cap) {
+    if (buf) (void)hipHostFree(buf);
+    buf = nullptr;
+    cap = 0;
+    if (hipHostMalloc((void**)&buf, n, hipHostMallocDefault) != hipSuccess) return nullptr;
+    cap = n;
+  }
+  return buf;
+}
+
+static bool tb_eligible(const ed_sector* s, int nev, int ncv) {
+  const int m = (int)std::min<int64_t>(ncv, s->dim);
+  return s && !s->hc && s->nrows == s->dim && s->row0 == 0 && resolve_path(s, -1) == 0 && s->d_sptr &&
+         s->d_diag && (s->d_words || (s->d_cols && s->d_vals)) && s->dim <= kTbMaxDim && m <= kTbMaxCols &&
+         nev >= 1 && nev < m && nev + 2 <= kTbMaxCols && s->dim > (int64_t)nev + 2 && s->nslice * 64 >= s->dim &&
+         // the multi-kernel A/B alternatives keep their own path
+         !(s->opts & (ED_OPT_TRLAN_UNFUSED | ED_OPT_TRLAN_NOLOCAL | ED_OPT_TRLAN_NOSOLO));
+}
+
+static int tb_run(ed_sector* const* secs, int n, int nev, int ncv, int maxit, double tol,
+                  const double* const* v0, double* evals, void* const* evecs, int32_t* nconv, int32_t* nhv,
+                  hipStream_t st, std::vector<int>& fallback) {
+  std::vector<TbSec> S;
+  std::vector<int> idx;
+  for (int i = 0; i < n; i++) {
+    if (!tb_eligible(secs[i], nev, ncv)) {
+      fallback.push_back(i);
+      continue;
+    }
+    TbSec b;
+    b.s = secs[i];
+    b.dim = secs[i]->dim;
+    b.m = (int)std::min<int64_t>(ncv, b.dim);
+    S.push_back(std::move(b));
+    idx.push_back(i);
+  }
+  const int ns = (int)S.size();
+  if (ns == 0) return ED_OK;
+  // device: per sector Vb (mcap columns) | w | alpha, beta (72 each) | pa, pb
+  // | coef | Y; the ws of all sectors contiguous (one start-vector upload),
+  // the mailboxes contiguous (one copy down per launch)
+  size_t nw = 0, per = 0;
+  std::vector<size_t> off(ns), woff(ns);
+  for (int k = 0; k < ns; k++) {
+    const int mcap = std::max(S[k].m, nev + 2);
+    woff[k] = nw;
+    nw += (size_t)S[k].dim;
+    off[k] = per;
+    per += (size_t)mcap * S[k].dim + 2 * 72 + 2 * kTbScreenLen + 2 * kTrlanMaxCols + kTbMaxCols * kTbMaxCols;
+  }
+  const size_t nmail = (size_t)ns * kTbMail;
+  const size_t ytot = (size_t)ns * kTbMaxCols * kTbMaxCols;  // rotations of one launch, packed
+  const size_t bytes = (per + nw + nmail + ytot) * sizeof(double) + (size_t)ns * sizeof(TrlTask);
+  char* dbase = nullptr;
+  HIPCK(hipMallocAsync((void**)&dbase, bytes, st));
+  struct Free {
+    char* p; hipStream_t s;
+    ~Free() { (void)hipFreeAsync(p, s); }
+  } free_guard{dbase, st};
+  double* const dsec = (double*)dbase;
+  double* const dw = dsec + per;
+  double* const dmail = dw + nw;
+  TrlTask* const dtask = (TrlTask*)(dmail + nmail);
+  // pinned: start vectors | mailboxes | tasks + rotations of one launch
+  // (the device mirrors the last part: [tasks | rotations packed])
+  const size_t hbytes = (nw + nmail + ytot) * sizeof(double) + (size_t)ns * sizeof(TrlTask);
+  char* hp = tb_pinned(hbytes);
+  if (!hp) return fail(ED_ERR_OOM, "pinned staging (batch eigh)");
+  double* const hv0 = (double*)hp;
+  double* const hmail = hv0 + nw;
+  TrlTask* const htask = (TrlTask*)(hmail + nmail);
+  for (int k = 0; k < ns; k++) {
+    TbSec& b = S[k];
+    const ed_sector* s = b.s;
+    double* p = dsec + off[k];
+    const int mcap = std::max(b.m, nev + 2);
+    TrlTask& t = b.task;
+    t.diag = (const double*)s->d_diag;
+    t.sptr = s->d_sptr;
+    t.words = s->d_words;
+    t.dict = (const double*)s->d_pdict;
+    t.cols = s->d_cols;
+    t.vals = (const double*)s->d_vals;
+    t.dim = b.dim;
+    t.Vb = p;
+    p += (size_t)mcap * b.dim;
+    t.alpha = p;
+    t.beta = p + 72;
+    p += 144;
+    t.pa = p;
+    t.pb = p + kTbScreenLen;
+    p += 2 * kTbScreenLen;
+    t.coef = (double2*)p;
+    p += 2 * kTrlanMaxCols;
+    t.Y = p;
+    t.w = dw + woff[k];
+    t.mail = dmail + (size_t)k * kTbMail;
+    t.m = b.m;
+    t.nev = nev;
+    t.locupd = !(s->opts & ED_OPT_TRLAN_FULLUPD);
+    t.op = kTbStart;
+    b.Tm.assign((size_t)b.m * b.m, 0.0);
+    const int i = idx[k];
+    if (v0 && v0[i]) memcpy(hv0 + woff[k], v0[i], b.dim * sizeof(double));
+    else
+      for (int64_t r = 0; r < b.dim; r++) hv0[woff[k] + r] = host_default_start(r);
+  }
+  HIPCK(hipMemcpyAsync(dw, hv0, nw * sizeof(double), hipMemcpyHostToDevice, st));
+  static std::once_flag lds_once;
+  static hipError_t lds_err = hipSuccess;
+  std::call_once(lds_once, [] {
+    lds_err = hipFuncSetAttribute((const void*)k_trl_batch, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)(kTbMaxDim * sizeof(double)));
+  });
+  HIPCK(lds_err);
+  std::vector<int> act;
+  for (;;) {
+    act.clear();
+    for (int k = 0; k < ns; k++)
+      if (S[k].state <= 2) act.push_back(k);
+    if (act.empty()) break;
+    // tasks and rotations of this launch (rotations packed, one copy up)
+    const int na = (int)act.size();
+    double* const hY = (double*)(htask + na);
+    const double* const dY = (const double*)(dtask + na);
+    size_t yo = 0;
+    int64_t maxdim = 0;
+    for (int a = 0; a < na; a++) {
+      TbSec& b = S[act[a]];
+      TrlTask t = b.task;
+      t.nrot = b.ny > 0 ? t.nrot : 0;
+      if (b.ny > 0) {
+        std::copy(b.Z.begin(), b.Z.begin() + b.ny, hY + yo);
+        t.Y = dY + yo;
+        yo += b.ny;
+      }
+      htask[a] = t;
+      maxdim = std::max(maxdim, b.dim);
+    }
+    HIPCK(hipMemcpyAsync(dtask, htask, na * sizeof(TrlTask) + yo * sizeof(double), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_trl_batch, dim3((unsigned)act.size()), dim3(kTbBlock), (size_t)maxdim * sizeof(double), st,
+                       (const TrlTask*)dtask);
+    HIPCK(hipGetLastError());
+    HIPCK(hipMemcpyAsync(hmail, dmail, nmail * sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPCK(hipStreamSynchronize(st));
+    for (int k : act) {
+      TbSec& b = S[k];
+      TrlTask& t = b.task;
+      const double* ml = hmail + (size_t)k * kTbMail;
+      const int m = b.m, ma = m;
+      b.ny = 0;
+      auto tm = [&](int i, int j) -> double& { return b.Tm[i + (size_t)ma * j]; };
+      if (b.state == 0) {  // a main sweep [j0, m) ran (trlan_core)
+        if (t.op == kTbStart && !(ml[64] > 0.0)) {
+          b.state = 4;
+          continue;
+        }
+        b.nhv += m - b.j0;
+        int jb = -1;
+        for (int j = b.j0; j < m; j++) {
+          tm(j, j) = ml[j];
+          if (j + 1 < ma) tm(j, j + 1) = tm(j + 1, j) = ml[32 + j];
+          const double scale = fabs(ml[j]) + (j > 0 ? fabs(tm(j - 1, j)) : 0.0) + 1e-300;
+          if (j + 1 < ma && ml[32 + j] < 1e-13 * scale) {
+            jb = j;
+            break;
+          }
+        }
+        if (jb >= 0) {  // invariant subspace: trlan_run continues from a random direction
+          b.state = 4;
+          continue;
+        }
+        const double beta = ml[32 + m - 1];
+        sym_eigh(ma, b.Tm, b.theta, b.Z);
+        const double eps23 = 3.6e-11;
+        b.conv = 0;
+        for (int i = 0; i < nev; i++)
+          if (fabs(beta * b.Z[(ma - 1) + (size_t)ma * i]) <= tol * std::max(eps23, fabs(b.theta[i]))) b.conv++;
+        if (b.conv == nev || b.it == maxit - 1 || m == b.dim) {
+          b.ev.assign(b.theta.begin(), b.theta.begin() + nev);
+          const int mp = (int)std::min<int64_t>(std::min(std::min(m, 20), kTrlanMaxCols - nev), b.dim - nev);
+          const bool verify = !(b.s->opts & ED_OPT_EIGH_NO_VERIFY) && mp >= 3 && b.conv == nev;
+          if (verify && (b.s->opts & ED_OPT_EIGH_FULLPROBE)) {
+            b.state = 4;
+            continue;
+          }
+          b.hint = verify && nev + 1 < m && !(b.s->opts & ED_OPT_EIGH_NOHINT);
+          const int nrot = b.hint ? nev + 1 : nev;
+          t.op = kTbScreen;
+          t.ldy = ma;
+          t.nrot = nrot;
+          b.ny = ma * nrot;
+          t.k0s = 0;
+          if (verify) {
+            b.state = 1;
+            b.maxsteps = (int)std::min<int64_t>(b.dim - nev, kScreenMaxSteps);
+            b.cut = b.ev[nev - 1] - kProbeMargin * std::max(1.0, fabs(b.ev[nev - 1]));
+            b.tprobe = std::max(tol, 1e-5);
+            t.k1 = std::min(b.maxsteps, kScreenChunk);
+            t.hint = b.hint ? 1 : 0;
+            t.seed = 3000;
+            b.sk = 0;
+            b.sal.clear();
+            b.sbe.clear();
+          } else {
+            b.state = 2;
+            t.k1 = 0;
+          }
+          continue;
+        }
+        // thick restart (trlan_core)
+        const int nkeep = std::max(nev, std::min(ma - 2, nev + (ma - nev) / 2));
+        t.op = kTbRestart;
+        t.ldy = ma;
+        t.nrot = nkeep;
+        b.ny = ma * nkeep;
+        std::fill(b.Tm.begin(), b.Tm.end(), 0.0);
+        for (int i = 0; i < nkeep; i++) {
+          tm(i, i) = b.theta[i];
+          tm(i, nkeep) = tm(nkeep, i) = beta * b.Z[(ma - 1) + (size_t)ma * i];
+        }
+        b.j0 = nkeep;
+        b.it++;
+        continue;
+      }
+      if (b.state == 2) {  // the final rotation ran: done
+        b.state = 3;
+        continue;
+      }
+      // a screen chunk [k0s, k1) ran (probe_screen)
+      const int nst = t.k1 - t.k0s;
+      b.nhv += nst;
+      for (int q = 0; q < nst; q++) {
+        b.sal.push_back(ml[q]);
+        b.sbe.push_back(ml[32 + q]);
+      }
+      t.nrot = 0;
+      const int K = (int)b.sal.size();
+      std::vector<double> ar(K), br(K, 0.0), E(K), z2(K), z1(K);
+      for (int i = 0; i < K; i++) ar[i] = b.sal[K - 1 - i];
+      for (int i = 1; i < K; i++) br[i] = b.sbe[K - 1 - i];
+      int dec = -1;
+      if (ed_tridiag_poles(K, ar.data(), br.data(), E.data(), z2.data(), z1.data()) == ED_OK) {
+        const double theta = E[0], resid = fabs(b.sbe[K - 1] * z1[0]);
+        if (theta < b.cut) dec = 1;
+        else {
+          const bool invariant = b.sbe[K - 1] < 1e-13 * (fabs(theta) + 1e-300);
+          const bool converged = resid <= b.tprobe * std::max(3.6e-11, fabs(theta));
+          if (invariant || (converged && theta - resid > b.cut)) dec = 0;
+        }
+      } else {
+        dec = 2;
+      }
+      if (dec == 0) b.state = 3;
+      else if (dec > 0 || t.k1 >= b.maxsteps) b.state = 4;
+      else {
+        t.k0s = t.k1;
+        t.k1 = std::min(b.maxsteps, t.k0s + kScreenChunk);
+      }
+    }
+  }
+  // results; fall-backs re-solved by the caller
+  for (int k = 0; k < ns; k++) {
+    TbSec& b = S[k];
+    const int i = idx[k];
+    if (b.state != 3) {
+      fallback.push_back(i);
+      if (nhv) nhv[i] = b.nhv;
+      continue;
+    }
+    for (int e = 0; e < nev; e++) evals[(size_t)i * nev + e] = b.ev[e];
+    if (evecs && evecs[i])
+      HIPCK(hipMemcpyAsync(evecs[i], b.task.Vb, (size_t)nev * b.dim * sizeof(double), hipMemcpyDefault, st));
+    if (nconv) nconv[i] = b.conv;
+    if (nhv) nhv[i] = b.nhv;
+  }
+  HIPCK(hipStreamSynchronize(st));
+  return ED_OK;
+}
+
 template <bool HC, bool VC>
 static int kron_split_launch(ed_sector* s, int part, int64_t o, int64_t n, const void* x, void* y, int acc,
                              hipStream_t st) {
@@ -3984,6 +4298,33 @@ int ed_sector_lanc_eigh(ed_sector* s, int32_t vtype, const void* v0, int32_t nit
     HIPCK(hipGetLastError());
     HIPCK(hipMemcpyAsync(vect, w.Y, s->dim * vs, hipMemcpyDefault, s->stream));
     HIPCK(hipStreamSynchronize(s->stream));
+  }
+  return ED_OK;
+}
+
+int ed_sectors_eigh_batch(ed_sector* const* secs, int32_t n, int32_t nev, int32_t ncv, int32_t maxit, double tol,
+                          const double* const* v0, double* evals, void* const* evecs, int32_t* nconv, int32_t* nhv,
+                          int32_t* nbatched, void* stream) {
+  if (!secs || n < 0 || !evals || maxit < 1) return fail(ED_ERR_ARG, "bad args");
+  if (n == 0) return ED_OK;
+  if (ncv > kTrlanMaxCols) return fail(ED_ERR_ARG, "ncv > 64 not supported");
+  for (int i = 0; i < n; i++) {
+    if (!secs[i]) return fail(ED_ERR_ARG, "null sector");
+    CK(whole_only(secs[i]));
+    if (secs[i]->hc) return fail(ED_ERR_ARG, "batched eigh: real vectors only (complex H needs vtype=1)");
+    if (secs[i]->device != secs[0]->device) return fail(ED_ERR_ARG, "batched eigh: sectors on different devices");
+  }
+  HIPCK(hipSetDevice(secs[0]->device));
+  hipStream_t st = stream ? (hipStream_t)stream : secs[0]->stream;
+  std::vector<int> fb;
+  CK(tb_run(secs, n, nev, ncv, maxit, tol, v0, evals, evecs, nconv, nhv, st, fb));
+  if (nbatched) *nbatched = n - (int)fb.size();
+  for (int i : fb) {
+    int32_t c = 0, h = 0;
+    CK(trlan_run<false>(secs[i], nev, ncv, maxit, tol, v0 ? v0[i] : nullptr, evals + (size_t)i * nev,
+                        evecs ? evecs[i] : nullptr, &c, &h));
+    if (nconv) nconv[i] = c;
+    if (nhv) nhv[i] += h;
   }
   return ED_OK;
 }

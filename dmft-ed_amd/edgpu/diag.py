@@ -16,7 +16,7 @@ eigenvalues, so a farmed run reproduces the serial list exactly.
 """
 from __future__ import annotations
 
-from dataclasses import dataclass, field
+from dataclasses import dataclass, field, replace
 from typing import Dict, Iterable, List, Optional, Tuple
 
 import numpy as np
@@ -73,6 +73,11 @@ class DiagOptions:
     # Cache instead of evicting each other to HBM; a sector larger than the
     # budget runs when nothing else big is in flight.  0: no limit.
     cache_budget_mb: float = 0.0
+    # thick-restart sectors of at most this many rows (real H, stored) are
+    # solved together by one host thread through ed_sectors_eigh_batch (one
+    # workgroup per sector, one launch per restart cycle for all of them)
+    # beside the other workers; 0: every sector alone (ed_sector_eigh)
+    batch_max_dim: int = 15360
     # multi-rank farms: "dynamic" — every rank's workers take the next sector
     # (largest cost first) from one global counter in the process group's
     # key-value store, so the ranks finish together whatever the cost
@@ -203,6 +208,50 @@ def solve_sector(cfg: EDConfig, sec: SectorId, opt: DiagOptions, device: int = 0
         return SectorResult(sec.isector, q, dim, w, neigen, v if opt.keep_vectors else None, "arpack")
 
 
+def batchable(cfg: EDConfig, sec: SectorId, opt: DiagOptions) -> bool:
+    """A sector `solve_batch` takes: thick-restart (arpack) path, real H,
+    at most opt.batch_max_dim rows, a Krylov basis of at most 32 columns."""
+    if opt.batch_max_dim <= 0 or opt.lanc_method != "arpack" or not cfg.is_real():
+        return False
+    neigen, _, nblock = lanczos_params(sec.dim, opt)
+    if neigen == sec.dim or sec.dim <= max(opt.lanc_dim_threshold, opt.mpi_size):
+        return False
+    ncv = min(max(nblock, neigen + 1), 64, sec.dim)
+    return sec.dim <= opt.batch_max_dim and ncv <= 32 and neigen + 2 <= 32
+
+
+def solve_batch(cfg: EDConfig, secs: List[SectorId], opt: DiagOptions, device: int = 0) -> List[SectorResult]:
+    """The arpack path of `solve_sector` for many small sectors at once
+    (ed_sectors_eigh_batch; the same start vector, Neigen, Nblock, Nitermax
+    and tolerance per sector, ED_DIAG.f90:88-167).  Results in `secs` order."""
+    from .hamiltonian import eigh_batch
+
+    st = _worker_stream(opt, device)
+    groups: Dict[Tuple[int, int, int], List[int]] = {}
+    for k, sec in enumerate(secs):
+        neigen, nitermax, nblock = lanczos_params(sec.dim, opt)
+        ncv = min(max(nblock, neigen + 1), 64, sec.dim)
+        groups.setdefault((neigen, ncv, max(nitermax, 10)), []).append(k)
+    out: List[Optional[SectorResult]] = [None] * len(secs)
+    for (neigen, ncv, maxit), ks in groups.items():
+        hs: List[Sector] = []
+        try:
+            for k in ks:
+                hs.append(Sector(cfg, secs[k].q1, secs[k].q2, stored=True, real=True, device=device,
+                                 options=opt.kernel_options, stream=st))
+            res, _ = eigh_batch(hs, neigen, ncv, maxit, opt.lanc_tolerance,
+                                [_start_vector(h.dim, False) for h in hs], vectors=opt.keep_vectors,
+                                on_device=opt.device_vectors, stream=st)
+        finally:
+            for h in hs:
+                h.close()
+        for k, (w, v, _, _) in zip(ks, res):
+            sec = secs[k]
+            out[k] = SectorResult(sec.isector, (sec.q1, sec.q2), sec.dim, w, neigen,
+                                  v if opt.keep_vectors else None, "arpack")
+    return out
+
+
 def state_list(results: Iterable[SectorResult], opt: DiagOptions) -> StateList:
     """T=0 state list, ED_DIAG.f90:224-235, replayed in isector order."""
     sl = StateList()
@@ -293,6 +342,21 @@ def solve_many(cfg: EDConfig, secs: List[SectorId], opt: DiagOptions, device: in
         if errs:
             raise errs[0]
         return out_g
+    if solver is solve_sector and opt.batch_max_dim > 0:
+        bidx = [i for i, s in enumerate(secs) if batchable(cfg, s, opt)]
+        if len(bidx) > 1:
+            bset = set(bidx)
+            ridx = [i for i in range(len(secs)) if i not in bset]
+            opt_nb = replace(opt, batch_max_dim=0)
+            rest, bres = with_batch(cfg, [secs[i] for i in bidx], opt, device,
+                                    lambda: solve_many(cfg, [secs[i] for i in ridx], opt_nb, device,
+                                                       solver=solver, cost=cost))
+            out_b: List[Optional[SectorResult]] = [None] * len(secs)
+            for i, r in zip(bidx, bres):
+                out_b[i] = r
+            for i, r in zip(ridx, rest):
+                out_b[i] = r
+            return out_b
     if opt.workers <= 1 or len(secs) <= 1:
         return [solver(cfg, sec, opt, device) for sec in secs]
 
@@ -346,6 +410,30 @@ def solve_many(cfg: EDConfig, secs: List[SectorId], opt: DiagOptions, device: in
     if err:
         raise err[0]
     return out
+
+
+def with_batch(cfg: EDConfig, bsecs: List[SectorId], opt: DiagOptions, device: int, fn):
+    """Run fn() (the other sectors' workers) while one more host thread
+    solves `bsecs` with solve_batch; returns (fn(), batch results)."""
+    import threading
+
+    box: List = [None, None]
+
+    def run():
+        try:
+            box[0] = solve_batch(cfg, bsecs, opt, device)
+        except BaseException as e:  # noqa: BLE001 - re-raised below
+            box[1] = e
+
+    th = threading.Thread(target=run, daemon=True)
+    th.start()
+    try:
+        rest = fn()
+    finally:
+        th.join()
+    if box[1] is not None:
+        raise box[1]
+    return rest, box[0]
 
 
 def ed_diag(cfg: EDConfig, opt: Optional[DiagOptions] = None,

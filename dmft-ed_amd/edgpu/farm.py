@@ -25,6 +25,7 @@ on the GPU box, gloo in the CPU tests).
 """
 from __future__ import annotations
 
+from dataclasses import replace
 from typing import Callable, Dict, List, Optional, Sequence
 
 import numpy as np
@@ -94,7 +95,7 @@ def farm_diag(cfg: EDConfig, opt: Optional[DiagOptions] = None, *, device: int =
               solver: Optional[Callable[[EDConfig, SectorId, DiagOptions, int], SectorResult]] = None
               ) -> FarmResult:
     """ed_diag over all ranks of the default process group (or serially)."""
-    from .diag import solve_many, solve_sector
+    from .diag import batchable, solve_many, solve_sector, with_batch
 
     opt = opt or DiagOptions()
     solver = solver or solve_sector
@@ -102,13 +103,36 @@ def farm_diag(cfg: EDConfig, opt: Optional[DiagOptions] = None, *, device: int =
     rank = dist.get_rank() if dist else 0
     world = dist.get_world_size() if dist else 1
     secs = [s for s in diag_sectors(cfg) if sectors is None or s.isector in set(sectors)]
-    costs = [sector_cost(cfg, s, opt) for s in secs]
     local: Dict[int, SectorResult] = {}
-    take = _global_queue(dist, len(secs)) if dist and world > 1 and opt.farm_schedule == "dynamic" else None
+    dynamic = bool(dist and world > 1 and opt.farm_schedule == "dynamic")
+    # dynamic queue: the small sectors solve_batch takes are dealt to the
+    # ranks up front (LPT on the cost model: the same on every rank), each
+    # rank's share in one batch beside its queue workers; the queue holds
+    # the others
+    bsecs: List[SectorId] = []
+    if dynamic and solver is solve_sector and opt.batch_max_dim > 0:
+        bsecs = [s for s in secs if batchable(cfg, s, opt)]
+        if len(bsecs) > 1:
+            bset = {s.isector for s in bsecs}
+            secs_q = [s for s in secs if s.isector not in bset]
+        else:
+            bsecs, secs_q = [], secs
+    else:
+        secs_q = secs
+    costs = [sector_cost(cfg, s, opt) for s in secs_q]
+    take = _global_queue(dist, len(secs_q)) if dynamic else None
     if take is not None:
-        order = sorted(range(len(secs)), key=lambda i: (-costs[i], i))   # the same on every rank
-        qsecs = [secs[i] for i in order]
-        for r in solve_many(cfg, qsecs, opt, device, solver=solver, take_global=take):
+        order = sorted(range(len(secs_q)), key=lambda i: (-costs[i], i))   # the same on every rank
+        qsecs = [secs_q[i] for i in order]
+        opt_q = replace(opt, batch_max_dim=0)
+        bparts = lpt_partition([sector_cost(cfg, s, opt) for s in bsecs], world)
+        mine_b = [bsecs[i] for i in bparts[rank]]
+        run_q = lambda: solve_many(cfg, qsecs, opt_q, device, solver=solver, take_global=take)  # noqa: E731
+        if len(mine_b) > 0:
+            rq, rb = with_batch(cfg, mine_b, opt, device, run_q)
+        else:
+            rq, rb = run_q(), []
+        for r in list(rq) + list(rb):
             if r is not None:
                 local[r.isector] = r
         assignment = None   # from the gathered tables below

@@ -274,6 +274,43 @@ class Sector:
         return vt, _ptr(arr)
 
 
+def eigh_batch(sectors, neigen: int = 6, ncv: int = 23, maxit: int = 512, tol: float = 1e-12,
+               v0s=None, vectors: bool = True, on_device: bool = False, stream=None):
+    """Sector.eigh (real vectors) for many sectors of one GPU at once
+    (ed_sectors_eigh_batch): the small stored sectors' restart cycles share
+    launches.  Returns one (eigenvalues, vectors (dim, neigen) or None, nconv,
+    H·v products) per sector, and the number finished inside the batch."""
+    n = len(sectors)
+    if n == 0:
+        return [], 0
+    lib = _lib.load()
+    hs = (ctypes.c_void_p * n)(*[s.handle for s in sectors])
+    keep = []
+    v0p = None
+    if v0s is not None:
+        v0p = (ctypes.c_void_p * n)()
+        for i, (s, v) in enumerate(zip(sectors, v0s)):
+            if v is None:
+                continue
+            a = np.ascontiguousarray(v, dtype=np.float64)
+            if a.shape != (s.dim,):
+                raise ValueError("start vector length != dim")
+            keep.append(a)
+            v0p[i] = a.ctypes.data
+    ev = np.zeros((n, neigen))
+    outs = [s._out_array((neigen, s.dim), 0, on_device) if vectors else None for s in sectors]
+    ep = (ctypes.c_void_p * n)(*[(o.ctypes.data if isinstance(o, np.ndarray) else o.data_ptr())
+                                 if o is not None else None for o in outs])
+    nconv = np.zeros(n, dtype=np.int32)
+    nhv = np.zeros(n, dtype=np.int32)
+    nb = ctypes.c_int32()
+    check(lib.ed_sectors_eigh_batch(hs, n, neigen, ncv, maxit, tol, v0p, _ptr(ev), ep, _ptr(nconv), _ptr(nhv),
+                                    ctypes.byref(nb), _stream_ptr(stream)), "ed_sectors_eigh_batch")
+    res = [(ev[i].copy(), outs[i].T if outs[i] is not None else None, int(nconv[i]), int(nhv[i]))
+           for i in range(n)]
+    return res, int(nb.value)
+
+
 # ------------------------------------------------------------ reference API
 _current: Optional[Sector] = None
 

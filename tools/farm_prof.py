@@ -38,6 +38,8 @@ ap.add_argument("--timeline", default="", help="write per-sector (start, end, th
 ap.add_argument("--maps", default="", help="write the process's shared-object mappings (for symbolising a crash)")
 ap.add_argument("--dim-range", default="", help="lo:hi — farm only the sectors with lo <= dim < hi (where the wall goes)")
 ap.add_argument("--small-workers", type=int, default=None, help="DiagOptions.small_workers (default: the library's)")
+ap.add_argument("--batch-max-dim", type=int, default=None,
+                help="DiagOptions.batch_max_dim (default: the library's; > 0 farms without the per-sector timeline)")
 ap.add_argument("--lib", default="", help="load this libedgpu.so build instead (A/B of kernel variants)")
 a = ap.parse_args()
 if a.lib:
@@ -77,6 +79,8 @@ if a.small_workers is not None:
     opt.small_workers = a.small_workers
 if a.budget is not None:
     opt.cache_budget_mb = a.budget
+if a.batch_max_dim is not None:
+    opt.batch_max_dim = a.batch_max_dim
 if a.maps:
     # every mapped shared object with its load base (the lowest start of its
     # mappings) and the executable segment (start, file offset): native crash
@@ -122,16 +126,20 @@ for rep in range(a.reps):
     events.clear()
     torch.cuda.synchronize()
     t = time.perf_counter()
-    res = farm_diag(cfg, opt, solver=timed_solver, sectors=subset)
+    # (the small-sector batch runs only with the library's own solver)
+    res = farm_diag(cfg, opt, solver=None if opt.batch_max_dim > 0 else timed_solver, sectors=subset)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t
-    print(f"farm workers={a.workers} wall {wall:.4f} s states={res.states.size}", flush=True)
+    print(f"farm workers={a.workers} batch_max_dim={opt.batch_max_dim} wall {wall:.4f} s "
+          f"states={res.states.size}", flush=True)
+    if not events:
+        continue
     busy = sum(e["t1"] - e["t0"] for e in events)
     first = min(e["t0"] for e in events) - t
     last = max(e["t1"] for e in events) - t
     print(f"  sector solves: sum {busy:.3f} s over {len(events)} (mean concurrency {busy / max(last - first, 1e-9):.2f}),"
           f" first start {first * 1e3:.1f} ms, last end {last * 1e3:.1f} ms", flush=True)
-if a.timeline:
+if a.timeline and events:
     t0 = min(e["t0"] for e in events)
     for e in events:
         e["t0"] = round(e["t0"] - t0, 6)
