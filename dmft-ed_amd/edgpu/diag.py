@@ -296,7 +296,7 @@ def working_set_bytes(cfg: EDConfig, sec: SectorId, opt: DiagOptions) -> float:
 
 
 def solve_many(cfg: EDConfig, secs: List[SectorId], opt: DiagOptions, device: int = 0,
-               solver=None, cost=None, take_global=None) -> List[SectorResult]:
+               solver=None, cost=None, take_global=None, batch_solver=None) -> List[SectorResult]:
     """Solve a list of sectors on one GPU with `opt.workers` host threads,
     largest first (`opt.small_workers` of them smallest first); results in
     the order of `secs` (each sector's result does not depend on the
@@ -310,8 +310,15 @@ def solve_many(cfg: EDConfig, secs: List[SectorId], opt: DiagOptions, device: in
     list then holds the sectors this process solved, None elsewhere.  The
     cache budget applies to the single-rank and LPT schedules only: a worker
     on the global queue takes the next index unconditionally (a warning says
-    so when a budget is set)."""
+    so when a budget is set).
+
+    batch_solver: solves the `batchable` sectors together in one more thread
+    beside the workers (default: solve_batch with the library's own solver;
+    opt.batch_max_dim = 0 turns it off); not on the multi-rank queue, where
+    farm_diag deals the batchable sectors to the ranks itself."""
     solver = solver or solve_sector
+    if batch_solver is None and solver is solve_sector:
+        batch_solver = solve_batch
     import threading
 
     if take_global is not None:
@@ -342,7 +349,7 @@ def solve_many(cfg: EDConfig, secs: List[SectorId], opt: DiagOptions, device: in
         if errs:
             raise errs[0]
         return out_g
-    if solver is solve_sector and opt.batch_max_dim > 0:
+    if batch_solver is not None and opt.batch_max_dim > 0 and take_global is None:
         bidx = [i for i, s in enumerate(secs) if batchable(cfg, s, opt)]
         if len(bidx) > 1:
             bset = set(bidx)
@@ -350,7 +357,7 @@ def solve_many(cfg: EDConfig, secs: List[SectorId], opt: DiagOptions, device: in
             opt_nb = replace(opt, batch_max_dim=0)
             rest, bres = with_batch(cfg, [secs[i] for i in bidx], opt, device,
                                     lambda: solve_many(cfg, [secs[i] for i in ridx], opt_nb, device,
-                                                       solver=solver, cost=cost))
+                                                       solver=solver, cost=cost), batch_solver)
             out_b: List[Optional[SectorResult]] = [None] * len(secs)
             for i, r in zip(bidx, bres):
                 out_b[i] = r
@@ -412,16 +419,18 @@ def solve_many(cfg: EDConfig, secs: List[SectorId], opt: DiagOptions, device: in
     return out
 
 
-def with_batch(cfg: EDConfig, bsecs: List[SectorId], opt: DiagOptions, device: int, fn):
+def with_batch(cfg: EDConfig, bsecs: List[SectorId], opt: DiagOptions, device: int, fn, batch_solver=None):
     """Run fn() (the other sectors' workers) while one more host thread
-    solves `bsecs` with solve_batch; returns (fn(), batch results)."""
+    solves `bsecs` with batch_solver (solve_batch); returns (fn(), batch
+    results)."""
     import threading
 
+    batch_solver = batch_solver or solve_batch
     box: List = [None, None]
 
     def run():
         try:
-            box[0] = solve_batch(cfg, bsecs, opt, device)
+            box[0] = batch_solver(cfg, bsecs, opt, device)
         except BaseException as e:  # noqa: BLE001 - re-raised below
             box[1] = e
 

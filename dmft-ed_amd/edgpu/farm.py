@@ -92,13 +92,19 @@ class FarmResult:
 
 def farm_diag(cfg: EDConfig, opt: Optional[DiagOptions] = None, *, device: int = 0,
               sectors: Optional[Sequence[int]] = None,
-              solver: Optional[Callable[[EDConfig, SectorId, DiagOptions, int], SectorResult]] = None
+              solver: Optional[Callable[[EDConfig, SectorId, DiagOptions, int], SectorResult]] = None,
+              batch_solver: Optional[Callable[[EDConfig, List[SectorId], DiagOptions, int], List[SectorResult]]] = None
               ) -> FarmResult:
-    """ed_diag over all ranks of the default process group (or serially)."""
-    from .diag import batchable, solve_many, solve_sector, with_batch
+    """ed_diag over all ranks of the default process group (or serially).
+    solver: one sector's solve (default solve_sector); batch_solver: the
+    `batchable` small sectors' joint solve (default solve_batch with the
+    default solver, none with another solver unless given)."""
+    from .diag import batchable, solve_batch, solve_many, solve_sector, with_batch
 
     opt = opt or DiagOptions()
     solver = solver or solve_sector
+    if batch_solver is None and solver is solve_sector:
+        batch_solver = solve_batch
     dist = _dist()
     rank = dist.get_rank() if dist else 0
     world = dist.get_world_size() if dist else 1
@@ -110,7 +116,7 @@ def farm_diag(cfg: EDConfig, opt: Optional[DiagOptions] = None, *, device: int =
     # rank's share in one batch beside its queue workers; the queue holds
     # the others
     bsecs: List[SectorId] = []
-    if dynamic and solver is solve_sector and opt.batch_max_dim > 0:
+    if dynamic and batch_solver is not None and opt.batch_max_dim > 0:
         bsecs = [s for s in secs if batchable(cfg, s, opt)]
         if len(bsecs) > 1:
             bset = {s.isector for s in bsecs}
@@ -129,7 +135,7 @@ def farm_diag(cfg: EDConfig, opt: Optional[DiagOptions] = None, *, device: int =
         mine_b = [bsecs[i] for i in bparts[rank]]
         run_q = lambda: solve_many(cfg, qsecs, opt_q, device, solver=solver, take_global=take)  # noqa: E731
         if len(mine_b) > 0:
-            rq, rb = with_batch(cfg, mine_b, opt, device, run_q)
+            rq, rb = with_batch(cfg, mine_b, opt, device, run_q, batch_solver)
         else:
             rq, rb = run_q(), []
         for r in list(rq) + list(rb):
@@ -140,7 +146,8 @@ def farm_diag(cfg: EDConfig, opt: Optional[DiagOptions] = None, *, device: int =
         parts = lpt_partition(costs, world)
         assignment = [[secs[i].isector for i in p] for p in parts]
         mine = [secs[i] for i in parts[rank]]
-        for r in solve_many(cfg, mine, opt, device, solver=solver, cost=lambda s: sector_cost(cfg, s, opt)):
+        for r in solve_many(cfg, mine, opt, device, solver=solver, cost=lambda s: sector_cost(cfg, s, opt),
+                            batch_solver=batch_solver):
             local[r.isector] = r
     # gather eigenvalues (tiny) from every rank
     mine = {k: (v.q, v.dim, v.neigen, np.asarray(v.eigenvalues[: max(v.neigen, 1)])) for k, v in local.items()}

@@ -110,7 +110,19 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, q, cfg_kw, method, schedule="dynamic", init="env"):
+def _oracle_batch(cfg, secs, opt, device):
+    """Stand-in for solve_batch on CPU: the oracle solver per sector, tagged."""
+    from oracle_solver import solve_sector_oracle
+
+    out = []
+    for s in secs:
+        r = solve_sector_oracle(cfg, s, opt, device)
+        r.method = "batch"
+        out.append(r)
+    return out
+
+
+def _worker(rank, world, port, q, cfg_kw, method, schedule="dynamic", init="env", batch=False):
     import torch.distributed as dist
     from oracle_solver import solve_sector_oracle
     from edgpu.farm import QUEUE_FALLBACK, broadcast_vector
@@ -135,7 +147,8 @@ def _worker(rank, world, port, q, cfg_kw, method, schedule="dynamic", init="env"
             for k in range(1, 4):
                 old.add(f"queue_{k}", 10_000)
         dist.barrier()
-    res = farm_diag(cfg, DiagOptions(lanc_method=method, farm_schedule=schedule), solver=solve_sector_oracle)
+    res = farm_diag(cfg, DiagOptions(lanc_method=method, farm_schedule=schedule), solver=solve_sector_oracle,
+                    batch_solver=_oracle_batch if batch else None)
     if init == "stale":   # a second farm call in the same job takes a fresh counter too
         res = farm_diag(cfg, DiagOptions(lanc_method=method, farm_schedule=schedule), solver=solve_sector_oracle)
     gs_owner = res.owners[0]
@@ -143,16 +156,17 @@ def _worker(rank, world, port, q, cfg_kw, method, schedule="dynamic", init="env"
     dim = [s for s in setup_pointers(cfg) if s.isector == res.states.sectors[0]][0].dim
     vb = broadcast_vector(v, gs_owner, dim, cplx=True)
     q.put((rank, res.states.energies, res.states.sectors, res.owners, res.assignment,
-           float(np.linalg.norm(vb)), list(QUEUE_FALLBACK)))
+           float(np.linalg.norm(vb)), list(QUEUE_FALLBACK),
+           sorted(k for k, r in res.local.items() if r.method == "batch")))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def _run_ranks(world, cfg_kw, method, schedule, init="env"):
+def _run_ranks(world, cfg_kw, method, schedule, init="env", batch=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, cfg_kw, method, schedule, init))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, cfg_kw, method, schedule, init, batch))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -178,7 +192,7 @@ def test_gloo_dynamic_queue(world, init, tmp_path):
     serial = farm_diag(cfg, DiagOptions(lanc_method=method), solver=solve_sector_oracle)
     init_arg = init if init in ("env", "stale") else f"file://{tmp_path}/rdzv"
     out = _run_ranks(world, cfg_kw, method, "dynamic", init_arg)
-    for rank, en, secs, owners, assignment, vnorm, fallback in out:
+    for rank, en, secs, owners, assignment, vnorm, fallback, _ in out:
         assert secs == serial.states.sectors
         np.testing.assert_allclose(en, serial.states.energies, rtol=0, atol=1e-12)
         assert abs(vnorm - 1.0) < 1e-10
@@ -205,7 +219,7 @@ def test_gloo_farm_matches_serial(cfg_kw, method, schedule):
     cfg = make_config(**cfg_kw)
     serial = farm_diag(cfg, DiagOptions(lanc_method=method), solver=solve_sector_oracle)
     out = _run_ranks(2, cfg_kw, method, schedule)
-    for rank, en, secs, owners, assignment, vnorm, fallback in out:
+    for rank, en, secs, owners, assignment, vnorm, fallback, _ in out:
         assert fallback == []
         assert secs == serial.states.sectors
         np.testing.assert_allclose(en, serial.states.energies, rtol=0, atol=1e-12)
@@ -216,6 +230,33 @@ def test_gloo_farm_matches_serial(cfg_kw, method, schedule):
     assert out[1][4] == assign
     if schedule == "lpt":
         assert all(len(a) > 0 for a in assign)
+    assert sorted(i for a in assign for i in a) == sorted(s.isector for s in setup_pointers(cfg))
+
+
+@pytest.mark.parametrize("schedule", ["dynamic", "lpt"])
+def test_gloo_farm_with_batch(schedule):
+    """Two ranks with the small-sector batch (a CPU stand-in batch solver):
+    the dynamic queue deals the batchable sectors to the ranks up front (LPT
+    on the cost model) and queues the others; the LPT schedule batches each
+    rank's share beside its workers.  Every sector solved exactly once, the
+    serial state list reproduced, both ranks batched some sectors."""
+    from oracle_solver import solve_sector_oracle
+
+    from edgpu.diag import batchable
+
+    cfg_kw, method = dict(Norb=1, Nbath=5), "arpack"
+    cfg = make_config(**cfg_kw)
+    opt = DiagOptions(lanc_method=method)
+    nb = sum(1 for s in setup_pointers(cfg) if batchable(cfg, s, opt))
+    assert nb >= 4
+    serial = farm_diag(cfg, opt, solver=solve_sector_oracle)
+    out = _run_ranks(2, cfg_kw, method, schedule, batch=True)
+    for rank, en, secs, owners, assignment, vnorm, fallback, batched in out:
+        assert secs == serial.states.sectors
+        np.testing.assert_allclose(en, serial.states.energies, rtol=0, atol=1e-12)
+        assert len(batched) > 0
+    assert sum(len(o[7]) for o in out) == nb
+    assign = out[0][4]
     assert sorted(i for a in assign for i in a) == sorted(s.isector for s in setup_pointers(cfg))
 
 
