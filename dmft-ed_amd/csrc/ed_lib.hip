@@ -3233,8 +3233,11 @@ static int tb_run(ed_sector* const* secs, int n, int nev, int ncv, int maxit, do
   static std::once_flag lds_once;
   static hipError_t lds_err = hipSuccess;
   std::call_once(lds_once, [] {
-    lds_err = hipFuncSetAttribute((const void*)k_trl_batch, hipFuncAttributeMaxDynamicSharedMemorySize,
+    lds_err = hipFuncSetAttribute((const void*)k_trl_batch<24>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)(kTbMaxDim * sizeof(double)));
+    if (lds_err == hipSuccess)
+      lds_err = hipFuncSetAttribute((const void*)k_trl_batch<32>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)(kTbMaxDim * sizeof(double)));
   });
   HIPCK(lds_err);
   std::vector<int> act;
@@ -3249,6 +3252,7 @@ static int tb_run(ed_sector* const* secs, int n, int nev, int ncv, int maxit, do
     const double* const dY = (const double*)(dtask + na);
     size_t yo = 0;
     int64_t maxdim = 0;
+    int maxm = 0;
     for (int a = 0; a < na; a++) {
       TbSec& b = S[act[a]];
       TrlTask t = b.task;
@@ -3260,10 +3264,15 @@ static int tb_run(ed_sector* const* secs, int n, int nev, int ncv, int maxit, do
       }
       htask[a] = t;
       maxdim = std::max(maxdim, b.dim);
+      maxm = std::max(maxm, std::max(b.m, nev + 2));
     }
     HIPCK(hipMemcpyAsync(dtask, htask, na * sizeof(TrlTask) + yo * sizeof(double), hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(k_trl_batch, dim3((unsigned)act.size()), dim3(kTbBlock), (size_t)maxdim * sizeof(double), st,
-                       (const TrlTask*)dtask);
+    if (maxm <= 24)
+      hipLaunchKernelGGL(k_trl_batch<24>, dim3((unsigned)na), dim3(kTbBlock), (size_t)maxdim * sizeof(double), st,
+                         (const TrlTask*)dtask);
+    else
+      hipLaunchKernelGGL(k_trl_batch<32>, dim3((unsigned)na), dim3(kTbBlock), (size_t)maxdim * sizeof(double), st,
+                         (const TrlTask*)dtask);
     HIPCK(hipGetLastError());
     HIPCK(hipMemcpyAsync(hmail, dmail, nmail * sizeof(double), hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));

@@ -493,7 +493,25 @@ __global__ void __launch_bounds__(kBlock) k_cgs(const val_t<VC>* __restrict__ V,
 constexpr int kOrthSoloBlock = 512;
 constexpr int64_t kOrthSoloMaxDim = 2048;  // measured: dim 2,640 35 us per step solo, 31 multi-kernel
 
-template <bool VC, int NC>
+// Global-address-space view of a pointer: loads through it are global_load,
+// not flat (a flat load also counts against lgkmcnt and waits behind LDS
+// traffic).  A no-op for kernel arguments; for pointers read from memory
+// (k_trl_batch's task table) the compiler cannot infer it by itself.
+template <class T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* gptr(T* p) {
+  return (__attribute__((address_space(1))) T*)p;
+}
+
+// (real vectors only: a class type such as double2 cannot be copied out of
+// an address-space-qualified lvalue; the complex callers pass kernel
+// arguments, which the compiler already knows to be global)
+template <bool VC, class T>
+__device__ __forceinline__ auto gptr_real(T* p) {
+  if constexpr (VC) return p;
+  else return gptr(p);
+}
+
+template <bool VC, int NC, int RU = 1>
 __device__ __forceinline__ void orth_solo_body(const val_t<VC>* __restrict__ V, int ncol,
                                                val_t<VC>* __restrict__ x, int64_t dim,
                                                double2* __restrict__ coef, double* __restrict__ alpha,
@@ -501,7 +519,9 @@ __device__ __forceinline__ void orth_solo_body(const val_t<VC>* __restrict__ V, 
                                                val_t<VC>* __restrict__ out, int shifted, int locupd,
                                                int jc = -1) {
   using Vt = val_t<VC>;
-  if (jc < 0) jc = jn;  // basis column of v_j (alpha slot jn)
+  if (jc < 0) jc = jn;
+  const auto Vg = gptr_real<VC>(V);
+  const auto xg = gptr_real<VC>(x);  // basis column of v_j (alpha slot jn)
   constexpr int NT = kOrthSoloBlock, NW = NT / 64;
   constexpr int NR = (VC ? 2 * NC : NC) + 1;  // partial slots: re[NC] | im[NC] | norm
   __shared__ double red[NW][NR];
@@ -553,14 +573,9 @@ __device__ __forceinline__ void orth_solo_body(const val_t<VC>* __restrict__ V, 
       if constexpr (VC) aim[c] = 0.0;
     }
   };
-  // x -= V[:, c0:ncol] h (h in LDS); optional dots of the result; returns |x|^2 partial
-  auto pass = [&](const double2* h, bool dots, int c0) {
-    double n2 = 0.0;
-    for (int64_t i = t; i < dim; i += NT) {
-      Vt v[NC];
-#pragma unroll
-      for (int c = 0; c < NC; c++) v[c] = (c >= c0 && c < ncol) ? V[(int64_t)c * dim + i] : vzero<Vt>();
-      Vt xi = x[i];
+  // one row: x_i -= V_i h (written back), dots, |x_i|^2
+  auto row = [&](const Vt (&v)[NC], Vt xi, int64_t i, const double2* h, bool dots, int c0, double& n2) {
+    {
       if (h) {
 #pragma unroll
         for (int c = 0; c < NC; c++) {
@@ -572,7 +587,7 @@ __device__ __forceinline__ void orth_solo_body(const val_t<VC>* __restrict__ V, 
             xi -= v[c] * h[c].x;
           }
         }
-        x[i] = xi;
+        xg[i] = xi;
       }
       if (dots) {
 #pragma unroll
@@ -584,8 +599,35 @@ __device__ __forceinline__ void orth_solo_body(const val_t<VC>* __restrict__ V, 
       }
       n2 += redot(xi, xi);
     }
-    return n2;
   };
+  auto pass = [&](const double2* h, bool dots, int c0) {
+    double n2 = 0.0;
+    int64_t i = t;
+    if constexpr (RU == 2) {
+      // two rows' loads in flight before either is used (one workgroup on a
+      // few thousand rows is bound by the load latency of each row); rows
+      // still processed in order, so the sums are those of the plain loop
+      for (; i + NT < dim; i += 2 * NT) {
+        Vt va[NC], vb[NC];
+#pragma unroll
+        for (int c = 0; c < NC; c++) {
+          const bool on = c >= c0 && c < ncol;
+          va[c] = on ? Vg[(int64_t)c * dim + i] : vzero<Vt>();
+          vb[c] = on ? Vg[(int64_t)c * dim + i + NT] : vzero<Vt>();
+        }
+        const Vt xa = xg[i], xb = xg[i + NT];
+        row(va, xa, i, h, dots, c0, n2);
+        row(vb, xb, i + NT, h, dots, c0, n2);
+      }
+    }
+    for (; i < dim; i += NT) {
+      Vt v[NC];
+#pragma unroll
+      for (int c = 0; c < NC; c++) v[c] = (c >= c0 && c < ncol) ? Vg[(int64_t)c * dim + i] : vzero<Vt>();
+      row(v, xg[i], i, h, dots, c0, n2);
+    }
+    return n2;
+  };  // x -= V[:, c0:ncol] h (h in LDS); optional dots of the result; returns |x|^2 partial
   // pass 1: h1 = V^H x, |x|^2
   zero();
   reduce(ncol, pass(nullptr, true, 0));
@@ -616,7 +658,8 @@ __device__ __forceinline__ void orth_solo_body(const val_t<VC>* __restrict__ V, 
   if (t == 0) beta[jslot] = b;
   if (out) {
     const double inv = b > 0.0 ? 1.0 / b : 0.0;
-    for (int64_t i = t; i < dim; i += NT) out[i] = scl(inv, x[i]);
+    const auto og = gptr_real<VC>(out);
+    for (int64_t i = t; i < dim; i += NT) og[i] = scl(inv, xg[i]);
   }
 }
 

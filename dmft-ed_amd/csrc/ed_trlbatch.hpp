@@ -70,28 +70,22 @@ __device__ __forceinline__ double tb_hash(int64_t i, uint64_t seed) {  // k_hash
   return (double)(z >> 11) * (1.0 / 9007199254740992.0) * 2.0 - 1.0;
 }
 
-// orth_solo_body with the column group chosen at run time (block-uniform)
-__device__ __forceinline__ void tb_orth(const double* V, int ncol, double* x, int64_t dim, double2* coef,
-                                        double* alpha, double* beta, int jn, int jslot, double* out,
-                                        int shifted, int locupd, int jc = -1) {
-  if (ncol <= 8) orth_solo_body<false, 8>(V, ncol, x, dim, coef, alpha, beta, jn, jslot, out, shifted, locupd, jc);
-  else if (ncol <= 16) orth_solo_body<false, 16>(V, ncol, x, dim, coef, alpha, beta, jn, jslot, out, shifted, locupd, jc);
-  else if (ncol <= 24) orth_solo_body<false, 24>(V, ncol, x, dim, coef, alpha, beta, jn, jslot, out, shifted, locupd, jc);
-  else orth_solo_body<false, 32>(V, ncol, x, dim, coef, alpha, beta, jn, jslot, out, shifted, locupd, jc);
-}
-
 // w = H v (v staged in LDS vl); shifted: w = (H - sg) v - bp vprev.  Row
 // sums in slot order, diagonal first (k_step_solo / k_spmv_pk).
 __device__ __forceinline__ void tb_hxv(const TrlTask& a, const double* vl, const double* sdict, double* x,
                                        const double* vprev, double sg, double bp, bool shifted) {
   const int t = threadIdx.x;
+  const auto sptr = gptr(a.sptr);
+  const auto diag = gptr(a.diag);
+  const auto xg = gptr(x);
+  const auto pg = gptr(vprev);
   for (int64_t i = t; i < a.dim; i += kTbBlock) {
-    const int64_t sl = i >> 6, s0 = a.sptr[sl];
-    const int w = (int)((a.sptr[sl + 1] - s0) >> 6);
+    const int64_t sl = i >> 6, s0 = sptr[sl];
+    const int w = (int)((sptr[sl + 1] - s0) >> 6);
     const double xi = vl[i];
-    double acc = 0.0 + a.diag[i] * xi;
+    double acc = 0.0 + diag[i] * xi;
     if (a.words) {
-      const uint32_t* wp = a.words + s0 + (i & 63);
+      const auto wp = gptr(a.words) + s0 + (i & 63);
       for (int k0 = 0; k0 < w; k0 += kChunk) {
         uint32_t c[kChunk];
 #pragma unroll
@@ -101,8 +95,8 @@ __device__ __forceinline__ void tb_hxv(const TrlTask& a, const double* vl, const
           if (k0 + k < w) acc = acc + sdict[c[k] >> kPackShift] * vl[c[k] & kPackColMask];
       }
     } else {
-      const int32_t* cp = a.cols + s0 + (i & 63);
-      const double* hp = a.vals + s0 + (i & 63);
+      const auto cp = gptr(a.cols) + s0 + (i & 63);
+      const auto hp = gptr(a.vals) + s0 + (i & 63);
       for (int k0 = 0; k0 < w; k0 += kChunk) {
         int32_t c[kChunk];
         double h[kChunk];
@@ -115,27 +109,30 @@ __device__ __forceinline__ void tb_hxv(const TrlTask& a, const double* vl, const
           if (k0 + k < w) acc = acc + h[k] * vl[c[k]];
       }
     }
-    x[i] = shifted ? (acc - sg * xi) - bp * vprev[i] : acc;
+    xg[i] = shifted ? (acc - sg * xi) - bp * pg[i] : acc;
   }
 }
 
 // V[:, :nout] = V[:, :ncol] Y (Y ncol x nout, column-major, in LDS), in
 // place row by row (k_rotate_ip's order); with scale_col >= 0 also
 // V[:, scale_col] = w * inv
+template <int NC>
 __device__ __forceinline__ void tb_rotate(double* Vb, int64_t dim, const double* ys, int ncol, int nout,
                                           const double* w, int scale_col, double inv) {
+  const auto Vg = gptr(Vb);
+  const auto wg = gptr(w);
   for (int64_t i = threadIdx.x; i < dim; i += kTbBlock) {
-    double v[kTbMaxCols];
+    double v[NC];
 #pragma unroll
-    for (int c = 0; c < kTbMaxCols; c++) v[c] = c < ncol ? Vb[(int64_t)c * dim + i] : 0.0;
+    for (int c = 0; c < NC; c++) v[c] = c < ncol ? Vg[(int64_t)c * dim + i] : 0.0;
     for (int k = 0; k < nout; k++) {
       double acc = 0.0;
 #pragma unroll
-      for (int c = 0; c < kTbMaxCols; c++)
+      for (int c = 0; c < NC; c++)
         if (c < ncol) acc = acc + ys[c + k * ncol] * v[c];
-      Vb[(int64_t)k * dim + i] = acc;
+      Vg[(int64_t)k * dim + i] = acc;
     }
-    if (scale_col >= 0) Vb[(int64_t)scale_col * dim + i] = inv * w[i];
+    if (scale_col >= 0) Vg[(int64_t)scale_col * dim + i] = inv * wg[i];
   }
 }
 
@@ -143,7 +140,8 @@ __device__ __forceinline__ void tb_rotate(double* Vb, int64_t dim, const double*
 __device__ __forceinline__ double tb_norm2(const double* x, int64_t dim) {
   __shared__ double red[kTbBlock / 64];
   double s = 0.0;
-  for (int64_t i = threadIdx.x; i < dim; i += kTbBlock) s += x[i] * x[i];
+  const auto xg = gptr(x);
+  for (int64_t i = threadIdx.x; i < dim; i += kTbBlock) s += xg[i] * xg[i];
   s = wave_sum_dpp(s);
   if ((threadIdx.x & 63) == 63) red[threadIdx.x >> 6] = s;
   __syncthreads();
@@ -154,6 +152,11 @@ __device__ __forceinline__ double tb_norm2(const double* x, int64_t dim) {
   return r;
 }
 
+// One instantiation per column bound NC (24: Nblock <= 24, else 32): the
+// sweep's column groups all use NC registers (loads stay guarded by ncol), so
+// the kernel holds one orth_solo_body, not four (four inlined: 1,318 SGPR
+// spills).
+template <int NC>
 __global__ void __launch_bounds__(kTbBlock) k_trl_batch(const TrlTask* __restrict__ tasks) {
   extern __shared__ double vl[];  // v_j of the current step (dim doubles)
   __shared__ double sdict[256];
@@ -170,13 +173,13 @@ __global__ void __launch_bounds__(kTbBlock) k_trl_batch(const TrlTask* __restric
   auto step = [&](int vc, int pc, const double* al, const double* be, int kprev, bool shifted, int ncol,
                   double* alpha, double* beta, int jn, double* out, int jc) {
     __syncthreads();  // previous step's out / alpha / beta written
-    const double* v = col(vc);
+    const auto v = gptr(col(vc));
     for (int64_t i = t; i < dim; i += kTbBlock) vl[i] = v[i];
     const double sg = shifted ? al[kprev] : 0.0, bp = shifted ? be[kprev] : 0.0;
     __syncthreads();
     tb_hxv(a, vl, sdict, a.w, shifted ? col(pc) : nullptr, sg, bp, shifted);
     // (the CGS passes read back only each thread's own rows of w)
-    tb_orth(a.Vb, ncol, a.w, dim, a.coef, alpha, beta, jn, jn, out, shifted ? 1 : 0,
+    orth_solo_body<false, NC, (NC <= 24 ? 2 : 1)>(a.Vb, ncol, a.w, dim, a.coef, alpha, beta, jn, jn, out, shifted ? 1 : 0,
             (shifted && a.locupd) ? 1 : 0, jc);
   };
   if (a.op == kTbStart || a.op == kTbRestart) {
@@ -188,7 +191,7 @@ __global__ void __launch_bounds__(kTbBlock) k_trl_batch(const TrlTask* __restric
       if (t == 0) a.mail[64] = b0;
     } else {
       const double bm = a.beta[a.m - 1];
-      tb_rotate(a.Vb, dim, ys, a.ldy, a.nrot, a.w, a.nrot, bm > 0.0 ? 1.0 / bm : 0.0);
+      tb_rotate<NC>(a.Vb, dim, ys, a.ldy, a.nrot, a.w, a.nrot, bm > 0.0 ? 1.0 / bm : 0.0);
       j0 = a.nrot;
     }
     for (int j = j0; j < a.m; j++) {
@@ -206,7 +209,7 @@ __global__ void __launch_bounds__(kTbBlock) k_trl_batch(const TrlTask* __restric
   // nev locked columns, alpha / beta in pa / pb
   const int ca = a.nev, cb = a.nev + 1;
   if (a.nrot > 0) {  // Ritz vectors of the main solve -> V[:, :nrot]
-    tb_rotate(a.Vb, dim, ys, a.ldy, a.nrot, nullptr, -1, 0.0);
+    tb_rotate<NC>(a.Vb, dim, ys, a.ldy, a.nrot, nullptr, -1, 0.0);
     __syncthreads();
   }
   if (a.k0s == 0 && a.k1 > 0) {
@@ -219,7 +222,7 @@ __global__ void __launch_bounds__(kTbBlock) k_trl_batch(const TrlTask* __restric
     }
     __syncthreads();
     // against the locked columns; the norm -> pb[kScreenMaxSteps + 1]; v_0 -> column ca
-    tb_orth(a.Vb, a.nev, a.w, dim, a.coef, nullptr, a.pb, -1, kTbScreenSlot, col(ca), 0, 0);
+    orth_solo_body<false, NC, (NC <= 24 ? 2 : 1)>(a.Vb, a.nev, a.w, dim, a.coef, nullptr, a.pb, -1, kTbScreenSlot, col(ca), 0, 0);
   }
   for (int k = a.k0s; k < a.k1; k++) {
     const int cur = (k & 1) ? cb : ca, prv = (k & 1) ? ca : cb;

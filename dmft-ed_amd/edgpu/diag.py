@@ -76,8 +76,13 @@ class DiagOptions:
     # thick-restart sectors of at most this many rows (real H, stored) are
     # solved together by one host thread through ed_sectors_eigh_batch (one
     # workgroup per sector, one launch per restart cycle for all of them)
-    # beside the other workers; 0: every sector alone (ed_sector_eigh)
-    batch_max_dim: int = 15360
+    # beside the other workers; 0: every sector alone (ed_sector_eigh).
+    # One workgroup's Krylov step grows ~linearly with the rows (configs[3]:
+    # ~13 us at 495-924 rows, ~200 us at 14,520, against ~20-30 us per step
+    # alone), so the batch takes the sectors up to 2,640 rows: configs[3]'s
+    # 36 of them in 28 ms instead of 141 ms one after the other
+    # (tools/batch_prof.py)
+    batch_max_dim: int = 2640
     # multi-rank farms: "dynamic" — every rank's workers take the next sector
     # (largest cost first) from one global counter in the process group's
     # key-value store, so the ranks finish together whatever the cost
