@@ -12,7 +12,11 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <map>
 #include <vector>
@@ -3141,7 +3145,67 @@ static bool tb_eligible(const ed_sector* s, int nev, int ncv) {
          !(s->opts & (ED_OPT_TRLAN_UNFUSED | ED_OPT_TRLAN_NOLOCAL | ED_OPT_TRLAN_NOSOLO));
 }
 
-static int tb_run(ed_sector* const* secs, int n, int nev, int ncv, int maxit, double tol,
+// Fork-join helpers for the batch's per-sector host work (projected
+// eigenproblem, screen QL): kept for one ed_sectors_eigh_batch call; the
+// calling thread works too.  With dozens of sectors per cycle the host part
+// was ~60 % of a batch (profiles/r6/batch_c4_timeline.json).
+struct TbPool {
+  std::vector<std::thread> th;
+  std::mutex mu;
+  std::condition_variable cv, cv_done;
+  const std::function<void(int)>* fn = nullptr;
+  std::atomic<int> next{0};
+  int n = 0, gen = 0, busy = 0;
+  bool quit = false;
+  explicit TbPool(int nt) {
+    for (int i = 0; i < nt; i++) th.emplace_back([this] { loop(); });
+  }
+  ~TbPool() {
+    {
+      std::lock_guard<std::mutex> g(mu);
+      quit = true;
+    }
+    cv.notify_all();
+    for (auto& t : th) t.join();
+  }
+  void work() {
+    for (int i; (i = next.fetch_add(1)) < n;) (*fn)(i);
+  }
+  void loop() {
+    int seen = 0;
+    std::unique_lock<std::mutex> lk(mu);
+    for (;;) {
+      cv.wait(lk, [&] { return quit || gen != seen; });
+      if (quit) return;
+      seen = gen;
+      lk.unlock();
+      work();
+      lk.lock();
+      if (--busy == 0) cv_done.notify_one();
+    }
+  }
+  void run(int count, const std::function<void(int)>& f) {
+    if (th.empty() || count < 8) {
+      for (int i = 0; i < count; i++) f(i);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> g(mu);
+      fn = &f;
+      n = count;
+      next = 0;
+      busy = (int)th.size();
+      gen++;
+    }
+    cv.notify_all();
+    work();
+    std::unique_lock<std::mutex> lk(mu);
+    cv_done.wait(lk, [&] { return busy == 0; });
+  }
+};
+static constexpr int kTbHostThreads = 3;  // helpers beside the calling thread
+
+static int tb_run(ed_sector* const* secs, int n, int nev, int ncv, const int32_t* maxits, double tol,
                   const double* const* v0, double* evals, void* const* evecs, int32_t* nconv, int32_t* nhv,
                   hipStream_t st, std::vector<int>& fallback) {
   std::vector<TbSec> S;
@@ -3241,6 +3305,125 @@ static int tb_run(ed_sector* const* secs, int n, int nev, int ncv, int maxit, do
   });
   HIPCK(lds_err);
   std::vector<int> act;
+  // per-sector host step after a launch (trlan_core's / probe_screen's logic)
+  const std::function<void(int)> process = [&](int a) {
+    const int k = act[a];
+    TbSec& b = S[k];
+    TrlTask& t = b.task;
+    const int maxit = maxits[idx[k]];
+    const double* ml = hmail + (size_t)k * kTbMail;
+    const int m = b.m, ma = m;
+    b.ny = 0;
+    auto tm = [&](int i, int j) -> double& { return b.Tm[i + (size_t)ma * j]; };
+    if (b.state == 0) {  // a main sweep [j0, m) ran (trlan_core)
+      if (t.op == kTbStart && !(ml[64] > 0.0)) {
+        b.state = 4;
+        return;
+      }
+      b.nhv += m - b.j0;
+      int jb = -1;
+      for (int j = b.j0; j < m; j++) {
+        tm(j, j) = ml[j];
+        if (j + 1 < ma) tm(j, j + 1) = tm(j + 1, j) = ml[32 + j];
+        const double scale = fabs(ml[j]) + (j > 0 ? fabs(tm(j - 1, j)) : 0.0) + 1e-300;
+        if (j + 1 < ma && ml[32 + j] < 1e-13 * scale) {
+          jb = j;
+          break;
+        }
+      }
+      if (jb >= 0) {  // invariant subspace: trlan_run continues from a random direction
+        b.state = 4;
+        return;
+      }
+      const double beta = ml[32 + m - 1];
+      sym_eigh(ma, b.Tm, b.theta, b.Z);
+      const double eps23 = 3.6e-11;
+      b.conv = 0;
+      for (int i = 0; i < nev; i++)
+        if (fabs(beta * b.Z[(ma - 1) + (size_t)ma * i]) <= tol * std::max(eps23, fabs(b.theta[i]))) b.conv++;
+      if (b.conv == nev || b.it == maxit - 1 || m == b.dim) {
+        b.ev.assign(b.theta.begin(), b.theta.begin() + nev);
+        const int mp = (int)std::min<int64_t>(std::min(std::min(m, 20), kTrlanMaxCols - nev), b.dim - nev);
+        const bool verify = !(b.s->opts & ED_OPT_EIGH_NO_VERIFY) && mp >= 3 && b.conv == nev;
+        if (verify && (b.s->opts & ED_OPT_EIGH_FULLPROBE)) {
+          b.state = 4;
+          return;
+        }
+        b.hint = verify && nev + 1 < m && !(b.s->opts & ED_OPT_EIGH_NOHINT);
+        const int nrot = b.hint ? nev + 1 : nev;
+        t.op = kTbScreen;
+        t.ldy = ma;
+        t.nrot = nrot;
+        b.ny = ma * nrot;
+        t.k0s = 0;
+        if (verify) {
+          b.state = 1;
+          b.maxsteps = (int)std::min<int64_t>(b.dim - nev, kScreenMaxSteps);
+          b.cut = b.ev[nev - 1] - kProbeMargin * std::max(1.0, fabs(b.ev[nev - 1]));
+          b.tprobe = std::max(tol, 1e-5);
+          t.k1 = std::min(b.maxsteps, kScreenChunk);
+          t.hint = b.hint ? 1 : 0;
+          t.seed = 3000;
+          b.sk = 0;
+          b.sal.clear();
+          b.sbe.clear();
+        } else {
+          b.state = 2;
+          t.k1 = 0;
+        }
+        return;
+      }
+      // thick restart (trlan_core)
+      const int nkeep = std::max(nev, std::min(ma - 2, nev + (ma - nev) / 2));
+      t.op = kTbRestart;
+      t.ldy = ma;
+      t.nrot = nkeep;
+      b.ny = ma * nkeep;
+      std::fill(b.Tm.begin(), b.Tm.end(), 0.0);
+      for (int i = 0; i < nkeep; i++) {
+        tm(i, i) = b.theta[i];
+        tm(i, nkeep) = tm(nkeep, i) = beta * b.Z[(ma - 1) + (size_t)ma * i];
+      }
+      b.j0 = nkeep;
+      b.it++;
+      return;
+    }
+    if (b.state == 2) {  // the final rotation ran: done
+      b.state = 3;
+      return;
+    }
+    // a screen chunk [k0s, k1) ran (probe_screen)
+    const int nst = t.k1 - t.k0s;
+    b.nhv += nst;
+    for (int q = 0; q < nst; q++) {
+      b.sal.push_back(ml[q]);
+      b.sbe.push_back(ml[32 + q]);
+    }
+    t.nrot = 0;
+    const int K = (int)b.sal.size();
+    std::vector<double> ar(K), br(K, 0.0), E(K), z2(K), z1(K);
+    for (int i = 0; i < K; i++) ar[i] = b.sal[K - 1 - i];
+    for (int i = 1; i < K; i++) br[i] = b.sbe[K - 1 - i];
+    int dec = -1;
+    if (ed_tridiag_poles(K, ar.data(), br.data(), E.data(), z2.data(), z1.data()) == ED_OK) {
+      const double theta = E[0], resid = fabs(b.sbe[K - 1] * z1[0]);
+      if (theta < b.cut) dec = 1;
+      else {
+        const bool invariant = b.sbe[K - 1] < 1e-13 * (fabs(theta) + 1e-300);
+        const bool converged = resid <= b.tprobe * std::max(3.6e-11, fabs(theta));
+        if (invariant || (converged && theta - resid > b.cut)) dec = 0;
+      }
+    } else {
+      dec = 2;
+    }
+    if (dec == 0) b.state = 3;
+    else if (dec > 0 || t.k1 >= b.maxsteps) b.state = 4;
+    else {
+      t.k0s = t.k1;
+      t.k1 = std::min(b.maxsteps, t.k0s + kScreenChunk);
+    }
+  };
+  TbPool pool(ns >= 8 ? kTbHostThreads : 0);
   for (;;) {
     act.clear();
     for (int k = 0; k < ns; k++)
@@ -3276,121 +3459,7 @@ static int tb_run(ed_sector* const* secs, int n, int nev, int ncv, int maxit, do
     HIPCK(hipGetLastError());
     HIPCK(hipMemcpyAsync(hmail, dmail, nmail * sizeof(double), hipMemcpyDeviceToHost, st));
     HIPCK(hipStreamSynchronize(st));
-    for (int k : act) {
-      TbSec& b = S[k];
-      TrlTask& t = b.task;
-      const double* ml = hmail + (size_t)k * kTbMail;
-      const int m = b.m, ma = m;
-      b.ny = 0;
-      auto tm = [&](int i, int j) -> double& { return b.Tm[i + (size_t)ma * j]; };
-      if (b.state == 0) {  // a main sweep [j0, m) ran (trlan_core)
-        if (t.op == kTbStart && !(ml[64] > 0.0)) {
-          b.state = 4;
-          continue;
-        }
-        b.nhv += m - b.j0;
-        int jb = -1;
-        for (int j = b.j0; j < m; j++) {
-          tm(j, j) = ml[j];
-          if (j + 1 < ma) tm(j, j + 1) = tm(j + 1, j) = ml[32 + j];
-          const double scale = fabs(ml[j]) + (j > 0 ? fabs(tm(j - 1, j)) : 0.0) + 1e-300;
-          if (j + 1 < ma && ml[32 + j] < 1e-13 * scale) {
-            jb = j;
-            break;
-          }
-        }
-        if (jb >= 0) {  // invariant subspace: trlan_run continues from a random direction
-          b.state = 4;
-          continue;
-        }
-        const double beta = ml[32 + m - 1];
-        sym_eigh(ma, b.Tm, b.theta, b.Z);
-        const double eps23 = 3.6e-11;
-        b.conv = 0;
-        for (int i = 0; i < nev; i++)
-          if (fabs(beta * b.Z[(ma - 1) + (size_t)ma * i]) <= tol * std::max(eps23, fabs(b.theta[i]))) b.conv++;
-        if (b.conv == nev || b.it == maxit - 1 || m == b.dim) {
-          b.ev.assign(b.theta.begin(), b.theta.begin() + nev);
-          const int mp = (int)std::min<int64_t>(std::min(std::min(m, 20), kTrlanMaxCols - nev), b.dim - nev);
-          const bool verify = !(b.s->opts & ED_OPT_EIGH_NO_VERIFY) && mp >= 3 && b.conv == nev;
-          if (verify && (b.s->opts & ED_OPT_EIGH_FULLPROBE)) {
-            b.state = 4;
-            continue;
-          }
-          b.hint = verify && nev + 1 < m && !(b.s->opts & ED_OPT_EIGH_NOHINT);
-          const int nrot = b.hint ? nev + 1 : nev;
-          t.op = kTbScreen;
-          t.ldy = ma;
-          t.nrot = nrot;
-          b.ny = ma * nrot;
-          t.k0s = 0;
-          if (verify) {
-            b.state = 1;
-            b.maxsteps = (int)std::min<int64_t>(b.dim - nev, kScreenMaxSteps);
-            b.cut = b.ev[nev - 1] - kProbeMargin * std::max(1.0, fabs(b.ev[nev - 1]));
-            b.tprobe = std::max(tol, 1e-5);
-            t.k1 = std::min(b.maxsteps, kScreenChunk);
-            t.hint = b.hint ? 1 : 0;
-            t.seed = 3000;
-            b.sk = 0;
-            b.sal.clear();
-            b.sbe.clear();
-          } else {
-            b.state = 2;
-            t.k1 = 0;
-          }
-          continue;
-        }
-        // thick restart (trlan_core)
-        const int nkeep = std::max(nev, std::min(ma - 2, nev + (ma - nev) / 2));
-        t.op = kTbRestart;
-        t.ldy = ma;
-        t.nrot = nkeep;
-        b.ny = ma * nkeep;
-        std::fill(b.Tm.begin(), b.Tm.end(), 0.0);
-        for (int i = 0; i < nkeep; i++) {
-          tm(i, i) = b.theta[i];
-          tm(i, nkeep) = tm(nkeep, i) = beta * b.Z[(ma - 1) + (size_t)ma * i];
-        }
-        b.j0 = nkeep;
-        b.it++;
-        continue;
-      }
-      if (b.state == 2) {  // the final rotation ran: done
-        b.state = 3;
-        continue;
-      }
-      // a screen chunk [k0s, k1) ran (probe_screen)
-      const int nst = t.k1 - t.k0s;
-      b.nhv += nst;
-      for (int q = 0; q < nst; q++) {
-        b.sal.push_back(ml[q]);
-        b.sbe.push_back(ml[32 + q]);
-      }
-      t.nrot = 0;
-      const int K = (int)b.sal.size();
-      std::vector<double> ar(K), br(K, 0.0), E(K), z2(K), z1(K);
-      for (int i = 0; i < K; i++) ar[i] = b.sal[K - 1 - i];
-      for (int i = 1; i < K; i++) br[i] = b.sbe[K - 1 - i];
-      int dec = -1;
-      if (ed_tridiag_poles(K, ar.data(), br.data(), E.data(), z2.data(), z1.data()) == ED_OK) {
-        const double theta = E[0], resid = fabs(b.sbe[K - 1] * z1[0]);
-        if (theta < b.cut) dec = 1;
-        else {
-          const bool invariant = b.sbe[K - 1] < 1e-13 * (fabs(theta) + 1e-300);
-          const bool converged = resid <= b.tprobe * std::max(3.6e-11, fabs(theta));
-          if (invariant || (converged && theta - resid > b.cut)) dec = 0;
-        }
-      } else {
-        dec = 2;
-      }
-      if (dec == 0) b.state = 3;
-      else if (dec > 0 || t.k1 >= b.maxsteps) b.state = 4;
-      else {
-        t.k0s = t.k1;
-        t.k1 = std::min(b.maxsteps, t.k0s + kScreenChunk);
-      }
-    }
+    pool.run((int)act.size(), process);
   }
   // results; fall-backs re-solved by the caller
   for (int k = 0; k < ns; k++) {
@@ -4311,10 +4380,12 @@ int ed_sector_lanc_eigh(ed_sector* s, int32_t vtype, const void* v0, int32_t nit
   return ED_OK;
 }
 
-int ed_sectors_eigh_batch(ed_sector* const* secs, int32_t n, int32_t nev, int32_t ncv, int32_t maxit, double tol,
-                          const double* const* v0, double* evals, void* const* evecs, int32_t* nconv, int32_t* nhv,
-                          int32_t* nbatched, void* stream) {
-  if (!secs || n < 0 || !evals || maxit < 1) return fail(ED_ERR_ARG, "bad args");
+int ed_sectors_eigh_batch(ed_sector* const* secs, int32_t n, int32_t nev, int32_t ncv, const int32_t* maxit,
+                          double tol, const double* const* v0, double* evals, void* const* evecs, int32_t* nconv,
+                          int32_t* nhv, int32_t* nbatched, void* stream) {
+  if (!secs || n < 0 || !evals || !maxit) return fail(ED_ERR_ARG, "bad args");
+  for (int i = 0; i < n; i++)
+    if (maxit[i] < 1) return fail(ED_ERR_ARG, "maxit < 1");
   if (n == 0) return ED_OK;
   if (ncv > kTrlanMaxCols) return fail(ED_ERR_ARG, "ncv > 64 not supported");
   for (int i = 0; i < n; i++) {
@@ -4330,7 +4401,7 @@ int ed_sectors_eigh_batch(ed_sector* const* secs, int32_t n, int32_t nev, int32_
   if (nbatched) *nbatched = n - (int)fb.size();
   for (int i : fb) {
     int32_t c = 0, h = 0;
-    CK(trlan_run<false>(secs[i], nev, ncv, maxit, tol, v0 ? v0[i] : nullptr, evals + (size_t)i * nev,
+    CK(trlan_run<false>(secs[i], nev, ncv, maxit[i], tol, v0 ? v0[i] : nullptr, evals + (size_t)i * nev,
                         evecs ? evecs[i] : nullptr, &c, &h));
     if (nconv) nconv[i] = c;
     if (nhv) nhv[i] += h;

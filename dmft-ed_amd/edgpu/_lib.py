@@ -50,7 +50,7 @@ SIGNATURES = {
     "ed_sector_kron_rows": ([_P, _i32, _i64, _i64, _P, _P, _P], ctypes.c_int),
     "ed_sector_kron_cols": ([_P, _i32, _i64, _i64, _P, _P, _i32, _P], ctypes.c_int),
     "ed_sector_eigh": ([_P, _i32, _i32, _i32, _i32, _f64, _P, _P, _P, _P, _P], ctypes.c_int),
-    "ed_sectors_eigh_batch": ([_P, _i32, _i32, _i32, _i32, _f64, _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
+    "ed_sectors_eigh_batch": ([_P, _i32, _i32, _i32, _P, _f64, _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
     "ed_sector_sell_view": ([_P, _P], ctypes.c_int),
     "ed_sector_apply_op": ([_P, _P, _i32, _i32, _i32, _P, _P, _P], ctypes.c_int),
     "ed_sector_apply_op_acc": ([_P, _P, _i32, _i32, _f64, _f64, _i32, _P, _P, _P], ctypes.c_int),

@@ -232,13 +232,14 @@ def solve_batch(cfg: EDConfig, secs: List[SectorId], opt: DiagOptions, device: i
     from .hamiltonian import eigh_batch
 
     st = _worker_stream(opt, device)
-    groups: Dict[Tuple[int, int, int], List[int]] = {}
+    groups: Dict[Tuple[int, int], List[int]] = {}
     for k, sec in enumerate(secs):
         neigen, nitermax, nblock = lanczos_params(sec.dim, opt)
         ncv = min(max(nblock, neigen + 1), 64, sec.dim)
-        groups.setdefault((neigen, ncv, max(nitermax, 10)), []).append(k)
+        groups.setdefault((neigen, ncv), []).append(k)
     out: List[Optional[SectorResult]] = [None] * len(secs)
-    for (neigen, ncv, maxit), ks in groups.items():
+    for (neigen, ncv), ks in groups.items():
+        maxit = [max(lanczos_params(secs[k].dim, opt)[1], 10) for k in ks]
         hs: List[Sector] = []
         try:
             for k in ks:

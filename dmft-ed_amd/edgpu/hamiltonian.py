@@ -274,12 +274,13 @@ class Sector:
         return vt, _ptr(arr)
 
 
-def eigh_batch(sectors, neigen: int = 6, ncv: int = 23, maxit: int = 512, tol: float = 1e-12,
+def eigh_batch(sectors, neigen: int = 6, ncv: int = 23, maxit=512, tol: float = 1e-12,
                v0s=None, vectors: bool = True, on_device: bool = False, stream=None):
     """Sector.eigh (real vectors) for many sectors of one GPU at once
     (ed_sectors_eigh_batch): the small stored sectors' restart cycles share
     launches.  Returns one (eigenvalues, vectors (dim, neigen) or None, nconv,
-    H·v products) per sector, and the number finished inside the batch."""
+    H·v products) per sector, and the number finished inside the batch.
+    maxit: one Nitermax for all, or one per sector."""
     n = len(sectors)
     if n == 0:
         return [], 0
@@ -304,7 +305,8 @@ def eigh_batch(sectors, neigen: int = 6, ncv: int = 23, maxit: int = 512, tol: f
     nconv = np.zeros(n, dtype=np.int32)
     nhv = np.zeros(n, dtype=np.int32)
     nb = ctypes.c_int32()
-    check(lib.ed_sectors_eigh_batch(hs, n, neigen, ncv, maxit, tol, v0p, _ptr(ev), ep, _ptr(nconv), _ptr(nhv),
+    mx = np.ascontiguousarray(np.broadcast_to(np.asarray(maxit, dtype=np.int32), (n,)))
+    check(lib.ed_sectors_eigh_batch(hs, n, neigen, ncv, _ptr(mx), tol, v0p, _ptr(ev), ep, _ptr(nconv), _ptr(nhv),
                                     ctypes.byref(nb), _stream_ptr(stream)), "ed_sectors_eigh_batch")
     res = [(ev[i].copy(), outs[i].T if outs[i] is not None else None, int(nconv[i]), int(nhv[i]))
            for i in range(n)]

@@ -272,11 +272,11 @@ int ed_sector_eigh(ed_sector* s, int32_t vtype, int32_t nev, int32_t ncv, int32_
  * (one launch and one host round trip per cycle for all of them); sectors
  * the batch cannot take or finish are solved by ed_sector_eigh's path
  * afterwards.  The farm's replacement of ED_DIAG.f90:71-249's loop over the
- * small sectors' sp_eigh calls.  v0[i] (host, or NULL / v0 NULL: the default
- * start), evals[i*nev + k], evecs[i] (host or device, dim x nev, or NULL),
+ * small sectors' sp_eigh calls.  maxit[i]: sector i's Nitermax; v0[i] (host,
+ * or NULL / v0 NULL: the default start), evals[i*nev + k], evecs[i] (host or device, dim x nev, or NULL),
  * nconv[i], nhv[i]; *nbatched: sectors finished inside the batch (or NULL);
  * stream: the launches' stream (NULL: the first sector's). */
-int ed_sectors_eigh_batch(ed_sector* const* secs, int32_t n, int32_t nev, int32_t ncv, int32_t maxit,
+int ed_sectors_eigh_batch(ed_sector* const* secs, int32_t n, int32_t nev, int32_t ncv, const int32_t* maxit,
                           double tol, const double* const* v0, double* evals, void* const* evecs,
                           int32_t* nconv, int32_t* nhv, int32_t* nbatched, void* stream);
 /* Fixed-length Lanczos on device pointers for benchmarking: runs exactly

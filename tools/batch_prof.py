@@ -2,7 +2,7 @@
 sector builds, the batch solve and the closes separately, against the same
 sectors solved one after the other with ed_sector_eigh.
 
-    python tools/batch_prof.py [--bath random] [--max-dim 15360] [--reps 3]
+    python tools/batch_prof.py [--bath random] [--max-dim N] [--reps 3] [--single]
 """
 import argparse
 import os
@@ -21,12 +21,12 @@ from golden.golden_configs import c4_config  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--bath", default="random")
-ap.add_argument("--max-dim", type=int, default=15360)
+ap.add_argument("--max-dim", type=int, default=None, help="DiagOptions.batch_max_dim (default: the library's)")
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--single", action="store_true", help="also the per-sector solves")
 a = ap.parse_args()
 cfg = c4_config(a.bath)
-opt = DiagOptions(batch_max_dim=a.max_dim)
+opt = DiagOptions() if a.max_dim is None else DiagOptions(batch_max_dim=a.max_dim)
 secs = [s for s in diag_sectors(cfg) if batchable(cfg, s, opt)]
 st = torch.cuda.Stream()
 print(f"{len(secs)} batchable sectors, dims {min(s.dim for s in secs)}-{max(s.dim for s in secs)}", flush=True)
@@ -37,9 +37,10 @@ for rep in range(a.reps):
     groups = {}
     for h, s in zip(hs, secs):
         ne, nit, nb = lanczos_params(s.dim, opt)
-        groups.setdefault((ne, min(nb, 64, s.dim), max(nit, 10)), []).append(h)
+        groups.setdefault((ne, min(nb, 64, s.dim)), []).append(h)
     nhv = nbat = 0
-    for (ne, ncv, mx), g in groups.items():
+    for (ne, ncv), g in groups.items():
+        mx = [max(lanczos_params(h.dim, opt)[1], 10) for h in g]
         res, nb = eigh_batch(g, ne, ncv, mx, opt.lanc_tolerance, [_start_vector(h.dim, False) for h in g],
                              vectors=True, on_device=True, stream=st)
         nhv += sum(r[3] for r in res)
