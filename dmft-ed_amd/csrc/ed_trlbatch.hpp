@@ -70,18 +70,52 @@ __device__ __forceinline__ double tb_hash(int64_t i, uint64_t seed) {  // k_hash
   return (double)(z >> 11) * (1.0 / 9007199254740992.0) * 2.0 - 1.0;
 }
 
-// w = H v (v staged in LDS vl); shifted: w = (H - sg) v - bp vprev.  Row
-// sums in slot order, diagonal first (k_step_solo / k_spmv_pk).
-__device__ __forceinline__ void tb_hxv(const TrlTask& a, const double* vl, const double* sdict, double* x,
-                                       const double* vprev, double sg, double bp, bool shifted) {
+// w = H v (v staged in LDS vl, the slice pointers in LDS ssp); shifted:
+// w = (H - sg) v - bp vprev.  Row sums in slot order, diagonal first
+// (k_step_solo / k_spmv_pk).  Packed words: two rows per iteration, both
+// rows' word loads in flight before either row's gathers (one workgroup on
+// thousands of rows is bound by the latency of each row's loads).
+__device__ __forceinline__ void tb_hxv(const TrlTask& a, const int64_t* ssp, const double* vl, const double* sdict,
+                                       double* x, const double* vprev, double sg, double bp, bool shifted) {
   const int t = threadIdx.x;
-  const auto sptr = gptr(a.sptr);
   const auto diag = gptr(a.diag);
   const auto xg = gptr(x);
   const auto pg = gptr(vprev);
-  for (int64_t i = t; i < a.dim; i += kTbBlock) {
-    const int64_t sl = i >> 6, s0 = sptr[sl];
-    const int w = (int)((sptr[sl + 1] - s0) >> 6);
+  int64_t i = t;
+  if (a.words) {
+    const auto wb = gptr(a.words);
+    for (; i + kTbBlock < a.dim; i += 2 * kTbBlock) {
+      const int64_t j = i + kTbBlock;
+      const int64_t s0a = ssp[i >> 6], s0b = ssp[j >> 6];
+      const int wa = (int)((ssp[(i >> 6) + 1] - s0a) >> 6), wbn = (int)((ssp[(j >> 6) + 1] - s0b) >> 6);
+      const auto pa = wb + s0a + (i & 63);
+      const auto pb = wb + s0b + (j & 63);
+      const double da = diag[i], db = diag[j];
+      const double qa = shifted ? pg[i] : 0.0, qb = shifted ? pg[j] : 0.0;
+      const double xa = vl[i], xb = vl[j];
+      double acca = 0.0 + da * xa, accb = 0.0 + db * xb;
+      const int wm = wa > wbn ? wa : wbn;
+      for (int k0 = 0; k0 < wm; k0 += kChunk) {
+        uint32_t ca[kChunk], cb[kChunk];
+#pragma unroll
+        for (int k = 0; k < kChunk; k++) {
+          ca[k] = (k0 + k < wa) ? pa[64 * (k0 + k)] : 0u;
+          cb[k] = (k0 + k < wbn) ? pb[64 * (k0 + k)] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < kChunk; k++)
+          if (k0 + k < wa) acca = acca + sdict[ca[k] >> kPackShift] * vl[ca[k] & kPackColMask];
+#pragma unroll
+        for (int k = 0; k < kChunk; k++)
+          if (k0 + k < wbn) accb = accb + sdict[cb[k] >> kPackShift] * vl[cb[k] & kPackColMask];
+      }
+      xg[i] = shifted ? (acca - sg * xa) - bp * qa : acca;
+      xg[j] = shifted ? (accb - sg * xb) - bp * qb : accb;
+    }
+  }
+  for (; i < a.dim; i += kTbBlock) {
+    const int64_t sl = i >> 6, s0 = ssp[sl];
+    const int w = (int)((ssp[sl + 1] - s0) >> 6);
     const double xi = vl[i];
     double acc = 0.0 + diag[i] * xi;
     if (a.words) {
@@ -161,11 +195,13 @@ __global__ void __launch_bounds__(kTbBlock) k_trl_batch(const TrlTask* __restric
   extern __shared__ double vl[];  // v_j of the current step (dim doubles)
   __shared__ double sdict[256];
   __shared__ double ys[kTbMaxCols * kTbMaxCols];
+  __shared__ int64_t ssp[kTbMaxDim / 64 + 2];  // SELL slice pointers
   const TrlTask a = tasks[blockIdx.x];
   const int t = threadIdx.x;
   const int64_t dim = a.dim;
   auto col = [&](int c) { return a.Vb + (int64_t)c * dim; };
   if (a.words && t < 256) sdict[t] = a.dict[t];
+  for (int64_t k = t; k <= (dim + 63) / 64; k += kTbBlock) ssp[k] = a.sptr[k];
   if (a.nrot > 0)
     for (int k = t; k < a.ldy * a.nrot; k += kTbBlock) ys[k] = a.Y[k];
   __syncthreads();
@@ -174,10 +210,11 @@ __global__ void __launch_bounds__(kTbBlock) k_trl_batch(const TrlTask* __restric
                   double* alpha, double* beta, int jn, double* out, int jc) {
     __syncthreads();  // previous step's out / alpha / beta written
     const auto v = gptr(col(vc));
+#pragma unroll 4
     for (int64_t i = t; i < dim; i += kTbBlock) vl[i] = v[i];
     const double sg = shifted ? al[kprev] : 0.0, bp = shifted ? be[kprev] : 0.0;
     __syncthreads();
-    tb_hxv(a, vl, sdict, a.w, shifted ? col(pc) : nullptr, sg, bp, shifted);
+    tb_hxv(a, ssp, vl, sdict, a.w, shifted ? col(pc) : nullptr, sg, bp, shifted);
     // (the CGS passes read back only each thread's own rows of w)
     orth_solo_body<false, NC, (NC <= 24 ? 2 : 1)>(a.Vb, ncol, a.w, dim, a.coef, alpha, beta, jn, jn, out, shifted ? 1 : 0,
             (shifted && a.locupd) ? 1 : 0, jc);
