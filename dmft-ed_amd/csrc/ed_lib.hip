@@ -25,6 +25,7 @@
 #include "ed_persist.hpp"
 #include "ed_trlan.hpp"
 #include "ed_trlbatch.hpp"
+#include "ed_trlmulti.hpp"
 #include "ed_fused.hpp"
 #include "ed_split.hpp"
 #include "ed_tables.hpp"
@@ -3145,6 +3146,125 @@ static bool tb_eligible(const ed_sector* s, int nev, int ncv) {
          !(s->opts & (ED_OPT_TRLAN_UNFUSED | ED_OPT_TRLAN_NOLOCAL | ED_OPT_TRLAN_NOSOLO));
 }
 
+// One sector's host step after a cycle of the batch (ed_trlbatch.hpp) or of
+// the lockstep multi-sector solve (ed_trlmulti.hpp), on its mailbox ml
+// (alpha [0, 32) | beta [32, 64) | scalar [64]): trlan_core's projected
+// eigenproblem, ARPACK convergence test and thick restart, then
+// probe_screen's decisions; sets the sector's next task (b.task, b.ny).
+static void tb_advance(TbSec& b, const double* ml, int nev, int maxit, double tol) {
+  TrlTask& t = b.task;
+  const int m = b.m, ma = m;
+  b.ny = 0;
+  auto tm = [&](int i, int j) -> double& { return b.Tm[i + (size_t)ma * j]; };
+  if (b.state == 0) {  // a main sweep [j0, m) ran (trlan_core)
+    if (t.op == kTbStart && !(ml[64] > 0.0)) {
+      b.state = 4;
+      return;
+    }
+    b.nhv += m - b.j0;
+    int jb = -1;
+    for (int j = b.j0; j < m; j++) {
+      tm(j, j) = ml[j];
+      if (j + 1 < ma) tm(j, j + 1) = tm(j + 1, j) = ml[32 + j];
+      const double scale = fabs(ml[j]) + (j > 0 ? fabs(tm(j - 1, j)) : 0.0) + 1e-300;
+      if (j + 1 < ma && ml[32 + j] < 1e-13 * scale) {
+        jb = j;
+        break;
+      }
+    }
+    if (jb >= 0) {  // invariant subspace: trlan_run continues from a random direction
+      b.state = 4;
+      return;
+    }
+    const double beta = ml[32 + m - 1];
+    sym_eigh(ma, b.Tm, b.theta, b.Z);
+    const double eps23 = 3.6e-11;
+    b.conv = 0;
+    for (int i = 0; i < nev; i++)
+      if (fabs(beta * b.Z[(ma - 1) + (size_t)ma * i]) <= tol * std::max(eps23, fabs(b.theta[i]))) b.conv++;
+    if (b.conv == nev || b.it == maxit - 1 || m == b.dim) {
+      b.ev.assign(b.theta.begin(), b.theta.begin() + nev);
+      const int mp = (int)std::min<int64_t>(std::min(std::min(m, 20), kTrlanMaxCols - nev), b.dim - nev);
+      const bool verify = !(b.s->opts & ED_OPT_EIGH_NO_VERIFY) && mp >= 3 && b.conv == nev;
+      if (verify && (b.s->opts & ED_OPT_EIGH_FULLPROBE)) {
+        b.state = 4;
+        return;
+      }
+      b.hint = verify && nev + 1 < m && !(b.s->opts & ED_OPT_EIGH_NOHINT);
+      const int nrot = b.hint ? nev + 1 : nev;
+      t.op = kTbScreen;
+      t.ldy = ma;
+      t.nrot = nrot;
+      b.ny = ma * nrot;
+      t.k0s = 0;
+      if (verify) {
+        b.state = 1;
+        b.maxsteps = (int)std::min<int64_t>(b.dim - nev, kScreenMaxSteps);
+        b.cut = b.ev[nev - 1] - kProbeMargin * std::max(1.0, fabs(b.ev[nev - 1]));
+        b.tprobe = std::max(tol, 1e-5);
+        t.k1 = std::min(b.maxsteps, kScreenChunk);
+        t.hint = b.hint ? 1 : 0;
+        t.seed = 3000;
+        b.sk = 0;
+        b.sal.clear();
+        b.sbe.clear();
+      } else {
+        b.state = 2;
+        t.k1 = 0;
+      }
+      return;
+    }
+    // thick restart (trlan_core)
+    const int nkeep = std::max(nev, std::min(ma - 2, nev + (ma - nev) / 2));
+    t.op = kTbRestart;
+    t.ldy = ma;
+    t.nrot = nkeep;
+    b.ny = ma * nkeep;
+    std::fill(b.Tm.begin(), b.Tm.end(), 0.0);
+    for (int i = 0; i < nkeep; i++) {
+      tm(i, i) = b.theta[i];
+      tm(i, nkeep) = tm(nkeep, i) = beta * b.Z[(ma - 1) + (size_t)ma * i];
+    }
+    b.j0 = nkeep;
+    b.it++;
+    return;
+  }
+  if (b.state == 2) {  // the final rotation ran: done
+    b.state = 3;
+    return;
+  }
+  // a screen chunk [k0s, k1) ran (probe_screen)
+  const int nst = t.k1 - t.k0s;
+  b.nhv += nst;
+  for (int q = 0; q < nst; q++) {
+    b.sal.push_back(ml[q]);
+    b.sbe.push_back(ml[32 + q]);
+  }
+  t.nrot = 0;
+  const int K = (int)b.sal.size();
+  std::vector<double> ar(K), br(K, 0.0), E(K), z2(K), z1(K);
+  for (int i = 0; i < K; i++) ar[i] = b.sal[K - 1 - i];
+  for (int i = 1; i < K; i++) br[i] = b.sbe[K - 1 - i];
+  int dec = -1;
+  if (ed_tridiag_poles(K, ar.data(), br.data(), E.data(), z2.data(), z1.data()) == ED_OK) {
+    const double theta = E[0], resid = fabs(b.sbe[K - 1] * z1[0]);
+    if (theta < b.cut) dec = 1;
+    else {
+      const bool invariant = b.sbe[K - 1] < 1e-13 * (fabs(theta) + 1e-300);
+      const bool converged = resid <= b.tprobe * std::max(3.6e-11, fabs(theta));
+      if (invariant || (converged && theta - resid > b.cut)) dec = 0;
+    }
+  } else {
+    dec = 2;
+  }
+  if (dec == 0) b.state = 3;
+  else if (dec > 0 || t.k1 >= b.maxsteps) b.state = 4;
+  else {
+    t.k0s = t.k1;
+    t.k1 = std::min(b.maxsteps, t.k0s + kScreenChunk);
+  }
+}
+
 // Fork-join helpers for the batch's per-sector host work (projected
 // eigenproblem, screen QL): kept for one ed_sectors_eigh_batch call; the
 // calling thread works too.  With dozens of sectors per cycle the host part
@@ -3205,12 +3325,12 @@ struct TbPool {
 };
 static constexpr int kTbHostThreads = 3;  // helpers beside the calling thread
 
-static int tb_run(ed_sector* const* secs, int n, int nev, int ncv, const int32_t* maxits, double tol,
-                  const double* const* v0, double* evals, void* const* evecs, int32_t* nconv, int32_t* nhv,
-                  hipStream_t st, std::vector<int>& fallback) {
+static int tb_run(ed_sector* const* secs, const std::vector<int>& which, int nev, int ncv, const int32_t* maxits,
+                  double tol, const double* const* v0, double* evals, void* const* evecs, int32_t* nconv,
+                  int32_t* nhv, hipStream_t st, std::vector<int>& fallback) {
   std::vector<TbSec> S;
   std::vector<int> idx;
-  for (int i = 0; i < n; i++) {
+  for (int i : which) {
     if (!tb_eligible(secs[i], nev, ncv)) {
       fallback.push_back(i);
       continue;
@@ -3308,120 +3428,7 @@ static int tb_run(ed_sector* const* secs, int n, int nev, int ncv, const int32_t
   // per-sector host step after a launch (trlan_core's / probe_screen's logic)
   const std::function<void(int)> process = [&](int a) {
     const int k = act[a];
-    TbSec& b = S[k];
-    TrlTask& t = b.task;
-    const int maxit = maxits[idx[k]];
-    const double* ml = hmail + (size_t)k * kTbMail;
-    const int m = b.m, ma = m;
-    b.ny = 0;
-    auto tm = [&](int i, int j) -> double& { return b.Tm[i + (size_t)ma * j]; };
-    if (b.state == 0) {  // a main sweep [j0, m) ran (trlan_core)
-      if (t.op == kTbStart && !(ml[64] > 0.0)) {
-        b.state = 4;
-        return;
-      }
-      b.nhv += m - b.j0;
-      int jb = -1;
-      for (int j = b.j0; j < m; j++) {
-        tm(j, j) = ml[j];
-        if (j + 1 < ma) tm(j, j + 1) = tm(j + 1, j) = ml[32 + j];
-        const double scale = fabs(ml[j]) + (j > 0 ? fabs(tm(j - 1, j)) : 0.0) + 1e-300;
-        if (j + 1 < ma && ml[32 + j] < 1e-13 * scale) {
-          jb = j;
-          break;
-        }
-      }
-      if (jb >= 0) {  // invariant subspace: trlan_run continues from a random direction
-        b.state = 4;
-        return;
-      }
-      const double beta = ml[32 + m - 1];
-      sym_eigh(ma, b.Tm, b.theta, b.Z);
-      const double eps23 = 3.6e-11;
-      b.conv = 0;
-      for (int i = 0; i < nev; i++)
-        if (fabs(beta * b.Z[(ma - 1) + (size_t)ma * i]) <= tol * std::max(eps23, fabs(b.theta[i]))) b.conv++;
-      if (b.conv == nev || b.it == maxit - 1 || m == b.dim) {
-        b.ev.assign(b.theta.begin(), b.theta.begin() + nev);
-        const int mp = (int)std::min<int64_t>(std::min(std::min(m, 20), kTrlanMaxCols - nev), b.dim - nev);
-        const bool verify = !(b.s->opts & ED_OPT_EIGH_NO_VERIFY) && mp >= 3 && b.conv == nev;
-        if (verify && (b.s->opts & ED_OPT_EIGH_FULLPROBE)) {
-          b.state = 4;
-          return;
-        }
-        b.hint = verify && nev + 1 < m && !(b.s->opts & ED_OPT_EIGH_NOHINT);
-        const int nrot = b.hint ? nev + 1 : nev;
-        t.op = kTbScreen;
-        t.ldy = ma;
-        t.nrot = nrot;
-        b.ny = ma * nrot;
-        t.k0s = 0;
-        if (verify) {
-          b.state = 1;
-          b.maxsteps = (int)std::min<int64_t>(b.dim - nev, kScreenMaxSteps);
-          b.cut = b.ev[nev - 1] - kProbeMargin * std::max(1.0, fabs(b.ev[nev - 1]));
-          b.tprobe = std::max(tol, 1e-5);
-          t.k1 = std::min(b.maxsteps, kScreenChunk);
-          t.hint = b.hint ? 1 : 0;
-          t.seed = 3000;
-          b.sk = 0;
-          b.sal.clear();
-          b.sbe.clear();
-        } else {
-          b.state = 2;
-          t.k1 = 0;
-        }
-        return;
-      }
-      // thick restart (trlan_core)
-      const int nkeep = std::max(nev, std::min(ma - 2, nev + (ma - nev) / 2));
-      t.op = kTbRestart;
-      t.ldy = ma;
-      t.nrot = nkeep;
-      b.ny = ma * nkeep;
-      std::fill(b.Tm.begin(), b.Tm.end(), 0.0);
-      for (int i = 0; i < nkeep; i++) {
-        tm(i, i) = b.theta[i];
-        tm(i, nkeep) = tm(nkeep, i) = beta * b.Z[(ma - 1) + (size_t)ma * i];
-      }
-      b.j0 = nkeep;
-      b.it++;
-      return;
-    }
-    if (b.state == 2) {  // the final rotation ran: done
-      b.state = 3;
-      return;
-    }
-    // a screen chunk [k0s, k1) ran (probe_screen)
-    const int nst = t.k1 - t.k0s;
-    b.nhv += nst;
-    for (int q = 0; q < nst; q++) {
-      b.sal.push_back(ml[q]);
-      b.sbe.push_back(ml[32 + q]);
-    }
-    t.nrot = 0;
-    const int K = (int)b.sal.size();
-    std::vector<double> ar(K), br(K, 0.0), E(K), z2(K), z1(K);
-    for (int i = 0; i < K; i++) ar[i] = b.sal[K - 1 - i];
-    for (int i = 1; i < K; i++) br[i] = b.sbe[K - 1 - i];
-    int dec = -1;
-    if (ed_tridiag_poles(K, ar.data(), br.data(), E.data(), z2.data(), z1.data()) == ED_OK) {
-      const double theta = E[0], resid = fabs(b.sbe[K - 1] * z1[0]);
-      if (theta < b.cut) dec = 1;
-      else {
-        const bool invariant = b.sbe[K - 1] < 1e-13 * (fabs(theta) + 1e-300);
-        const bool converged = resid <= b.tprobe * std::max(3.6e-11, fabs(theta));
-        if (invariant || (converged && theta - resid > b.cut)) dec = 0;
-      }
-    } else {
-      dec = 2;
-    }
-    if (dec == 0) b.state = 3;
-    else if (dec > 0 || t.k1 >= b.maxsteps) b.state = 4;
-    else {
-      t.k0s = t.k1;
-      t.k1 = std::min(b.maxsteps, t.k0s + kScreenChunk);
-    }
+    tb_advance(S[k], hmail + (size_t)k * kTbMail, nev, maxits[idx[k]], tol);
   };
   TbPool pool(ns >= 8 ? kTbHostThreads : 0);
   for (;;) {
@@ -3473,6 +3480,232 @@ static int tb_run(ed_sector* const* secs, int n, int nev, int ncv, const int32_t
     for (int e = 0; e < nev; e++) evals[(size_t)i * nev + e] = b.ev[e];
     if (evecs && evecs[i])
       HIPCK(hipMemcpyAsync(evecs[i], b.task.Vb, (size_t)nev * b.dim * sizeof(double), hipMemcpyDefault, st));
+    if (nconv) nconv[i] = b.conv;
+    if (nhv) nhv[i] = b.nhv;
+  }
+  HIPCK(hipStreamSynchronize(st));
+  return ED_OK;
+}
+
+// ------------------------------------- lockstep multi-sector eigh
+// tm_run: trlan_run's algorithm for stored sectors above the one-workgroup
+// batch's size, all of them in lockstep (ed_trlmulti.hpp): one cycle = the
+// rotations, then S steps of 7 launches each carrying every running sector,
+// one mailbox copy down and the per-sector host step (tb_advance) on the
+// pool.  Sectors it cannot take or finish go to `fallback`.
+static bool tm_eligible(const ed_sector* s, int nev, int ncv) {
+  const int m = (int)std::min<int64_t>(ncv, s->dim);
+  return s && !s->hc && s->nrows == s->dim && s->row0 == 0 && resolve_path(s, -1) == 0 && s->d_sptr &&
+         s->d_diag && s->d_words && s->d_pdict && m <= kTbMaxCols && nev >= 1 && nev < m &&
+         nev + 2 <= kTbMaxCols && s->dim > (int64_t)nev + 2 && s->nslice * 64 >= s->dim &&
+         !(s->opts & (ED_OPT_TRLAN_UNFUSED | ED_OPT_TRLAN_NOLOCAL | ED_OPT_TRLAN_NOSOLO));
+}
+
+static int tm_run(ed_sector* const* secs, const std::vector<int>& which, int nev, int ncv, const int32_t* maxits,
+                  double tol, const double* const* v0, double* evals, void* const* evecs, int32_t* nconv,
+                  int32_t* nhv, hipStream_t st, std::vector<int>& fallback) {
+  const int ns = (int)which.size();
+  if (ns == 0) return ED_OK;
+  std::vector<TbSec> S(ns);
+  std::vector<TmSec> hs(ns);
+  std::vector<size_t> off(ns);
+  size_t per = 0;
+  for (int k = 0; k < ns; k++) {
+    ed_sector* s = secs[which[k]];
+    TbSec& b = S[k];
+    b.s = s;
+    b.dim = s->dim;
+    b.m = (int)std::min<int64_t>(ncv, b.dim);
+    b.Tm.assign((size_t)b.m * b.m, 0.0);
+    // (as one sector's sweep alone, at most kTrlanGridCap blocks: every block
+    // of the DGKS and local-only decisions sums all G partials; ~2,048 rows
+    // per block below that)
+    const int G = (int)std::max<int64_t>(
+        1, std::min<int64_t>((b.dim + kTmRowsPerBlock - 1) / kTmRowsPerBlock, kTrlanGridCap));
+    hs[k].G = G;
+    hs[k].Gh = (int)std::min<int64_t>((b.dim + 4 * kBlock - 1) / (4 * kBlock), 4096);  // 4 rows per thread
+    const int mcap = std::max(b.m, nev + 2);
+    off[k] = per;
+    // (every sub-array starts on a 16-byte boundary: the double2 ones need it)
+    per += (size_t)mcap * b.dim + 2 + (size_t)b.dim + 2 + 4 * (size_t)kTrlanMaxCols * G +
+           (3 * (size_t)G + 1) / 2 * 2 + 4 * kTrlanMaxCols + 2 + 144 + 2 * kTbScreenLen;
+    per = (per + 1) & ~(size_t)1;
+  }
+  const size_t nmail = (size_t)ns * kTbMail;
+  const size_t ytot = (size_t)ns * kTbMaxCols * kTbMaxCols;
+  const size_t ctab = (size_t)ns * sizeof(TmCyc) + 2 * (ns + 1) * sizeof(int) + 64;
+  const size_t bytes = (per + nmail + ytot) * sizeof(double) + (size_t)ns * sizeof(TmSec) + ctab;
+  char* dbase = nullptr;
+  HIPCK(hipMallocAsync((void**)&dbase, bytes, st));
+  struct Free {
+    char* p; hipStream_t s;
+    ~Free() { (void)hipFreeAsync(p, s); }
+  } free_guard{dbase, st};
+  double* const dsec = (double*)dbase;
+  double* const dmail = dsec + per;
+  TmSec* const dtab = (TmSec*)(dmail + nmail);
+  char* const dcyc = (char*)(dtab + ns);  // [TmCyc | boffG | boffH | pad | Y packed] of one cycle
+  // pinned: start column / mailboxes | cycle table
+  const int64_t maxdim = [&] { int64_t d = 0; for (auto& b : S) d = std::max(d, b.dim); return d; }();
+  const size_t hbytes = std::max<size_t>(maxdim, nmail) * sizeof(double) + ctab + ytot * sizeof(double);
+  char* hp = tb_pinned(hbytes);
+  if (!hp) return fail(ED_ERR_OOM, "pinned staging (multi-sector eigh)");
+  double* const hmail = (double*)hp;
+  char* const hcyc = hp + std::max<size_t>(maxdim, nmail) * sizeof(double);
+  for (int k = 0; k < ns; k++) {
+    TbSec& b = S[k];
+    const ed_sector* s = b.s;
+    TmSec& t = hs[k];
+    double* p = dsec + off[k];
+    const int mcap = std::max(b.m, nev + 2);
+    t.diag = (const double*)s->d_diag;
+    t.sptr = s->d_sptr;
+    t.words = s->d_words;
+    t.dict = (const double*)s->d_pdict;
+    t.dim = b.dim;
+    // (columns at stride dim, as the sweeps index them; each sub-array starts
+    // on a 16-byte boundary)
+    auto even = [](size_t q) { return (q + 1) & ~(size_t)1; };
+    t.Vb = p;
+    p += even((size_t)mcap * b.dim);
+    t.w = p;
+    p += even(b.dim);
+    t.part = (double2*)p;
+    p += 2 * (size_t)kTrlanMaxCols * t.G;
+    t.part2 = (double2*)p;
+    p += 2 * (size_t)kTrlanMaxCols * t.G;
+    t.npA = p;
+    t.npB = p + t.G;
+    t.npart = p + 2 * t.G;
+    p += (3 * (size_t)t.G + 1) / 2 * 2;
+    t.h = (double2*)p;
+    t.coef = (double2*)(p + 2 * kTrlanMaxCols);
+    p += 4 * kTrlanMaxCols;
+    t.lof = (int*)p;
+    p += 2;
+    t.alpha = p;
+    t.beta = p + 72;
+    p += 144;
+    t.pa = p;
+    t.pb = p + kTbScreenLen;
+    t.mail = dmail + (size_t)k * kTbMail;
+    b.task.m = b.m;
+    b.task.nev = nev;
+    b.task.locupd = !(s->opts & ED_OPT_TRLAN_FULLUPD);
+    b.task.op = kTbStart;
+    // V_0 = v0 / |v0| (host norm)
+    double* h0 = (double*)hp;
+    const int i = which[k];
+    double n2 = 0.0;
+    for (int64_t r = 0; r < b.dim; r++) {
+      h0[r] = (v0 && v0[i]) ? v0[i][r] : host_default_start(r);
+      n2 += h0[r] * h0[r];
+    }
+    if (!(n2 > 0.0)) {
+      b.state = 4;
+      continue;
+    }
+    const double inv = 1.0 / sqrt(n2);
+    for (int64_t r = 0; r < b.dim; r++) h0[r] *= inv;
+    HIPCK(hipMemcpyAsync(t.Vb, h0, b.dim * sizeof(double), hipMemcpyHostToDevice, st));
+    HIPCK(hipStreamSynchronize(st));  // (the staging buffer is reused for the next sector)
+  }
+  HIPCK(hipMemcpyAsync(dtab, hs.data(), ns * sizeof(TmSec), hipMemcpyHostToDevice, st));
+  std::vector<int> act;
+  const std::function<void(int)> process = [&](int a) {
+    const int k = act[a];
+    tb_advance(S[k], hmail + (size_t)k * kTbMail, nev, maxits[which[k]], tol);
+  };
+  TbPool pool(ns >= 8 ? kTbHostThreads : 0);
+  for (;;) {
+    act.clear();
+    for (int k = 0; k < ns; k++)
+      if (S[k].state <= 2) act.push_back(k);
+    if (act.empty()) break;
+    const int na = (int)act.size();
+    TmCyc* const hc = (TmCyc*)hcyc;
+    int* const hboG = (int*)(hc + na);
+    int* const hboH = hboG + (na + 1);
+    const size_t yoff = ((na * sizeof(TmCyc) + 2 * (na + 1) * sizeof(int)) + 63) / 64 * 64;
+    double* const hY = (double*)(hcyc + yoff);
+    const double* const dY = (const double*)(dcyc + yoff);
+    size_t yo = 0;
+    int steps = 0, maxm = 0, bG = 0, bH = 0;
+    bool rot = false;
+    for (int a = 0; a < na; a++) {
+      TbSec& b = S[act[a]];
+      const TrlTask& t = b.task;
+      TmCyc c{};
+      c.sec = act[a];
+      c.m = b.m;
+      c.nev = nev;
+      c.locupd = t.locupd;
+      c.scale_col = -1;
+      c.ldy = t.ldy;
+      c.nrot = b.ny > 0 ? t.nrot : 0;
+      if (t.op == kTbStart) {
+        c.phase = 0;
+        c.j0 = 0;
+      } else if (t.op == kTbRestart) {
+        c.phase = 0;
+        c.j0 = t.nrot;
+        c.scale_col = t.nrot;
+      } else {
+        c.phase = 1;
+        c.k0s = t.k0s;
+        c.k1 = t.k1;
+        c.sstart = (t.k0s == 0 && t.k1 > 0) ? 1 : 0;
+        c.hint = t.hint;
+        c.seed = t.seed;
+      }
+      if (b.ny > 0) {
+        std::copy(b.Z.begin(), b.Z.begin() + b.ny, hY + yo);
+        c.Y = dY + yo;
+        yo += b.ny;
+      }
+      rot = rot || c.nrot > 0 || c.scale_col >= 0;
+      steps = std::max(steps, c.phase == 0 ? c.m - c.j0 : c.k1 - c.k0s + c.sstart);
+      maxm = std::max(maxm, c.phase == 0 ? c.m : nev + 2);
+      hc[a] = c;
+      hboG[a] = bG;
+      hboH[a] = bH;
+      bG += hs[act[a]].G;
+      bH += hs[act[a]].Gh;
+    }
+    hboG[na] = bG;
+    hboH[na] = bH;
+    HIPCK(hipMemcpyAsync(dcyc, hcyc, yoff + yo * sizeof(double), hipMemcpyHostToDevice, st));
+    const TmCyc* dc = (const TmCyc*)dcyc;
+    const int* dboG = (const int*)(dc + na);
+    const int* dboH = dboG + (na + 1);
+    if (rot) hipLaunchKernelGGL(k_tm_rotate, dim3(bG), dim3(kBlock), 0, st, dtab, dc, dboG, na);
+    for (int q = 0; q < steps; q++) {
+      hipLaunchKernelGGL(k_tm_hxv, dim3(bH), dim3(kBlock), 0, st, dtab, dc, dboH, na, q);
+      for (int pass = 1; pass <= 3; pass++) {
+        if (maxm <= 24) hipLaunchKernelGGL(k_tm_cgs<24>, dim3(bG), dim3(kBlock), 0, st, dtab, dc, dboG, na, q, pass);
+        else hipLaunchKernelGGL(k_tm_cgs<32>, dim3(bG), dim3(kBlock), 0, st, dtab, dc, dboG, na, q, pass);
+        if (pass < 3)
+          hipLaunchKernelGGL(k_tm_fin, dim3(na * kTmFinBlocks), dim3(kBlock), 0, st, dtab, dc, na, q, pass);
+      }
+      hipLaunchKernelGGL(k_tm_coef, dim3(bG), dim3(kBlock), 0, st, dtab, dc, dboG, na, q);
+    }
+    hipLaunchKernelGGL(k_tm_mail, dim3(na), dim3(64), 0, st, dtab, dc);
+    HIPCK(hipGetLastError());
+    HIPCK(hipMemcpyAsync(hmail, dmail, nmail * sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPCK(hipStreamSynchronize(st));
+    pool.run(na, process);
+  }
+  for (int k = 0; k < ns; k++) {
+    TbSec& b = S[k];
+    const int i = which[k];
+    if (b.state != 3) {
+      fallback.push_back(i);
+      if (nhv) nhv[i] = b.nhv;
+      continue;
+    }
+    for (int e = 0; e < nev; e++) evals[(size_t)i * nev + e] = b.ev[e];
+    if (evecs && evecs[i])
+      HIPCK(hipMemcpyAsync(evecs[i], hs[k].Vb, (size_t)nev * b.dim * sizeof(double), hipMemcpyDefault, st));
     if (nconv) nconv[i] = b.conv;
     if (nhv) nhv[i] = b.nhv;
   }
@@ -4394,10 +4627,44 @@ int ed_sectors_eigh_batch(ed_sector* const* secs, int32_t n, int32_t nev, int32_
     if (secs[i]->hc) return fail(ED_ERR_ARG, "batched eigh: real vectors only (complex H needs vtype=1)");
     if (secs[i]->device != secs[0]->device) return fail(ED_ERR_ARG, "batched eigh: sectors on different devices");
   }
-  HIPCK(hipSetDevice(secs[0]->device));
+  const int dev = secs[0]->device;
+  HIPCK(hipSetDevice(dev));
   hipStream_t st = stream ? (hipStream_t)stream : secs[0]->stream;
-  std::vector<int> fb;
-  CK(tb_run(secs, n, nev, ncv, maxit, tol, v0, evals, evecs, nconv, nhv, st, fb));
+  // up to kTbWgMaxDim rows: one workgroup per sector (ed_trlbatch.hpp), on a
+  // second stream from a helper thread; larger: the lockstep multi-sector
+  // solve (ed_trlmulti.hpp) here; the rest one by one afterwards
+  std::vector<int> small, multi, fb, fb_small;
+  for (int i = 0; i < n; i++) {
+    if (secs[i]->dim <= kTbWgMaxDim && tb_eligible(secs[i], nev, ncv)) small.push_back(i);
+    else if (tm_eligible(secs[i], nev, ncv)) multi.push_back(i);
+    else fb.push_back(i);
+  }
+  int rc_small = ED_OK;
+  std::string err_small;
+  std::thread th;
+  hipStream_t st2 = nullptr;
+  if (!small.empty()) {
+    if (multi.empty()) {
+      rc_small = tb_run(secs, small, nev, ncv, maxit, tol, v0, evals, evecs, nconv, nhv, st, fb_small);
+    } else {
+      HIPCK(hipStreamCreateWithFlags(&st2, hipStreamNonBlocking));
+      th = std::thread([&] {
+        if (hipSetDevice(dev) != hipSuccess) rc_small = ED_ERR_HIP;
+        else rc_small = tb_run(secs, small, nev, ncv, maxit, tol, v0, evals, evecs, nconv, nhv, st2, fb_small);
+        if (rc_small != ED_OK) err_small = ed_err_slot();
+      });
+    }
+  }
+  int rc_multi = ED_OK;
+  for (size_t c0 = 0; c0 < multi.size() && rc_multi == ED_OK; c0 += kTmMaxEntries) {
+    const std::vector<int> part(multi.begin() + c0, multi.begin() + std::min(multi.size(), c0 + kTmMaxEntries));
+    rc_multi = tm_run(secs, part, nev, ncv, maxit, tol, v0, evals, evecs, nconv, nhv, st, fb);
+  }
+  if (th.joinable()) th.join();
+  if (st2) (void)hipStreamDestroy(st2);
+  if (rc_multi != ED_OK) return rc_multi;
+  if (rc_small != ED_OK) return fail(rc_small, err_small.empty() ? ed_err_slot() : err_small);
+  fb.insert(fb.end(), fb_small.begin(), fb_small.end());
   if (nbatched) *nbatched = n - (int)fb.size();
   for (int i : fb) {
     int32_t c = 0, h = 0;

@@ -293,6 +293,24 @@ __global__ void __launch_bounds__(kBlock) k_coef_scale(const double* __restrict_
     out[i] = scl(inv, x[i]);
 }
 
+// Global-address-space view of a pointer: loads through it are global_load,
+// not flat (a flat load also counts against lgkmcnt and waits behind LDS
+// traffic).  A no-op for kernel arguments; for pointers read from memory
+// (k_trl_batch's task table) the compiler cannot infer it by itself.
+template <class T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* gptr(T* p) {
+  return (__attribute__((address_space(1))) T*)p;
+}
+
+// (real vectors only: a class type such as double2 cannot be copied out of
+// an address-space-qualified lvalue; the complex callers pass kernel
+// arguments, which the compiler already knows to be global)
+template <bool VC, class T>
+__device__ __forceinline__ auto gptr_real(T* p) {
+  if constexpr (VC) return p;
+  else return gptr(p);
+}
+
 // N wave sums at once (N a multiple of 4): a transposing reduction — each
 // v_permlane32_swap / v_permlane16_swap step exchanges half of two values'
 // lanes so that one add halves the lanes of both, and the 16-lane rows that
@@ -349,15 +367,15 @@ __device__ __forceinline__ void wave_sum_multi(const double (&v)[N], double* out
 // The row loop, the per-thread accumulation order and the subtraction order
 // are those of k_vdot_part / k_vaxpy; the block sums use DPP wave sums and one
 // barrier for all 2*NC+1 partials.
+// (the body takes the launch's block count G and this block's index bx:
+// k_cgs passes gridDim.x / blockIdx.x, the lockstep multi-sector solve
+// (ed_trlmulti.hpp) its sector's own)
 template <bool VC, int NC>
-__global__ void __launch_bounds__(kBlock) k_cgs(const val_t<VC>* __restrict__ V, int ncol,
-                                                const double2* __restrict__ hin,
-                                                val_t<VC>* __restrict__ x, int64_t dim,
-                                                double2* __restrict__ part, double* __restrict__ npart,
-                                                const double2* __restrict__ pin = nullptr, int gin = 0,
-                                                double2* __restrict__ coef = nullptr, int add = 0,
-                                                const double* dgA = nullptr, const double* dgB = nullptr,
-                                                int* lof = nullptr, const double* locA = nullptr) {
+__device__ __forceinline__ void cgs_body(const val_t<VC>* __restrict__ V, int ncol, const double2* __restrict__ hin,
+                                         val_t<VC>* __restrict__ x, int64_t dim, double2* __restrict__ part,
+                                         double* __restrict__ npart, const double2* __restrict__ pin, int gin,
+                                         double2* __restrict__ coef, int add, const double* dgA, const double* dgB,
+                                         int* lof, const double* locA, int G, int bx) {
   constexpr int NW = kBlock / 64;
   constexpr int NR = (VC ? 2 * NC : NC) + 1;  // partial slots per wave
   constexpr int NRP = (NR + 3) / 4 * 4;       // padded for wave_sum_multi
@@ -365,8 +383,8 @@ __global__ void __launch_bounds__(kBlock) k_cgs(const val_t<VC>* __restrict__ V,
   __shared__ double red[NW][NR];
   // conditional second pass (dgA != null): when the DGKS test says the first
   // pass sufficed, the norm partials of w' (dgB) are this pass's result
-  if (dgA && dgks_skip(dgA, dgB, gridDim.x)) {
-    if (threadIdx.x == 0) npart[blockIdx.x] = dgB[blockIdx.x];
+  if (dgA && dgks_skip(dgA, dgB, G)) {
+    if (threadIdx.x == 0) npart[bx] = dgB[bx];
     return;
   }
   if (pin) {
@@ -385,7 +403,7 @@ __global__ void __launch_bounds__(kBlock) k_cgs(const val_t<VC>* __restrict__ V,
       if constexpr (VC) im = wave_sum_dpp(im);
       if (lane == 63) {
         hs[c] = make_double2(re, im);
-        if (coef && blockIdx.x == 0) coef[c] = add ? make_double2(coef[c].x + re, coef[c].y + im) : make_double2(re, im);
+        if (coef && bx == 0) coef[c] = add ? make_double2(coef[c].x + re, coef[c].y + im) : make_double2(re, im);
       }
     }
     __syncthreads();
@@ -399,13 +417,15 @@ __global__ void __launch_bounds__(kBlock) k_cgs(const val_t<VC>* __restrict__ V,
   // for the second pass (the columns it updates)
   int c0 = 0;
   if (locA) {
-    const bool lo = cgs_loc_only(hs, ncol, locA, pin ? gin : (int)gridDim.x);
-    if (blockIdx.x == 0 && threadIdx.x == 0) *lof = lo ? 1 : 0;
+    const bool lo = cgs_loc_only(hs, ncol, locA, pin ? gin : G);
+    if (bx == 0 && threadIdx.x == 0) *lof = lo ? 1 : 0;
     if (lo) c0 = ncol - 2;
   } else if (lof && *lof) {
     c0 = ncol - 2;
   }
   const bool upd = hin || pin;
+  const auto Vg = gptr_real<VC>(V);
+  const auto xg = gptr_real<VC>(x);
   double are[NC], aim[VC ? NC : 1];
 #pragma unroll
   for (int c = 0; c < NC; c++) {
@@ -413,11 +433,51 @@ __global__ void __launch_bounds__(kBlock) k_cgs(const val_t<VC>* __restrict__ V,
     if constexpr (VC) aim[c] = 0.0;
   }
   double n2 = 0.0;
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < dim; i += (int64_t)gridDim.x * kBlock) {
+  // local-only update on real vectors (the common shifted step): two columns
+  // and x per row, so the generic loop keeps only ~3 loads in flight per
+  // thread; here four rows' loads go out before the first is used (rows
+  // still processed in order: the sums are the generic loop's, bit for bit)
+  bool loc2 = false;
+  double al0 = 0.0, al1 = 0.0;
+  if constexpr (!VC) {
+    if (upd && c0 > 0 && c0 == ncol - 2) {
+      loc2 = true;
+      const auto V0 = Vg + (int64_t)c0 * dim;
+      const auto V1 = V0 + dim;
+      const double h0 = hs[c0].x, h1 = hs[c0 + 1].x;
+      const int64_t st = (int64_t)G * kBlock;
+      int64_t i = (int64_t)bx * kBlock + threadIdx.x;
+      auto row = [&](double a, double b, double xi, int64_t r) {
+        xi -= a * h0;
+        xi -= b * h1;
+        xg[r] = xi;
+        if (part) {
+          al0 += a * xi;
+          al1 += b * xi;
+        }
+        if (npart) n2 += xi * xi;
+      };
+      for (; i + 3 * st < dim; i += 4 * st) {
+        double a[4], b[4], xv[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          a[r] = V0[i + r * st];
+          b[r] = V1[i + r * st];
+          xv[r] = xg[i + r * st];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++) row(a[r], b[r], xv[r], i + r * st);
+      }
+      for (; i < dim; i += st) row(V0[i], V1[i], xg[i], i);
+#pragma unroll
+      for (int c = 0; c < NC; c++) are[c] = c == c0 ? al0 : c == c0 + 1 ? al1 : are[c];
+    }
+  }
+  for (int64_t i = (int64_t)bx * kBlock + threadIdx.x; !loc2 && i < dim; i += (int64_t)G * kBlock) {
     val_t<VC> v[NC];
 #pragma unroll
-    for (int c = 0; c < NC; c++) v[c] = (c >= c0 && c < ncol) ? V[(int64_t)c * dim + i] : vzero<val_t<VC>>();
-    auto xi = x[i];
+    for (int c = 0; c < NC; c++) v[c] = (c >= c0 && c < ncol) ? Vg[(int64_t)c * dim + i] : vzero<val_t<VC>>();
+    auto xi = xg[i];
     if (upd) {
 #pragma unroll
       for (int c = 0; c < NC; c++) {
@@ -429,7 +489,7 @@ __global__ void __launch_bounds__(kBlock) k_cgs(const val_t<VC>* __restrict__ V,
           xi -= v[c] * hs[c].x;
         }
       }
-      x[i] = xi;
+      xg[i] = xi;
     }
     if (part) {
 #pragma unroll
@@ -468,14 +528,27 @@ __global__ void __launch_bounds__(kBlock) k_cgs(const val_t<VC>* __restrict__ V,
       re = re + red[w][t];
       if constexpr (VC) im = im + red[w][NC + t];
     }
-    part[(int64_t)t * gridDim.x + blockIdx.x] = make_double2(re, im);
+    part[(int64_t)t * G + bx] = make_double2(re, im);
   }
   if (npart && t == kBlock - 1) {
     double r = 0.0;
 #pragma unroll
     for (int w = 0; w < NW; w++) r = r + red[w][NR - 1];
-    npart[blockIdx.x] = r;
+    npart[bx] = r;
   }
+}
+
+template <bool VC, int NC>
+__global__ void __launch_bounds__(kBlock) k_cgs(const val_t<VC>* __restrict__ V, int ncol,
+                                                const double2* __restrict__ hin,
+                                                val_t<VC>* __restrict__ x, int64_t dim,
+                                                double2* __restrict__ part, double* __restrict__ npart,
+                                                const double2* __restrict__ pin = nullptr, int gin = 0,
+                                                double2* __restrict__ coef = nullptr, int add = 0,
+                                                const double* dgA = nullptr, const double* dgB = nullptr,
+                                                int* lof = nullptr, const double* locA = nullptr) {
+  cgs_body<VC, NC>(V, ncol, hin, x, dim, part, npart, pin, gin, coef, add, dgA, dgB, lof, locA, (int)gridDim.x,
+                   (int)blockIdx.x);
 }
 
 // ------------------------------------------------------------------------
@@ -492,24 +565,6 @@ __global__ void __launch_bounds__(kBlock) k_cgs(const val_t<VC>* __restrict__ V,
 // EpiTrlLoc product).
 constexpr int kOrthSoloBlock = 512;
 constexpr int64_t kOrthSoloMaxDim = 2048;  // measured: dim 2,640 35 us per step solo, 31 multi-kernel
-
-// Global-address-space view of a pointer: loads through it are global_load,
-// not flat (a flat load also counts against lgkmcnt and waits behind LDS
-// traffic).  A no-op for kernel arguments; for pointers read from memory
-// (k_trl_batch's task table) the compiler cannot infer it by itself.
-template <class T>
-__device__ __forceinline__ __attribute__((address_space(1))) T* gptr(T* p) {
-  return (__attribute__((address_space(1))) T*)p;
-}
-
-// (real vectors only: a class type such as double2 cannot be copied out of
-// an address-space-qualified lvalue; the complex callers pass kernel
-// arguments, which the compiler already knows to be global)
-template <bool VC, class T>
-__device__ __forceinline__ auto gptr_real(T* p) {
-  if constexpr (VC) return p;
-  else return gptr(p);
-}
 
 template <bool VC, int NC, int RU = 1>
 __device__ __forceinline__ void orth_solo_body(const val_t<VC>* __restrict__ V, int ncol,

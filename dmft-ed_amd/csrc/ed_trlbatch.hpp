@@ -29,6 +29,10 @@ constexpr int kTbMail = 72;               // mailbox: alpha [0, 32) | beta [32, 
 constexpr int kTbScreenLen = 416;         // pa / pb entries (kScreenMaxSteps + the norm slot)
 constexpr int kTbScreenSlot = kTbScreenLen - 1;
 constexpr int64_t kTbMaxDim = 15360;      // v_j staged in LDS (120 KB)
+// ed_sectors_eigh_batch gives sectors up to this many rows one workgroup each
+// (a workgroup's step grows with the rows: ~13 us at 495-924 rows, ~180 us
+// at 14,520) and the larger ones to the lockstep solve
+constexpr int64_t kTbWgMaxDim = 2640;
 
 enum : int {
   kTbStart = 0,    // V_0 = w / |w| (w: the uploaded start vector), sweep [0, m)

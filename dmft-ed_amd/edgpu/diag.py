@@ -74,14 +74,16 @@ class DiagOptions:
     # budget runs when nothing else big is in flight.  0: no limit.
     cache_budget_mb: float = 0.0
     # thick-restart sectors of at most this many rows (real H, stored) are
-    # solved together by one host thread through ed_sectors_eigh_batch (one
-    # workgroup per sector, one launch per restart cycle for all of them)
-    # beside the other workers; 0: every sector alone (ed_sector_eigh).
-    # One workgroup's Krylov step grows ~linearly with the rows (configs[3]:
-    # ~13 us at 495-924 rows, ~200 us at 14,520, against ~20-30 us per step
-    # alone), so the batch takes the sectors up to 2,640 rows: configs[3]'s
-    # 36 of them in 28 ms instead of 141 ms one after the other
-    # (tools/batch_prof.py)
+    # solved together by one host thread through ed_sectors_eigh_batch beside
+    # the other workers; 0: every sector alone (ed_sector_eigh).  The library
+    # gives the sectors of up to 2,640 rows one workgroup each (one launch per
+    # restart cycle for all of them: configs[3]'s 36 in 17 ms instead of 138
+    # ms one after the other) and runs larger ones in lockstep (every kernel
+    # of a Krylov step carries that step of all of them).  Lockstep for all
+    # 136 configs[3] Lanczos sectors (batch_max_dim = 1 << 30) measured slower
+    # than the 8-worker farm (0.81-0.96 vs 0.65-0.73 s: its steps run at ~4
+    # TB/s while all sectors are in, then a long tail of few sectors; DESIGN.md
+    # §2), so the default stops at 2,640
     batch_max_dim: int = 2640
     # multi-rank farms: "dynamic" — every rank's workers take the next sector
     # (largest cost first) from one global counter in the process group's
@@ -238,19 +240,30 @@ def solve_batch(cfg: EDConfig, secs: List[SectorId], opt: DiagOptions, device: i
         ncv = min(max(nblock, neigen + 1), 64, sec.dim)
         groups.setdefault((neigen, ncv), []).append(k)
     out: List[Optional[SectorResult]] = [None] * len(secs)
-    for (neigen, ncv), ks in groups.items():
-        maxit = [max(lanczos_params(secs[k].dim, opt)[1], 10) for k in ks]
-        hs: List[Sector] = []
-        try:
-            for k in ks:
-                hs.append(Sector(cfg, secs[k].q1, secs[k].q2, stored=True, real=True, device=device,
-                                 options=opt.kernel_options, stream=st))
-            res, _ = eigh_batch(hs, neigen, ncv, maxit, opt.lanc_tolerance,
-                                [_start_vector(h.dim, False) for h in hs], vectors=opt.keep_vectors,
-                                on_device=opt.device_vectors, stream=st)
-        finally:
-            for h in hs:
-                h.close()
+    from concurrent.futures import ThreadPoolExecutor
+
+    def build(k):   # on the pool thread's own stream (the build synchronises it)
+        return Sector(cfg, secs[k].q1, secs[k].q2, stored=True, real=True, device=device,
+                      options=opt.kernel_options, stream=_worker_stream(opt, device))
+
+    # the sector builds (a few ms of small launches and host syncs each) on
+    # opt.workers threads, then one batch call, then the frees in parallel
+    with ThreadPoolExecutor(max_workers=max(1, opt.workers)) as ex:
+        for (neigen, ncv), ks in groups.items():
+            maxit = [max(lanczos_params(secs[k].dim, opt)[1], 10) for k in ks]
+            futs = [ex.submit(build, k) for k in ks]
+            hs: List[Sector] = []
+            try:
+                for f in futs:
+                    hs.append(f.result())
+                res, _ = eigh_batch(hs, neigen, ncv, maxit, opt.lanc_tolerance,
+                                    [_start_vector(h.dim, False) for h in hs], vectors=opt.keep_vectors,
+                                    on_device=opt.device_vectors, stream=st)
+            finally:
+                for f in futs:
+                    if f.exception() is None and f.result() not in hs:
+                        hs.append(f.result())
+                list(ex.map(lambda h: h.close(), hs))
         for k, (w, v, _, _) in zip(ks, res):
             sec = secs[k]
             out[k] = SectorResult(sec.isector, (sec.q1, sec.q2), sec.dim, w, neigen,
