@@ -1,11 +1,13 @@
-"""Batched small-sector thick-restart Lanczos (ed_sectors_eigh_batch) against
-the per-sector solver, the dense configs[3] fixtures and the adversarial
+"""Batched thick-restart Lanczos (ed_sectors_eigh_batch) against the
+per-sector solver, the dense configs[3] fixtures and the adversarial
 degeneracy fixture.
 
 The batch runs trlan_run's algorithm (ED_DIAG.f90:145-167's sp_eigh
-replacement) for many sectors at once, one workgroup per sector and one
-launch per restart cycle; sectors it cannot finish fall back to the
-per-sector path, so the results must meet the same 1e-10 bar either way.
+replacement) for many sectors at once: one workgroup per sector and one
+launch per restart cycle up to 2,640 rows (ed_trlbatch.hpp), every step of
+the larger ones in shared launches (ed_trlmulti.hpp); sectors it cannot
+finish fall back to the per-sector path, so the results must meet the same
+1e-10 bar either way.
 """
 import json
 import os
@@ -28,11 +30,13 @@ def _small_sectors(cfg, opt, lo=257, hi=15360):
 
 @pytest.mark.parametrize("bath", ["random", "flat"])
 def test_batch_matches_fixture_and_single(bath):
-    """Every batchable configs[3] sector (dims 495-14,520) solved in one
-    batch: eigenvalues within 1e-10 of |E0| of the dense fixture, and of the
-    per-sector solver (ed_sector_eigh); the random bath finishes (nearly)
-    every sector inside the batch, the flat bath sends the sectors with a
-    missed degenerate copy to the per-sector probe."""
+    """Every configs[3] Lanczos sector of 495-14,520 rows in one batch call
+    (up to 2,640 rows one workgroup each, the larger ones in lockstep):
+    eigenvalues within 1e-10 of |E0| of the dense fixture, and of the
+    per-sector solver (ed_sector_eigh); eigenvectors orthonormal with H v =
+    w v; the random bath finishes (nearly) every sector inside the batch, the
+    flat bath sends the sectors with a missed degenerate copy to the
+    per-sector probe."""
     from edgpu.diag import DiagOptions, _start_vector, lanczos_params
     from edgpu.hamiltonian import Sector, eigh_batch
     from golden.golden_configs import c4_config
