@@ -78,13 +78,13 @@ class DiagOptions:
     # the other workers; 0: every sector alone (ed_sector_eigh).  The library
     # gives the sectors of up to 2,640 rows one workgroup each (one launch per
     # restart cycle for all of them: configs[3]'s 36 in 17 ms instead of 138
-    # ms one after the other) and runs larger ones in lockstep (every kernel
-    # of a Krylov step carries that step of all of them).  Lockstep for all
-    # 136 configs[3] Lanczos sectors (batch_max_dim = 1 << 30) measured slower
-    # than the 8-worker farm (0.81-0.96 vs 0.65-0.73 s: its steps run at ~4
-    # TB/s while all sectors are in, then a long tail of few sectors; DESIGN.md
-    # §2), so the default stops at 2,640
-    batch_max_dim: int = 2640
+    # ms one after the other) and runs the larger ones in lockstep (every
+    # kernel of a Krylov step carries that step of all of them).  configs[3]
+    # farm, one box, alternating runs (gpurun_out r6bm2): cap
+    # 2,640 median 0.652 s, 33,000 0.638 s, 60,000 0.594 s (the 52 sectors of
+    # 4,356-52,272 rows in lockstep beside the workers' large sectors); every
+    # sector in lockstep 0.81-0.96 s (its tail of few sectors is serial)
+    batch_max_dim: int = 60000
     # multi-rank farms: "dynamic" — every rank's workers take the next sector
     # (largest cost first) from one global counter in the process group's
     # key-value store, so the ranks finish together whatever the cost
