@@ -266,16 +266,18 @@ int ed_sector_lanc_mode(ed_sector* s, int32_t vtype, int32_t path);
  * nconv: converged pairs; nhv: H·v products used.  ncv <= 64. */
 int ed_sector_eigh(ed_sector* s, int32_t vtype, int32_t nev, int32_t ncv, int32_t maxit, double tol,
                    const void* v0, double* evals, void* evecs, int32_t* nconv, int32_t* nhv);
-/* ed_sector_eigh (real vectors) for n sectors at once, the same algorithm
- * and options per sector: the restart cycles and degeneracy-screen chunks of
- * every small stored sector run as one workgroup each in a shared launch
- * (one launch and one host round trip per cycle for all of them); sectors
- * the batch cannot take or finish are solved by ed_sector_eigh's path
- * afterwards.  The farm's replacement of ED_DIAG.f90:71-249's loop over the
- * small sectors' sp_eigh calls.  maxit[i]: sector i's Nitermax; v0[i] (host,
- * or NULL / v0 NULL: the default start), evals[i*nev + k], evecs[i] (host or device, dim x nev, or NULL),
- * nconv[i], nhv[i]; *nbatched: sectors finished inside the batch (or NULL);
- * stream: the launches' stream (NULL: the first sector's). */
+/* ed_sector_eigh (real vectors) for n stored sectors at once, the same
+ * algorithm and options per sector: sectors of up to 2,640 rows run their
+ * restart cycles and degeneracy-screen chunks as one workgroup each in a
+ * shared launch (one launch and one host round trip per cycle for all of
+ * them); larger ones run in lockstep, every kernel of a Krylov step carrying
+ * that step of all of them; sectors the batch cannot take or finish are
+ * solved by ed_sector_eigh's path afterwards.  The farm's replacement of
+ * ED_DIAG.f90:71-249's loop over the sectors' sp_eigh calls.  maxit[i]:
+ * sector i's Nitermax; v0[i] (host, or NULL / v0 NULL: the default start),
+ * evals[i*nev + k], evecs[i] (host or device, dim x nev, or NULL), nconv[i],
+ * nhv[i]; *nbatched: sectors finished inside the batch (or NULL); stream:
+ * the launches' stream (NULL: the first sector's). */
 int ed_sectors_eigh_batch(ed_sector* const* secs, int32_t n, int32_t nev, int32_t ncv, const int32_t* maxit,
                           double tol, const double* const* v0, double* evals, void* const* evecs,
                           int32_t* nconv, int32_t* nhv, int32_t* nbatched, void* stream);
