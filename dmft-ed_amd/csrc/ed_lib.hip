@@ -4615,7 +4615,7 @@ int ed_sector_lanc_eigh(ed_sector* s, int32_t vtype, const void* v0, int32_t nit
 
 int ed_sectors_eigh_batch(ed_sector* const* secs, int32_t n, int32_t nev, int32_t ncv, const int32_t* maxit,
                           double tol, const double* const* v0, double* evals, void* const* evecs, int32_t* nconv,
-                          int32_t* nhv, int32_t* nbatched, void* stream) {
+                          int32_t* nhv, int32_t* nbatched, int32_t flags, void* stream) {
   if (!secs || n < 0 || !evals || !maxit) return fail(ED_ERR_ARG, "bad args");
   for (int i = 0; i < n; i++)
     if (maxit[i] < 1) return fail(ED_ERR_ARG, "maxit < 1");
@@ -4666,6 +4666,11 @@ int ed_sectors_eigh_batch(ed_sector* const* secs, int32_t n, int32_t nev, int32_
   if (rc_small != ED_OK) return fail(rc_small, err_small.empty() ? ed_err_slot() : err_small);
   fb.insert(fb.end(), fb_small.begin(), fb_small.end());
   if (nbatched) *nbatched = n - (int)fb.size();
+  if (flags & ED_BATCH_NO_FALLBACK) {  // the caller solves them (nconv -1)
+    for (int i : fb)
+      if (nconv) nconv[i] = -1;
+    return ED_OK;
+  }
   for (int i : fb) {
     int32_t c = 0, h = 0;
     CK(trlan_run<false>(secs[i], nev, ncv, maxit[i], tol, v0 ? v0[i] : nullptr, evals + (size_t)i * nev,

@@ -15,6 +15,7 @@ LIB_PATH = os.path.join(_PKG_ROOT, "libedgpu.so")
 ED_STORED, ED_DIRECT, ED_REAL = 0x1, 0x2, 0x4
 ED_NO_PACK, ED_KRON2_OFF, ED_KRON2_ON, ED_NO_SPLIT, ED_SPLIT_ON = 0x10, 0x20, 0x40, 0x80, 0x100
 ED_FUSED_ON, ED_NO_FUSED = 0x200, 0x400
+ED_BATCH_NO_FALLBACK = 0x1   # ed_sectors_eigh_batch flags
 # kernel alternatives of a built sector (ed_sector_set_options, include/ed_gpu.h)
 OPTIONS = {
     "no_persist": 0x001, "persist_stored": 0x002, "no_preg": 0x004, "no_pkron": 0x008,
@@ -50,7 +51,7 @@ SIGNATURES = {
     "ed_sector_kron_rows": ([_P, _i32, _i64, _i64, _P, _P, _P], ctypes.c_int),
     "ed_sector_kron_cols": ([_P, _i32, _i64, _i64, _P, _P, _i32, _P], ctypes.c_int),
     "ed_sector_eigh": ([_P, _i32, _i32, _i32, _i32, _f64, _P, _P, _P, _P, _P], ctypes.c_int),
-    "ed_sectors_eigh_batch": ([_P, _i32, _i32, _i32, _P, _f64, _P, _P, _P, _P, _P, _P, _P], ctypes.c_int),
+    "ed_sectors_eigh_batch": ([_P, _i32, _i32, _i32, _P, _f64, _P, _P, _P, _P, _P, _P, _i32, _P], ctypes.c_int),
     "ed_sector_sell_view": ([_P, _P], ctypes.c_int),
     "ed_sector_apply_op": ([_P, _P, _i32, _i32, _i32, _P, _P, _P], ctypes.c_int),
     "ed_sector_apply_op_acc": ([_P, _P, _i32, _i32, _f64, _f64, _i32, _P, _P, _P], ctypes.c_int),

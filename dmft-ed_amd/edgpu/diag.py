@@ -258,16 +258,23 @@ def solve_batch(cfg: EDConfig, secs: List[SectorId], opt: DiagOptions, device: i
                     hs.append(f.result())
                 res, _ = eigh_batch(hs, neigen, ncv, maxit, opt.lanc_tolerance,
                                     [_start_vector(h.dim, False) for h in hs], vectors=opt.keep_vectors,
-                                    on_device=opt.device_vectors, stream=st)
+                                    on_device=opt.device_vectors, stream=st, fallback=False)
             finally:
                 for f in futs:
                     if f.exception() is None and f.result() not in hs:
                         hs.append(f.result())
                 list(ex.map(lambda h: h.close(), hs))
-        for k, (w, v, _, _) in zip(ks, res):
-            sec = secs[k]
-            out[k] = SectorResult(sec.isector, (sec.q1, sec.q2), sec.dim, w, neigen,
-                                  v if opt.keep_vectors else None, "arpack")
+            # the sectors the batch left (a missed degenerate copy to probe, an
+            # invariant subspace, ...): the per-sector solve on the pool's threads
+            redo = [k for k, r in zip(ks, res) if r[2] < 0]
+            again = dict(zip(redo, ex.map(lambda k: solve_sector(cfg, secs[k], opt, device), redo)))
+            for k, (w, v, _, _) in zip(ks, res):
+                if k in again:
+                    out[k] = again[k]
+                    continue
+                sec = secs[k]
+                out[k] = SectorResult(sec.isector, (sec.q1, sec.q2), sec.dim, w, neigen,
+                                      v if opt.keep_vectors else None, "arpack")
     return out
 
 

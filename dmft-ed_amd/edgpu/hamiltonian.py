@@ -275,12 +275,15 @@ class Sector:
 
 
 def eigh_batch(sectors, neigen: int = 6, ncv: int = 23, maxit=512, tol: float = 1e-12,
-               v0s=None, vectors: bool = True, on_device: bool = False, stream=None):
+               v0s=None, vectors: bool = True, on_device: bool = False, stream=None,
+               fallback: bool = True):
     """Sector.eigh (real vectors) for many sectors of one GPU at once
     (ed_sectors_eigh_batch): the small stored sectors' restart cycles share
     launches.  Returns one (eigenvalues, vectors (dim, neigen) or None, nconv,
     H·v products) per sector, and the number finished inside the batch.
-    maxit: one Nitermax for all, or one per sector."""
+    maxit: one Nitermax for all, or one per sector.  fallback=False: sectors
+    the batch cannot take or finish come back with nconv == -1 (and no
+    eigenvalues) for the caller to solve, instead of one after the other here."""
     n = len(sectors)
     if n == 0:
         return [], 0
@@ -307,7 +310,8 @@ def eigh_batch(sectors, neigen: int = 6, ncv: int = 23, maxit=512, tol: float = 
     nb = ctypes.c_int32()
     mx = np.ascontiguousarray(np.broadcast_to(np.asarray(maxit, dtype=np.int32), (n,)))
     check(lib.ed_sectors_eigh_batch(hs, n, neigen, ncv, _ptr(mx), tol, v0p, _ptr(ev), ep, _ptr(nconv), _ptr(nhv),
-                                    ctypes.byref(nb), _stream_ptr(stream)), "ed_sectors_eigh_batch")
+                                    ctypes.byref(nb), 0 if fallback else _lib.ED_BATCH_NO_FALLBACK,
+                                    _stream_ptr(stream)), "ed_sectors_eigh_batch")
     res = [(ev[i].copy(), outs[i].T if outs[i] is not None else None, int(nconv[i]), int(nhv[i]))
            for i in range(n)]
     return res, int(nb.value)

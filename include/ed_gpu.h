@@ -276,11 +276,14 @@ int ed_sector_eigh(ed_sector* s, int32_t vtype, int32_t nev, int32_t ncv, int32_
  * ED_DIAG.f90:71-249's loop over the sectors' sp_eigh calls.  maxit[i]:
  * sector i's Nitermax; v0[i] (host, or NULL / v0 NULL: the default start),
  * evals[i*nev + k], evecs[i] (host or device, dim x nev, or NULL), nconv[i],
- * nhv[i]; *nbatched: sectors finished inside the batch (or NULL); stream:
- * the launches' stream (NULL: the first sector's). */
+ * nhv[i]; *nbatched: sectors finished inside the batch (or NULL); flags:
+ * ED_BATCH_NO_FALLBACK leaves the others to the caller (their nconv[i] = -1,
+ * e.g. to solve them on several threads); stream: the launches' stream
+ * (NULL: the first sector's). */
+#define ED_BATCH_NO_FALLBACK 0x1
 int ed_sectors_eigh_batch(ed_sector* const* secs, int32_t n, int32_t nev, int32_t ncv, const int32_t* maxit,
                           double tol, const double* const* v0, double* evals, void* const* evecs,
-                          int32_t* nconv, int32_t* nhv, int32_t* nbatched, void* stream);
+                          int32_t* nconv, int32_t* nhv, int32_t* nbatched, int32_t flags, void* stream);
 /* Fixed-length Lanczos on device pointers for benchmarking: runs exactly
  * `niter` iterations (no convergence test) from device vector v0 and writes
  * alfa/beta (host).  Returns the elapsed device time in ms in *ms (or NULL). */
