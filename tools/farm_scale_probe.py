@@ -29,10 +29,12 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--out", default="gpurun_out/farm_scale.json")
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--ranks", default="1,2,4,8")
+ap.add_argument("--batch-max-dim", type=int, default=None, help="DiagOptions.batch_max_dim (default: the library's)")
+ap.add_argument("--no-solo", action="store_true", help="skip the per-sector solo times")
 args = ap.parse_args()
 
 cfg = c4_config("random")
-opt = DiagOptions()
+opt = DiagOptions() if args.batch_max_dim is None else DiagOptions(batch_max_dim=args.batch_max_dim)
 secs = diag_sectors(cfg)
 costs = [sector_cost(cfg, s, opt) for s in secs]
 
@@ -54,19 +56,23 @@ def run(part):
 run(list(range(len(secs))))  # warm-up: code objects, allocator pools
 # every sector alone (one thread), to compare with the cost model
 solo = []
-for i, s in enumerate(secs):
+for i, s in enumerate([] if args.no_solo else secs):
     torch.cuda.synchronize()
     t = time.perf_counter()
     r = solve_sector(cfg, s, opt)
     torch.cuda.synchronize()
     solo.append(time.perf_counter() - t)
     del r
-print(f"solo sum {sum(solo):.3f}s, largest {max(solo):.4f}s", flush=True)
+if solo:
+    print(f"solo sum {sum(solo):.3f}s, largest {max(solo):.4f}s", flush=True)
+else:
+    solo = [0.0] * len(secs)
 
 res = {"workload": "configs[3] Norb=2 Nbath=5 random bath, 169 sectors, Neigen=6 ncv=23 tol 1e-12",
        "method": "each LPT part of N ranks timed alone on one MI355X with the farm's worker threads; "
                  "projected N-GPU wall = max over parts (the eigenvalue all_gather is KB and not included)",
-       "workers": opt.workers, "solo_sum_s": round(sum(solo), 4), "ranks": {}}
+       "workers": opt.workers, "batch_max_dim": opt.batch_max_dim, "solo_sum_s": round(sum(solo), 4),
+       "ranks": {}}
 base = None
 for n in [int(x) for x in args.ranks.split(",")]:
     parts = lpt_partition(costs, n)
