@@ -2535,8 +2535,9 @@ struct Trlan {
   // grids up to this fold the coefficient reduction into the next CGS pass
   // (every block re-reads G x ncol partials; 0 with ED_OPT_TRLAN_NOFOLD: A/B)
   // (round 6, in the 8-worker farm: folding at 256 or 512 blocks, with the
-  // sweep grid at 512 or 256, within noise of this, gpurun_out r6k)
-  int kFinFoldG = 128;
+  // sweep grid at 512 or 256, within noise of 128, gpurun_out r6k; at the
+  // closing build 256 with the 256-block grid: see kTrlanGridCap)
+  int kFinFoldG = 256;
   bool graphs_on = true;  // false (ED_OPT_NO_GRAPH): sweeps launched directly
   bool solo = true;       // false (ED_OPT_TRLAN_NOSOLO): multi-kernel CGS on small sectors too (A/B)
   bool locupd = true;     // false (ED_OPT_TRLAN_FULLUPD): full CGS update every step (A/B)
@@ -2752,8 +2753,12 @@ static double* trlan_pinned() {
 // blocks of the O(dim) Krylov sweeps
 // (1024 until round 4: 512 measured 13 % faster per large-sector solve,
 // tools/trlan_ab.py --grid; round 6 in the 8-worker farm: 128 and 256 within
-// noise of 512, gpurun_out r6j)
-static constexpr int kTrlanGridCap = 512;
+// noise of 512, gpurun_out r6j; at the closing build — the medium sectors in
+// the lockstep batch, the local-only CGS pass — 256 with the coefficient
+// fold at 256 blocks (5 launches per step instead of 7): farm median 0.618
+// -> 0.567 s over 6 reps each, lone (6,6) 82-84 -> 85 us per step, 128:
+// 0.588 s, gpurun_out r6gc, profiles/r6/grid_cap_ab.json)
+static constexpr int kTrlanGridCap = 256;
 // One thick-restart Lanczos solve on the columns [k0, m) of the basis; the
 // columns [0, k0) are locked (deflation: every new vector is orthogonalised
 // against them, their coefficients are not part of the projected matrix).
