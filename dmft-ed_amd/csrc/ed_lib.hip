@@ -2759,6 +2759,12 @@ static double* trlan_pinned() {
 // -> 0.567 s over 6 reps each, lone (6,6) 82-84 -> 85 us per step, 128:
 // 0.588 s, gpurun_out r6gc, profiles/r6/grid_cap_ab.json)
 static constexpr int kTrlanGridCap = 256;
+// ... except the largest sectors (configs[3]'s nine of 627,264-853,776 rows),
+// whose lone solve is the critical path of a many-GPU farm: 512 blocks, the
+// coefficient sums in their own launches (lone (6,6) 86.5-87.3 -> 83.6-84.2
+// us per step, farm median 0.578 -> 0.570 s, gpurun_out r6big,
+// profiles/r6/grid_big_ab.json)
+static constexpr int64_t kTrlanBigDim = 600000;
 // One thick-restart Lanczos solve on the columns [k0, m) of the basis; the
 // columns [0, k0) are locked (deflation: every new vector is orthogonalised
 // against them, their coefficients are not part of the projected matrix).
@@ -2989,7 +2995,7 @@ static int trlan_run(ed_sector* s, int nev, int ncv, int maxit, double tol, cons
   T.path = resolve_path(s, -1);
   T.st = s->stream;
   T.dim = s->dim;
-  T.G = (int)std::min<int64_t>(grid_for(s->dim), kTrlanGridCap);
+  T.G = (int)std::min<int64_t>(grid_for(s->dim), s->dim > kTrlanBigDim ? 2 * kTrlanGridCap : kTrlanGridCap);
   T.hp = trlan_pinned();
   if (!T.hp) return fail(ED_ERR_OOM, "pinned host staging buffer");
   T.fused = !(s->opts & ED_OPT_TRLAN_UNFUSED);
