@@ -87,12 +87,18 @@ for n in [int(x) for x in args.ranks.split(",")]:
                        "solo_load_s": [round(m, 4) for m in measured]}
     print(f"N={n}: wall {wall:.4f}s parts {[round(t, 3) for t in times]} speedup {base / wall:.2f}", flush=True)
 
-# largest sectors: cost model vs measured
+# largest sectors: cost model vs measured (skipped with --no-solo)
+if args.no_solo:
+    res.pop("solo_sum_s")
+    for v in res["ranks"].values():
+        v.pop("solo_load_s")
 res["solo"] = [{"sector": [s.q1, s.q2], "dim": s.dim, "solo_s": round(solo[i], 5), "cost_model": costs[i]}
                for i, s in enumerate(secs)]
 top = sorted(range(len(secs)), key=lambda i: -solo[i])[:12]
 res["largest"] = [{"sector": [secs[i].q1, secs[i].q2], "dim": secs[i].dim, "solo_s": round(solo[i], 4),
                    "cost_model": costs[i]} for i in top]
+if args.no_solo:
+    del res["solo"], res["largest"]
 os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
 with open(args.out, "w") as f:
     json.dump(res, f, indent=1)
